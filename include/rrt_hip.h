@@ -1,0 +1,231 @@
+/*
+ * rrt_hip.h — C-ABI of librrt_hip.so, the MI355X (gfx950) path-tracing backend.
+ *
+ * This is the drop-in boundary for the reference's GPU-backend slot:
+ *   src/main.rs:58-71            `--backend cuda` -> cuda::render_in_one_weekend()
+ *   src/cuda/mod.rs:337-439      imp::render(camera, &spheres, &materials) -> Result<(), String>
+ *   src/gpu/mod.rs:124-301       build_in_one_weekend_scene() -> (CameraUniform, Vec<SphereGpu>, Vec<MaterialGpu>)
+ *   src/render_io.rs:3-31        write_ppm_from_accum(w, h, &[f32] RGBA accum, spp)
+ *
+ * Plain C types only (no torch / HIP types in signatures). Every entry point returns
+ * 0 on success or a negative RRT_E* code; rrt_hip_last_error() then holds the message
+ * (thread-local, valid until the next call on that thread) — the Rust shim maps a
+ * non-zero return to Err(rrt_hip_last_error()) exactly like cuda/mod.rs maps its
+ * `map_err(|e| format!(...))` strings.
+ *
+ * Struct layouts are byte-identical to the reference's #[repr(C)] Pod structs, so the
+ * Rust side passes `bytemuck::cast_slice` views of its existing vectors unchanged.
+ */
+#ifndef RRT_HIP_H
+#define RRT_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RRT_ABI_VERSION 1u
+
+/* ---- scene ABI (== src/gpu/mod.rs:13-42) ------------------------------------------ */
+
+/* == CameraUniform (gpu/mod.rs:15-25), 144 B.
+ * params_f = [defocus_radius, image_width, image_height, samples_per_pixel]
+ * params_u = [max_depth, sample_seed, n_spheres, background_mode(0 sky, 1 `background`)] */
+typedef struct RrtCamera {
+    float origin[4];
+    float pixel00[4];
+    float pixel_delta_u[4];
+    float pixel_delta_v[4];
+    float u[4];
+    float v[4];
+    float background[4];
+    float params_f[4];
+    uint32_t params_u[4];
+} RrtCamera;
+
+/* == SphereGpu (gpu/mod.rs:29-33), 32 B. */
+typedef struct RrtSphere {
+    float center_radius[4];
+    uint32_t material_index;
+    uint32_t _pad[3];
+} RrtSphere;
+
+/* == MaterialGpu (gpu/mod.rs:37-42), 32 B. kind 0..2 are the reference's; 3 and 4 extend
+ * the ABI for the textured-earth config (the_next_week/material.rs:27-53,116-135):
+ *   3 = textured Lambertian, _pad[0] = texture index into the RrtTexture array
+ *   4 = diffuse light, albedo_fuzz.xyz = emitted radiance */
+typedef struct RrtMaterial {
+    float albedo_fuzz[4];
+    uint32_t kind;
+    float ref_idx;
+    uint32_t _pad[2];
+} RrtMaterial;
+
+enum {
+    RRT_MAT_LAMBERTIAN = 0,
+    RRT_MAT_METAL = 1,
+    RRT_MAT_DIELECTRIC = 2,
+    RRT_MAT_TEXTURED_LAMBERTIAN = 3,
+    RRT_MAT_DIFFUSE_LIGHT = 4
+};
+
+/* Image texture, RGB8 row-major (rtw_image.rs:57-67 `to_rgb8().into_raw()`). Borrowed. */
+typedef struct RrtTexture {
+    const uint8_t *rgb8;
+    int32_t width;
+    int32_t height;
+} RrtTexture;
+
+/* == config::RenderOverrides (config.rs:1-14): has_* = Some(..). */
+typedef struct RrtOverrides {
+    int32_t has_aspect_ratio;   double aspect_ratio;
+    int32_t has_image_width;    int32_t image_width;
+    int32_t has_samples_per_pixel; int32_t samples_per_pixel;
+    int32_t has_max_depth;      int32_t max_depth;
+    int32_t has_vfov;           double vfov;
+    int32_t has_lookfrom;       double lookfrom[3];
+    int32_t has_lookat;         double lookat[3];
+    int32_t has_vup;            double vup[3];
+    int32_t has_defocus_angle;  double defocus_angle;
+    int32_t has_focus_dist;     double focus_dist;
+    int32_t has_background;     double background[3];
+} RrtOverrides;
+
+/* ---- flags ------------------------------------------------------------------------ */
+/* Book-2 camera: each camera ray draws a `time` sample after the jitter/disk draws
+ * (the_next_week/camera.rs:160). Required for bit-parity with the book-2 oracle. */
+#define RRT_FLAG_RAY_TIME 0x1u
+/* Suppress the stderr progress lines (cuda/mod.rs:426-431 style). */
+#define RRT_FLAG_QUIET 0x2u
+
+/* ---- error codes ------------------------------------------------------------------ */
+#define RRT_OK 0
+#define RRT_E_INVALID (-1)
+#define RRT_E_HIP (-2)
+#define RRT_E_NOMEM (-3)
+#define RRT_E_NODEV (-4)
+#define RRT_E_IO (-5)
+
+/* ---- one-shot drop-in entry (replaces cuda::imp::render, cuda/mod.rs:342-439) ----------
+ * Renders total_spp samples per pixel of the scene on n_gpus devices (row-interleaved
+ * bands, one host thread per device), writes RGBA float accum into caller-owned
+ * accum_out[W*H*4] (W,H = params_f[1], params_f[2]); accum_out[4i+3] = sample count.
+ * total_spp == 0 means params_f[3] (cuda/mod.rs:384). BVH is built inside. */
+int32_t rrt_hip_render(const RrtCamera *cam,
+                       const RrtSphere *spheres, uint32_t n_spheres,
+                       const RrtMaterial *materials, uint32_t n_materials,
+                       const RrtTexture *textures, uint32_t n_textures,
+                       uint32_t total_spp, uint32_t n_gpus, uint32_t flags,
+                       float *accum_out);
+
+/* Thread-local message for the last failing call on this thread ("" if none). */
+const char *rrt_hip_last_error(void);
+uint32_t rrt_hip_abi_version(void);
+
+/* ---- device-resident API (bench / multi-rank hosts) --------------------------------- */
+typedef struct RrtScene RrtScene;
+
+/* A tile = the rows this rank owns (row bands of `band_rows`, band b -> rank b % n_ranks)
+ * crossed with the sample range [sample_begin, sample_end). */
+typedef struct RrtTile {
+    uint32_t band_rows;
+    uint32_t rank;
+    uint32_t n_ranks;
+    uint32_t sample_begin;
+    uint32_t sample_end;
+} RrtTile;
+
+/* Counters accumulated by every render launch on the scene since the last reset.
+ * rays = closest-hit queries (camera + scattered: one world.hit, camera.rs:187).
+ * node_visits / sphere_tests are only filled by rrt_scene_count_work (instrumented). */
+typedef struct RrtCounters {
+    uint64_t rays;
+    uint64_t paths;
+    uint64_t node_visits;
+    uint64_t box_tests;
+    uint64_t sphere_tests;
+} RrtCounters;
+
+/* Uploads the scene to `device`, builds the BVH (SAH, bvh.rs:21-156 criterion) on the host. */
+int32_t rrt_scene_create(const RrtCamera *cam,
+                         const RrtSphere *spheres, uint32_t n_spheres,
+                         const RrtMaterial *materials, uint32_t n_materials,
+                         const RrtTexture *textures, uint32_t n_textures,
+                         uint32_t flags, int32_t device, RrtScene **out);
+int32_t rrt_scene_destroy(RrtScene *scene);
+
+/* Number of image rows `tile` owns (the tile's accum is rows*W float4). */
+int32_t rrt_tile_rows(const RrtScene *scene, const RrtTile *tile, uint32_t *rows_out);
+/* Global image row of the tile's local row `local_row`. */
+int32_t rrt_tile_row_index(const RrtScene *scene, const RrtTile *tile, uint32_t local_row, uint32_t *row_out);
+
+/* Enqueue the render of `tile` on `stream` (a hipStream_t, NULL = default stream).
+ * d_accum: device pointer to rows*W*4 floats, OVERWRITTEN with this tile's sums
+ * (RGB sums over the tile's samples, w = sample count). Asynchronous. */
+int32_t rrt_render_tile_async(RrtScene *scene, const RrtTile *tile, float *d_accum, void *stream);
+
+/* Counters (synchronises the scene's device). */
+int32_t rrt_scene_read_counters(RrtScene *scene, RrtCounters *out);
+int32_t rrt_scene_reset_counters(RrtScene *scene);
+/* Runs the instrumented kernel variant (same seed => same paths) over `tile` into a
+ * scratch accum and returns node visits / box tests / sphere tests / rays / paths. */
+int32_t rrt_scene_count_work(RrtScene *scene, const RrtTile *tile, RrtCounters *out);
+
+/* BVH summary: nodes, leaves, max depth, bytes resident. */
+typedef struct RrtBvhInfo {
+    uint32_t n_nodes;
+    uint32_t n_leaves;
+    uint32_t max_depth;
+    uint32_t max_leaf_size;
+    uint64_t node_bytes;
+    uint64_t prim_bytes;
+} RrtBvhInfo;
+int32_t rrt_scene_bvh_info(const RrtScene *scene, RrtBvhInfo *out);
+
+/* ---- host-side callers of the boundary ------------------------------------------------ */
+
+/* == gpu::build_in_one_weekend_scene (gpu/mod.rs:124-301): RTOW final scene from
+ * SmallRng::seed_from_u64(seed) (reference: 0x5EED_1234) with the grid a,b in
+ * [-grid_half, grid_half) (reference: 11; 50 = the 10k-sphere stress config).
+ * Writes up to sphere_cap spheres/materials; *n_spheres = needed count (call with
+ * cap 0 to size). ov may be NULL (= RenderOverrides::none()). */
+int32_t rrt_build_in_one_weekend_scene(const RrtOverrides *ov, uint64_t seed, int32_t grid_half,
+                                       RrtCamera *cam, RrtSphere *spheres, RrtMaterial *materials,
+                                       uint32_t sphere_cap, uint32_t *n_spheres);
+
+/* Camera::initialize (in_one_weekend/camera.rs:102-150) in f64, cast to the f32 ABI as
+ * gpu/mod.rs:278-298 does. lookfrom/lookat/vup are 3-vectors. */
+int32_t rrt_make_camera(double aspect_ratio, int32_t image_width, int32_t samples_per_pixel,
+                        int32_t max_depth, double vfov, const double *lookfrom, const double *lookat,
+                        const double *vup, double defocus_angle, double focus_dist,
+                        const double *background /* NULL = sky */, uint32_t sample_seed,
+                        uint32_t n_spheres, RrtCamera *cam);
+
+/* Apply RenderOverrides to a Camera's parameters (in_one_weekend/mod.rs:23-55; book 2
+ * the_next_week/mod.rs:31-65 also applies `background`). in/out by pointer. */
+int32_t rrt_apply_overrides(const RrtOverrides *ov, int32_t book,
+                            double *aspect_ratio, int32_t *image_width, int32_t *samples_per_pixel,
+                            int32_t *max_depth, double *vfov, double *lookfrom, double *lookat,
+                            double *vup, double *defocus_angle, double *focus_dist,
+                            double *background, int32_t *has_background);
+
+/* == render_io::write_ppm_from_accum (render_io.rs:3-31), byte-identical P3 text.
+ * Writes to `path` ("-" = stdout). */
+int32_t rrt_write_ppm_from_accum(uint32_t width, uint32_t height, const float *accum,
+                                 uint32_t samples_per_pixel, const char *path);
+/* Same bytes into a caller buffer; *written = bytes needed (call with cap 0 to size). */
+int32_t rrt_format_ppm_from_accum(uint32_t width, uint32_t height, const float *accum,
+                                  uint32_t samples_per_pixel, char *buf, size_t cap, size_t *written);
+/* Quantiser only (render_io.rs:8-26): rgb8[3*W*H]. */
+int32_t rrt_quantize_accum(uint32_t width, uint32_t height, const float *accum,
+                           uint32_t samples_per_pixel, uint8_t *rgb8);
+
+/* Number of visible HIP devices (0 when no GPU). */
+int32_t rrt_device_count(int32_t *count);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RRT_HIP_H */

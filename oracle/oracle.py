@@ -1,0 +1,170 @@
+"""ctypes binding of oracle/build/librrt_oracle.so — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module,
+and only as the checker / CPU baseline. The product (rustraytrace_amd) never imports it.
+See rrt_oracle.cpp for the reference file:line each restated function follows.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_double, c_float, c_int, c_uint8, c_uint32, c_uint64, c_void_p
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "librrt_oracle.so")
+TWIN, BOOKS = 0, 1
+
+_LIB = None
+
+
+def build() -> None:
+    import subprocess
+
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def load() -> ctypes.CDLL:
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        build()
+    lib = ctypes.CDLL(LIB_PATH)
+    P = c_void_p
+    lib.oracle_render.restype = c_int
+    lib.oracle_render.argtypes = [P, P, c_uint32, P, c_uint32, P, c_uint32, c_uint32, c_int, c_uint32, c_uint32,
+                                  c_uint32, c_uint32, c_int, P, P, P]
+    lib.oracle_rtow_scene.restype = c_int
+    lib.oracle_rtow_scene.argtypes = [c_uint64, c_int, P, P, P, P, P, c_uint32, P, P]
+    lib.oracle_write_color.restype = None
+    lib.oracle_write_color.argtypes = [P, P]
+    lib.oracle_quantize_render_io.restype = None
+    lib.oracle_quantize_render_io.argtypes = [c_uint32, P, c_uint32, P]
+    lib.oracle_sphere_hit.restype = c_int
+    lib.oracle_sphere_hit.argtypes = [c_int, P, c_double, P, P, c_double, c_double, P, P, P]
+    lib.oracle_aabb_hit.restype = c_int
+    lib.oracle_aabb_hit.argtypes = [c_int, P, P, P, P, c_double, c_double]
+    lib.oracle_reflect_refract.restype = None
+    lib.oracle_reflect_refract.argtypes = [c_int, P, P, c_double, P, P, P]
+    lib.oracle_path_stream.restype = None
+    lib.oracle_path_stream.argtypes = [c_uint32, c_uint32, c_uint32, c_uint32, P]
+    lib.oracle_acos_atan2_f32.restype = None
+    lib.oracle_acos_atan2_f32.argtypes = [c_float, c_float, P, P]
+    _LIB = lib
+    return lib
+
+
+def _p(a):
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        if a.size == 0:
+            return None
+        assert a.flags["C_CONTIGUOUS"]
+        return c_void_p(a.ctypes.data)
+    return ctypes.cast(ctypes.byref(a), c_void_p)
+
+
+class _Tex(ctypes.Structure):
+    _fields_ = [("rgb8", POINTER(c_uint8)), ("width", ctypes.c_int32), ("height", ctypes.c_int32)]
+
+
+def render(scene, mode=TWIN, rows=None, samples=None, threads=1):
+    """Render `scene` (rustraytrace_amd.SceneData-like: camera/spheres/materials/textures/flags).
+
+    rows = (y0, y1) image rows, samples = (s0, s1) sample range. Returns (accum, rays, sphere_tests)
+    with accum float64 (y1-y0, W, 4); in TWIN mode every value is an exact float32 sum."""
+    lib = load()
+    W, H = int(scene.camera["params_f"][0, 1]), int(scene.camera["params_f"][0, 2])
+    spp = max(int(scene.camera["params_f"][0, 3]), 1)
+    y0, y1 = rows if rows is not None else (0, H)
+    s0, s1 = samples if samples is not None else (0, spp)
+    accum = np.zeros((y1 - y0, W, 4), dtype=np.float64)
+    keep = [np.ascontiguousarray(t, dtype=np.uint8) for t in scene.textures]
+    tex = (_Tex * max(len(keep), 1))()
+    for i, t in enumerate(keep):
+        tex[i].rgb8 = t.ctypes.data_as(POINTER(c_uint8))
+        tex[i].height, tex[i].width = t.shape[0], t.shape[1]
+    rays, tests = c_uint64(0), c_uint64(0)
+    rc = lib.oracle_render(_p(scene.camera), _p(scene.spheres), len(scene.spheres), _p(scene.materials),
+                           len(scene.materials), ctypes.cast(tex, c_void_p) if keep else None, len(keep),
+                           int(scene.flags), int(mode), y0, y1, s0, s1, int(threads), _p(accum),
+                           ctypes.byref(rays), ctypes.byref(tests))
+    if rc != 0:
+        raise RuntimeError(f"oracle_render failed ({rc})")
+    return accum, rays.value, tests.value
+
+
+def rtow_scene(seed=0x5EED_1234, grid_half=11):
+    """Restated gpu::build_in_one_weekend_scene sphere/material list (no camera)."""
+    lib = load()
+    n, sseed = c_uint32(0), c_uint32(0)
+    lib.oracle_rtow_scene(seed, grid_half, None, None, None, None, None, 0, ctypes.byref(n), ctypes.byref(sseed))
+    k = n.value
+    cr = np.zeros((k, 4), np.float32)
+    mi = np.zeros(k, np.uint32)
+    af = np.zeros((k, 4), np.float32)
+    kind = np.zeros(k, np.uint32)
+    ri = np.zeros(k, np.float32)
+    rc = lib.oracle_rtow_scene(seed, grid_half, _p(cr), _p(mi), _p(af), _p(kind), _p(ri), k, ctypes.byref(n),
+                               ctypes.byref(sseed))
+    assert rc == 0
+    return dict(center_radius=cr, material_index=mi, albedo_fuzz=af, kind=kind, ref_idx=ri, sample_seed=sseed.value)
+
+
+def write_color(pixel_color_scaled):
+    lib = load()
+    v = np.ascontiguousarray(pixel_color_scaled, dtype=np.float64)
+    out = np.zeros(3, np.int32)
+    lib.oracle_write_color(_p(v), _p(out))
+    return out
+
+
+def quantize_render_io(accum_f32, spp):
+    lib = load()
+    a = np.ascontiguousarray(accum_f32, dtype=np.float32).reshape(-1, 4)
+    out = np.zeros((a.shape[0], 3), np.uint8)
+    lib.oracle_quantize_render_io(a.shape[0], _p(a), spp, _p(out))
+    return out
+
+
+def sphere_hit(center, radius, o, d, tmin=0.001, tmax=float("inf"), f32=False):
+    lib = load()
+    t = c_double(0)
+    n = np.zeros(3)
+    front = c_int(0)
+    c, oo, dd = (np.asarray(x, np.float64) for x in (center, o, d))
+    hit = lib.oracle_sphere_hit(int(f32), _p(c), float(radius), _p(oo), _p(dd), tmin, tmax, ctypes.byref(t), _p(n),
+                                ctypes.byref(front))
+    return (t.value, n, bool(front.value)) if hit else None
+
+
+def aabb_hit(lo, hi, o, d, tmin=0.001, tmax=float("inf"), f32=False):
+    lib = load()
+    a = [np.asarray(x, np.float64) for x in (lo, hi, o, d)]
+    return bool(lib.oracle_aabb_hit(int(f32), *(_p(x) for x in a), tmin, tmax))
+
+
+def reflect_refract(v, n, eta, cosine, ri, f32=False):
+    lib = load()
+    vv, nn = np.asarray(v, np.float64), np.asarray(n, np.float64)
+    refl, refr = np.zeros(3), np.zeros(3)
+    sc = np.array([cosine, ri, 0.0])
+    lib.oracle_reflect_refract(int(f32), _p(vv), _p(nn), float(eta), _p(refl), _p(refr), _p(sc))
+    return refl, refr, sc[2]
+
+
+def path_stream(seed, pixel, sample, count):
+    lib = load()
+    out = np.zeros(count, np.uint32)
+    lib.oracle_path_stream(seed, pixel, sample, count, _p(out))
+    return out
+
+
+def acos_atan2_f32(x, y):
+    lib = load()
+    a, b = c_float(0), c_float(0)
+    lib.oracle_acos_atan2_f32(x, y, ctypes.byref(a), ctypes.byref(b))
+    return a.value, b.value

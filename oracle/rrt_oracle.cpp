@@ -1,0 +1,864 @@
+// rrt_oracle.cpp — CPU restatement of the reference's "books" path. TEST INFRASTRUCTURE ONLY:
+// only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this
+// library, and only as the checker / CPU baseline — never as the thing measured or shipped.
+//
+// The reference (jwheo12/RustRayTrace) is Rust and cannot be built here (no cargo/rustc,
+// no crates offline: SURVEY §8c). This file restates its CPU path as text, function by
+// function (citations are relative to /root/reference/src):
+//
+//   Vec3 / dot / unit_vector / reflect / refract / random_*   books/in_one_weekend/vec3.rs
+//   Interval::surrounds / clamp                               books/in_one_weekend/interval.rs:30-42
+//   Aabb::new / from_points / from_boxes / hit / pad          books/in_one_weekend/aabb.rs:23-115
+//   BvhNode::build (binned SAH, 12 buckets) / hit             books/in_one_weekend/bvh.rs:16-172
+//   Sphere::new / hit, HitRecord::new                          books/in_one_weekend/sphere.rs:16-51, hittable.rs:20-32
+//   Lambertian / Metal / Dielectric scatter, reflectance      books/in_one_weekend/material.rs:28-102
+//   Camera::get_ray / sample_square / defocus_disk_sample     books/in_one_weekend/camera.rs:152-180
+//   Camera::ray_color (recursive, RR from bounce 5)           books/in_one_weekend/camera.rs:182-209
+//   book-2 ray_color (emission, background), time draw        books/the_next_week/camera.rs:148-201
+//   get_sphere_uv, ImageTexture::value, RtwImage::pixel_data  the_next_week/sphere.rs:46-52, texture.rs:177-196,
+//                                                             rtw_image.rs:46-78
+//   DiffuseLight::emitted                                     the_next_week/material.rs:116-135
+//   write_color (f64 quantiser)                               books/in_one_weekend/color.rs:6-32
+//   write_ppm_from_accum (f32 quantiser)                      render_io.rs:3-31
+//   build_in_one_weekend_scene (seeded SmallRng scene)        gpu/mod.rs:124-301
+//
+// Two modes over the same scene and the same per-path random stream:
+//   BOOKS (mode 1): T = double, the reference's recursion (ray_color calls itself, the
+//          throughput multiplies back-to-front), the reference's BVH tree walked left-first
+//          exactly as BvhNode::hit. The books-faithful CPU baseline.
+//   TWIN  (mode 0): T = float, every operation in the reference's order, throughput carried
+//          front-to-back like the HIP kernel. Its per-pixel f32 sums are the bit-parity target
+//          for the GPU (no FP contraction: built with -ffp-contract=off).
+// Deliberate restatement choices:
+//   * RNG: the reference's thread-local SmallRng::from_entropy (rtweekend.rs:9-11) is not
+//     reproducible; both sides use a PCG32 stream per (seed, pixel, sample) instead, and
+//     random_double() = (u32 >> 8) * 2^-24 (exact in f32 and f64).
+//   * f32 twin: 1e-160 (vec3.rs:185) underflows to 0; transcendentals of sphere UV use the
+//     Cephes f32 polynomials the kernel uses (books mode uses libm acos/atan2).
+#include "../include/rrt_hip.h"
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <limits>
+#include <memory>
+#include <thread>
+#include <type_traits>
+#include <vector>
+
+namespace {
+
+template <class T>
+constexpr T lit(double d, float f) {
+    if constexpr (std::is_same_v<T, float>) return f;
+    else return (T)d;
+}
+#define L(x) lit<T>(x, x##f)
+
+// ---- vec3.rs ----------------------------------------------------------------------------
+template <class T>
+struct Vec3 {
+    T e[3];
+    T x() const { return e[0]; }
+    T y() const { return e[1]; }
+    T z() const { return e[2]; }
+    T operator[](int i) const { return e[i]; }
+};
+template <class T> Vec3<T> mk(T a, T b, T c) { return Vec3<T>{{a, b, c}}; }
+template <class T> Vec3<T> operator+(Vec3<T> a, Vec3<T> b) { return mk(a.e[0] + b.e[0], a.e[1] + b.e[1], a.e[2] + b.e[2]); }
+template <class T> Vec3<T> operator-(Vec3<T> a, Vec3<T> b) { return mk(a.e[0] - b.e[0], a.e[1] - b.e[1], a.e[2] - b.e[2]); }
+template <class T> Vec3<T> operator-(Vec3<T> a) { return mk(-a.e[0], -a.e[1], -a.e[2]); }
+template <class T> Vec3<T> operator*(Vec3<T> a, Vec3<T> b) { return mk(a.e[0] * b.e[0], a.e[1] * b.e[1], a.e[2] * b.e[2]); }
+// vec3.rs:118-132: Vec3 * f64 and f64 * Vec3 both compute e[i] * s
+template <class T> Vec3<T> operator*(Vec3<T> a, T s) { return mk(a.e[0] * s, a.e[1] * s, a.e[2] * s); }
+template <class T> Vec3<T> operator*(T s, Vec3<T> a) { return a * s; }
+// vec3.rs:142-148: Div<f64> is (1.0 / rhs) * self
+template <class T> Vec3<T> operator/(Vec3<T> a, T s) { return (T(1) / s) * a; }
+template <class T> T length_squared(Vec3<T> v) { return v.e[0] * v.e[0] + v.e[1] * v.e[1] + v.e[2] * v.e[2]; }
+template <class T> T length(Vec3<T> v) { return std::sqrt(length_squared(v)); }
+template <class T> T dot(Vec3<T> u, Vec3<T> v) { return u.e[0] * v.e[0] + u.e[1] * v.e[1] + u.e[2] * v.e[2]; }
+template <class T> Vec3<T> unit_vector(Vec3<T> v) { return v / length(v); }
+template <class T> bool near_zero(Vec3<T> v) {  // vec3.rs:38-41
+    const T s = L(1e-8);
+    return std::fabs(v.e[0]) < s && std::fabs(v.e[1]) < s && std::fabs(v.e[2]) < s;
+}
+template <class T> Vec3<T> reflect(Vec3<T> v, Vec3<T> n) { return v - T(2) * dot(v, n) * n; }  // vec3.rs:201-203
+template <class T> T rmin(T a, T b) { return a < b ? a : b; }  // f64::min with a possibly NaN: returns b
+template <class T> Vec3<T> refract(Vec3<T> uv, Vec3<T> n, T etai_over_etat) {  // vec3.rs:205-210
+    const T cos_theta = rmin(-dot(uv, n), T(1));
+    const Vec3<T> r_out_perp = etai_over_etat * (uv + cos_theta * n);
+    const Vec3<T> r_out_parallel = -std::sqrt(std::fabs(T(1) - length_squared(r_out_perp))) * n;
+    return r_out_perp + r_out_parallel;
+}
+
+// ---- RNG (restatement choice, see header) ---------------------------------------------------
+uint64_t splitmix64(uint64_t z) {
+    z += 0x9e3779b97f4a7c15ull;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+struct PathRng {
+    uint64_t s;
+    uint32_t next() {
+        const uint64_t old = s;
+        s = old * 6364136223846793005ull + 1442695040888963407ull;
+        const uint32_t xs = (uint32_t)(((old >> 18) ^ old) >> 27);
+        const uint32_t rot = (uint32_t)(old >> 59);
+        return (xs >> rot) | (xs << ((32u - rot) & 31u));
+    }
+    template <class T> T random_double() { return (T)(next() >> 8) * lit<T>(0x1.0p-24, 0x1.0p-24f); }
+    template <class T> T random_double_range(T lo, T hi) { return random_double<T>() * (hi - lo) + lo; }
+};
+
+template <class T> Vec3<T> random_unit_vector(PathRng &rng) {  // vec3.rs:181-189
+    for (;;) {
+        const T a = rng.random_double_range<T>(T(-1), T(1));
+        const T b = rng.random_double_range<T>(T(-1), T(1));
+        const T c = rng.random_double_range<T>(T(-1), T(1));
+        const Vec3<T> p = mk(a, b, c);
+        const T lensq = length_squared(p);
+        if (L(1e-160) < lensq && lensq <= T(1)) return p / std::sqrt(lensq);
+    }
+}
+template <class T> Vec3<T> random_in_unit_disk(PathRng &rng) {  // vec3.rs:172-179
+    for (;;) {
+        const T a = rng.random_double_range<T>(T(-1), T(1));
+        const T b = rng.random_double_range<T>(T(-1), T(1));
+        const Vec3<T> p = mk(a, b, T(0));
+        if (length_squared(p) < T(1)) return p;
+    }
+}
+
+// ---- Cephes f32 acos / atan2 (twin) or libm (books) ------------------------------------------
+float asin_core(float x) {
+    const float z = x * x;
+    return ((((4.2163199048e-2f * z + 2.4181311049e-2f) * z + 4.5470025998e-2f) * z + 7.4953002686e-2f) * z +
+            1.6666752422e-1f) * z * x + x;
+}
+const float kPiF = 3.14159265358979323846f;
+float cephes_acosf(float x) {
+    if (x < -0.5f) return kPiF - 2.0f * asin_core(std::sqrt(0.5f * (1.0f + x)));
+    if (x > 0.5f) return 2.0f * asin_core(std::sqrt(0.5f * (1.0f - x)));
+    return 1.57079632679489661923f - asin_core(x);
+}
+float cephes_atanf(float x) {
+    float sgn = 1.0f;
+    if (x < 0.0f) { sgn = -1.0f; x = -x; }
+    float y = 0.0f;
+    if (x > 2.414213562373095f) { y = 1.57079632679489661923f; x = -1.0f / x; }
+    else if (x > 0.4142135623730950f) { y = 0.78539816339744830962f; x = (x - 1.0f) / (x + 1.0f); }
+    const float z = x * x;
+    y = y + ((((8.05374449538e-2f * z - 1.38776856032e-1f) * z + 1.99777106478e-1f) * z - 3.33329491539e-1f) * z * x + x);
+    return sgn * y;
+}
+float cephes_atan2f(float y, float x) {
+    if (x == 0.0f) {
+        if (y > 0.0f) return 1.57079632679489661923f;
+        if (y < 0.0f) return -1.57079632679489661923f;
+        return 0.0f;
+    }
+    float z = cephes_atanf(y / x);
+    if (x < 0.0f) z = (y < 0.0f) ? z - kPiF : z + kPiF;
+    return z;
+}
+template <class T> T t_acos(T x) { if constexpr (std::is_same_v<T, float>) return cephes_acosf(x); else return std::acos(x); }
+template <class T> T t_atan2(T y, T x) { if constexpr (std::is_same_v<T, float>) return cephes_atan2f(y, x); else return std::atan2(y, x); }
+template <class T> T t_pi() { return lit<T>(3.14159265358979323846, 3.14159265358979323846f); }
+
+// ---- interval.rs / aabb.rs -----------------------------------------------------------------
+template <class T> struct Interval {
+    T min, max;
+    T size() const { return max - min; }
+    bool surrounds(T x) const { return min < x && x < max; }
+    T clamp(T x) const { return x < min ? min : (x > max ? max : x); }
+    Interval expand(T delta) const { const T p = delta / T(2); return Interval{min - p, max + p}; }
+};
+template <class T> Interval<T> iv_union(Interval<T> a, Interval<T> b) {
+    return Interval<T>{a.min <= b.min ? a.min : b.min, a.max >= b.max ? a.max : b.max};
+}
+template <class T> struct Aabb {
+    Interval<T> ax[3];
+};
+template <class T> Aabb<T> pad(Aabb<T> b) {  // aabb.rs:104-115
+    const T delta = L(0.0001);
+    for (int i = 0; i < 3; ++i)
+        if (b.ax[i].size() < delta) b.ax[i] = b.ax[i].expand(delta);
+    return b;
+}
+template <class T> Aabb<T> empty_box() {
+    const T inf = std::numeric_limits<T>::infinity();
+    return Aabb<T>{{{inf, -inf}, {inf, -inf}, {inf, -inf}}};
+}
+template <class T> Aabb<T> from_boxes(const Aabb<T> &a, const Aabb<T> &b) {
+    return pad(Aabb<T>{{iv_union(a.ax[0], b.ax[0]), iv_union(a.ax[1], b.ax[1]), iv_union(a.ax[2], b.ax[2])}});
+}
+template <class T> Aabb<T> from_points(Vec3<T> a, Vec3<T> b) {  // aabb.rs:29-34
+    Aabb<T> r;
+    for (int i = 0; i < 3; ++i) r.ax[i] = a[i] <= b[i] ? Interval<T>{a[i], b[i]} : Interval<T>{b[i], a[i]};
+    return pad(r);
+}
+template <class T> int longest_axis(const Aabb<T> &b) {
+    if (b.ax[0].size() > b.ax[1].size()) return b.ax[0].size() > b.ax[2].size() ? 0 : 2;
+    return b.ax[1].size() > b.ax[2].size() ? 1 : 2;
+}
+template <class T> T surface_area(const Aabb<T> &b) {
+    const T a = b.ax[0].size(), c = b.ax[1].size(), d = b.ax[2].size();
+    return T(2) * (a * c + a * d + c * d);
+}
+template <class T> bool aabb_hit(const Aabb<T> &box, Vec3<T> o, Vec3<T> d, Interval<T> ray_t) {  // aabb.rs:52-85
+    for (int axis = 0; axis < 3; ++axis) {
+        const Interval<T> ax = box.ax[axis];
+        const T adinv = T(1) / d[axis];
+        const T t0 = (ax.min - o[axis]) * adinv;
+        const T t1 = (ax.max - o[axis]) * adinv;
+        if (t0 < t1) {
+            if (t0 > ray_t.min) ray_t.min = t0;
+            if (t1 < ray_t.max) ray_t.max = t1;
+        } else {
+            if (t1 > ray_t.min) ray_t.min = t1;
+            if (t0 < ray_t.max) ray_t.max = t0;
+        }
+        if (ray_t.max <= ray_t.min) return false;
+    }
+    return true;
+}
+
+// ---- scene in T ---------------------------------------------------------------------------------
+template <class T> struct Sphere {
+    Vec3<T> center;
+    T radius;
+    uint32_t mat;
+    Aabb<T> bbox;
+};
+template <class T> struct Material {
+    uint32_t kind;
+    Vec3<T> albedo;
+    T fuzz;
+    T ref_idx;
+    uint32_t tex;
+};
+struct Texture {
+    const uint8_t *data;
+    int32_t width, height;
+};
+
+template <class T> struct Hit {
+    T t;
+    int32_t sphere;
+};
+
+// BvhNode per bvh.rs: children are either spheres (>= 0 as ~index? no: tagged) or nodes.
+struct ChildRef {
+    bool is_sphere;
+    int32_t index;
+};
+template <class T> struct BvhNode {
+    ChildRef left, right;
+    Aabb<T> bbox;
+};
+
+template <class T> struct World {
+    std::vector<Sphere<T>> spheres;
+    std::vector<Material<T>> mats;
+    std::vector<Texture> texs;
+    std::vector<BvhNode<T>> nodes;
+    ChildRef root{false, -1};
+
+    ChildRef build(std::vector<int32_t> &objs, size_t lo, size_t hi) {  // bvh.rs:21-156
+        const size_t span = hi - lo;
+        Aabb<T> bbox = empty_box<T>();
+        for (size_t i = lo; i < hi; ++i) bbox = from_boxes(bbox, spheres[objs[i]].bbox);
+        const int32_t me = (int32_t)nodes.size();
+        nodes.push_back(BvhNode<T>{});
+        ChildRef left, right;
+        if (span == 1) {
+            left = right = ChildRef{true, objs[lo]};
+        } else if (span == 2) {
+            left = ChildRef{true, objs[lo]};
+            right = ChildRef{true, objs[lo + 1]};
+        } else {
+            const int kBuckets = 12;
+            const int axis = longest_axis(bbox);
+            auto cmp = [&](int32_t a, int32_t b) { return spheres[a].bbox.ax[axis].min < spheres[b].bbox.ax[axis].min; };
+            auto centroid = [&](int32_t o) {
+                const Interval<T> iv = spheres[o].bbox.ax[axis];
+                return T(0.5) * (iv.min + iv.max);
+            };
+            T cmin = std::numeric_limits<T>::infinity(), cmax = -std::numeric_limits<T>::infinity();
+            for (size_t i = lo; i < hi; ++i) {
+                const T c = centroid(objs[i]);
+                if (c < cmin) cmin = c;
+                if (c > cmax) cmax = c;
+            }
+            size_t mid;
+            bool median = false;
+            if (std::fabs(cmax - cmin) < L(1e-12)) {
+                median = true;
+            } else {
+                auto bucket = [&](int32_t o) {
+                    size_t idx = (size_t)((centroid(o) - cmin) / (cmax - cmin) * (T)kBuckets);
+                    return idx >= (size_t)kBuckets ? (size_t)kBuckets - 1 : idx;
+                };
+                size_t count[12] = {0};
+                Aabb<T> bb[12];
+                for (int i = 0; i < kBuckets; ++i) bb[i] = empty_box<T>();
+                for (size_t i = lo; i < hi; ++i) {
+                    const size_t b = bucket(objs[i]);
+                    count[b]++;
+                    bb[b] = from_boxes(bb[b], spheres[objs[i]].bbox);
+                }
+                Aabb<T> rbox[12];
+                size_t rcnt[12];
+                Aabb<T> acc = empty_box<T>();
+                size_t accn = 0;
+                for (int i = kBuckets - 1; i >= 0; --i) {
+                    accn += count[i];
+                    acc = from_boxes(acc, bb[i]);
+                    rbox[i] = acc;
+                    rcnt[i] = accn;
+                }
+                Aabb<T> lbox = empty_box<T>();
+                size_t lcnt = 0;
+                T best = std::numeric_limits<T>::infinity();
+                size_t best_split = 0;
+                for (int i = 0; i < kBuckets - 1; ++i) {
+                    lcnt += count[i];
+                    lbox = from_boxes(lbox, bb[i]);
+                    if (lcnt == 0 || rcnt[i + 1] == 0) continue;
+                    const T cost = surface_area(lbox) * (T)lcnt + surface_area(rbox[i + 1]) * (T)rcnt[i + 1];
+                    if (cost < best) {
+                        best = cost;
+                        best_split = (size_t)i;
+                    }
+                }
+                if (!std::isfinite(best)) {
+                    median = true;
+                } else {
+                    size_t m = 0;
+                    for (size_t i = 0; i < span; ++i)
+                        if (bucket(objs[lo + i]) <= best_split) std::swap(objs[lo + i], objs[lo + m++]);
+                    if (m == 0 || m == span) median = true;
+                    else mid = lo + m;
+                }
+            }
+            if (median) {
+                std::stable_sort(objs.begin() + lo, objs.begin() + hi, cmp);
+                mid = lo + span / 2;
+            }
+            left = build(objs, lo, mid);
+            right = build(objs, mid, hi);
+        }
+        nodes[me] = BvhNode<T>{left, right, bbox};
+        return ChildRef{false, me};
+    }
+
+    // Sphere::hit (sphere.rs:24-51): Some(t) iff a root lies in the open interval.
+    bool hit_sphere(int32_t i, Vec3<T> o, Vec3<T> d, Interval<T> ray_t, T &t_out, uint64_t *tests) const {
+        if (tests) ++*tests;
+        const Sphere<T> &s = spheres[i];
+        const Vec3<T> oc = s.center - o;
+        const T a = length_squared(d);
+        const T h = dot(d, oc);
+        const T c = length_squared(oc) - s.radius * s.radius;
+        const T disc = h * h - a * c;
+        if (disc < T(0)) return false;
+        const T sqrtd = std::sqrt(disc);
+        T root = (h - sqrtd) / a;
+        if (!ray_t.surrounds(root)) {
+            root = (h + sqrtd) / a;
+            if (!ray_t.surrounds(root)) return false;
+        }
+        t_out = root;
+        return true;
+    }
+
+    // HittableObject::hit dispatch + BvhNode::hit (bvh.rs:159-172), left first, right with
+    // max = left.t, result = right.or(left).
+    bool hit(ChildRef ref, Vec3<T> o, Vec3<T> d, Interval<T> ray_t, Hit<T> &rec, uint64_t *tests) const {
+        if (ref.is_sphere) {
+            T t;
+            if (!hit_sphere(ref.index, o, d, ray_t, t, tests)) return false;
+            rec = Hit<T>{t, ref.index};
+            return true;
+        }
+        const BvhNode<T> &n = nodes[ref.index];
+        if (!aabb_hit(n.bbox, o, d, ray_t)) return false;
+        Hit<T> hl, hr;
+        const bool l = hit(n.left, o, d, ray_t, hl, tests);
+        const bool r = hit(n.right, o, d, Interval<T>{ray_t.min, l ? hl.t : ray_t.max}, hr, tests);
+        if (r) { rec = hr; return true; }
+        if (l) { rec = hl; return true; }
+        return false;
+    }
+};
+
+template <class T> struct Cam {
+    Vec3<T> center, p00, du, dv, disk_u, disk_v, background;
+    T radius;
+    uint32_t max_depth, seed, bg_mode, flags;
+    uint32_t width, height;
+};
+
+template <class T>
+void load_world(World<T> &w, Cam<T> &cam, const RrtCamera *c, const RrtSphere *s, uint32_t n, const RrtMaterial *m,
+                uint32_t nm, const RrtTexture *tex, uint32_t ntex, uint32_t flags) {
+    auto v3 = [](const float *f) { return mk<T>((T)f[0], (T)f[1], (T)f[2]); };
+    cam.center = v3(c->origin);
+    cam.p00 = v3(c->pixel00);
+    cam.du = v3(c->pixel_delta_u);
+    cam.dv = v3(c->pixel_delta_v);
+    cam.radius = (T)c->params_f[0];
+    cam.disk_u = v3(c->u) * cam.radius;  // defocus_disk_u = u * defocus_radius (camera.rs:136-138)
+    cam.disk_v = v3(c->v) * cam.radius;
+    cam.background = v3(c->background);
+    cam.max_depth = c->params_u[0];
+    cam.seed = c->params_u[1];
+    cam.bg_mode = c->params_u[3];
+    cam.flags = flags;
+    cam.width = (uint32_t)c->params_f[1];
+    cam.height = (uint32_t)c->params_f[2];
+    w.spheres.resize(n);
+    for (uint32_t i = 0; i < n; ++i) {  // Sphere::new (sphere.rs:16-21)
+        const Vec3<T> center = v3(s[i].center_radius);
+        const T r = std::max((T)s[i].center_radius[3], T(0));
+        const Vec3<T> rvec = mk(r, r, r);
+        w.spheres[i] = Sphere<T>{center, r, s[i].material_index, from_points(center - rvec, center + rvec)};
+    }
+    w.mats.resize(nm);
+    for (uint32_t i = 0; i < nm; ++i) {
+        Material<T> &mm = w.mats[i];
+        mm.kind = m[i].kind;
+        mm.albedo = v3(m[i].albedo_fuzz);
+        const T fuzz = (T)m[i].albedo_fuzz[3];
+        mm.fuzz = fuzz < T(1) ? fuzz : T(1);  // Metal::new (material.rs:48-50)
+        mm.ref_idx = (T)m[i].ref_idx;
+        mm.tex = m[i]._pad[0];
+    }
+    for (uint32_t i = 0; i < ntex; ++i) w.texs.push_back(Texture{tex[i].rgb8, tex[i].width, tex[i].height});
+    if (n) {
+        std::vector<int32_t> objs(n);
+        for (uint32_t i = 0; i < n; ++i) objs[i] = (int32_t)i;
+        w.root = w.build(objs, 0, n);
+    }
+}
+
+template <class T> struct Record {
+    Vec3<T> p, normal, outward;
+    bool front;
+    uint32_t mat;
+};
+
+template <class T>
+bool world_hit(const World<T> &w, Vec3<T> o, Vec3<T> d, Record<T> &rec, uint64_t *tests) {  // camera.rs:187
+    if (w.root.index < 0) return false;
+    Hit<T> h;
+    if (!w.hit(w.root, o, d, Interval<T>{L(0.001), std::numeric_limits<T>::infinity()}, h, tests)) return false;
+    const Sphere<T> &s = w.spheres[h.sphere];
+    rec.p = o + h.t * d;                         // Ray::at
+    rec.outward = (rec.p - s.center) / s.radius;  // sphere.rs:48
+    rec.front = dot(d, rec.outward) < T(0);       // hittable.rs:28-29
+    rec.normal = rec.front ? rec.outward : -rec.outward;
+    rec.mat = s.mat;
+    return true;
+}
+
+template <class T>
+Vec3<T> texture_value(const World<T> &w, uint32_t tex, Vec3<T> outward) {
+    // get_sphere_uv (the_next_week/sphere.rs:46-52)
+    const T theta = t_acos<T>(-outward.y());
+    const T phi = t_atan2<T>(-outward.z(), outward.x()) + t_pi<T>();
+    T u = phi / (T(2) * t_pi<T>());
+    T v = theta / t_pi<T>();
+    const Texture &t = w.texs[tex];
+    if (t.height <= 0) return mk(T(0), T(1), T(1));  // texture.rs:179-181
+    const Interval<T> unit{T(0), T(1)};
+    u = unit.clamp(u);
+    v = T(1) - unit.clamp(v);
+    auto to_i32 = [](T x) -> int32_t {  // Rust `as i32`: saturating, NaN -> 0
+        if (!(x == x)) return 0;
+        if (x <= (T)INT32_MIN) return INT32_MIN;
+        if (x >= (T)INT32_MAX) return INT32_MAX;
+        return (int32_t)x;
+    };
+    int32_t i = to_i32(u * (T)t.width);
+    int32_t j = to_i32(v * (T)t.height);
+    auto clampi = [](int32_t x, int32_t lo, int32_t hi) { return x < lo ? lo : (x < hi ? x : hi - 1); };  // rtw_image.rs:326-334
+    if (!t.data) return mk(T(1), T(0), T(1));  // rtw_image.rs:303-305
+    i = clampi(i, 0, t.width);
+    j = clampi(j, 0, t.height);
+    const uint8_t *px = t.data + ((size_t)j * t.width + i) * 3;
+    const T cs = T(1) / T(255);
+    return mk(cs * (T)px[0], cs * (T)px[1], cs * (T)px[2]);
+}
+
+// Material::scatter (material.rs:28-102; book 2 material.rs:41-53). Returns false for None.
+template <class T>
+bool scatter(const World<T> &w, PathRng &rng, Vec3<T> d_in, const Record<T> &rec, Vec3<T> &att, Vec3<T> &dir) {
+    const Material<T> &m = w.mats[rec.mat];
+    switch (m.kind) {
+        case RRT_MAT_LAMBERTIAN:
+        case RRT_MAT_TEXTURED_LAMBERTIAN: {
+            Vec3<T> sd = rec.normal + random_unit_vector<T>(rng);
+            if (near_zero(sd)) sd = rec.normal;
+            dir = sd;
+            att = m.kind == RRT_MAT_LAMBERTIAN ? m.albedo : texture_value(w, m.tex, rec.outward);
+            return true;
+        }
+        case RRT_MAT_METAL: {
+            Vec3<T> reflected = reflect(d_in, rec.normal);
+            reflected = unit_vector(reflected) + m.fuzz * random_unit_vector<T>(rng);
+            dir = reflected;
+            att = m.albedo;
+            return dot(dir, rec.normal) > T(0);
+        }
+        case RRT_MAT_DIELECTRIC: {
+            att = mk(T(1), T(1), T(1));
+            const T ri = rec.front ? T(1) / m.ref_idx : m.ref_idx;
+            const Vec3<T> ud = unit_vector(d_in);
+            const T cos_theta = rmin(-dot(ud, rec.normal), T(1));
+            const T sin_theta = std::sqrt(T(1) - cos_theta * cos_theta);
+            const bool cannot = ri * sin_theta > T(1);
+            // reflectance (material.rs:75-80): powi(5) == x * ((x*x)*(x*x))
+            auto reflectance = [&](T cosine, T rix) {
+                T r0 = (T(1) - rix) / (T(1) + rix);
+                r0 = r0 * r0;
+                const T x = T(1) - cosine;
+                const T x2 = x * x;
+                const T x4 = x2 * x2;
+                return r0 + (T(1) - r0) * (x * x4);
+            };
+            if (cannot || reflectance(cos_theta, ri) > rng.random_double<T>()) dir = reflect(ud, rec.normal);
+            else dir = refract(ud, rec.normal, ri);
+            return true;
+        }
+        default:  // DiffuseLight: scatter -> None
+            return false;
+    }
+}
+
+template <class T> Vec3<T> emitted(const World<T> &w, const Record<T> &rec) {
+    const Material<T> &m = w.mats[rec.mat];
+    return m.kind == RRT_MAT_DIFFUSE_LIGHT ? m.albedo : mk(T(0), T(0), T(0));
+}
+
+template <class T> Vec3<T> miss_color(const Cam<T> &cam, Vec3<T> d) {
+    if (cam.bg_mode == 1u) return cam.background;  // book-2 background / reference GPU bg_mode
+    const Vec3<T> ud = unit_vector(d);             // camera.rs:206-208
+    const T a = L(0.5) * (ud.y() + T(1));
+    return (T(1) - a) * mk(T(1), T(1), T(1)) + a * mk(L(0.5), L(0.7), T(1));
+}
+
+template <class T> T rr_probability(Vec3<T> att) {  // camera.rs:191-195
+    T p = att.x();
+    if (att.y() > p) p = att.y();
+    if (att.z() > p) p = att.z();
+    if (p < L(0.05)) p = L(0.05);
+    if (p > L(0.95)) p = L(0.95);
+    return p;
+}
+
+struct Tally {
+    uint64_t rays = 0, tests = 0;
+};
+
+// BOOKS: Camera::ray_color (camera.rs:182-209 / the_next_week/camera.rs:174-201), recursive.
+template <class T>
+Vec3<T> ray_color_books(const World<T> &w, const Cam<T> &cam, PathRng &rng, Vec3<T> o, Vec3<T> d, int depth, Tally &tl) {
+    if (depth <= 0) return mk(T(0), T(0), T(0));
+    tl.rays++;
+    Record<T> rec;
+    if (!world_hit(w, o, d, rec, &tl.tests)) return miss_color(cam, d);
+    const Vec3<T> em = emitted(w, rec);
+    Vec3<T> att, dir;
+    if (!scatter(w, rng, d, rec, att, dir)) return em;
+    const int bounces = (int)cam.max_depth - depth;
+    if (bounces >= 5) {
+        const T p = rr_probability(att);
+        if (rng.random_double<T>() > p) return em;
+        return em + att * ray_color_books(w, cam, rng, rec.p, dir, depth - 1, tl) / p;
+    }
+    return em + att * ray_color_books(w, cam, rng, rec.p, dir, depth - 1, tl);
+}
+
+// TWIN: the same path, throughput front-to-back (the HIP kernel's order, rrt_kernel.hip).
+template <class T>
+Vec3<T> ray_color_twin(const World<T> &w, const Cam<T> &cam, PathRng &rng, Vec3<T> o, Vec3<T> d, Tally &tl) {
+    Vec3<T> Tp = mk(T(1), T(1), T(1)), Lp = mk(T(0), T(0), T(0));
+    for (uint32_t k = 0; k < cam.max_depth; ++k) {
+        tl.rays++;
+        Record<T> rec;
+        if (!world_hit(w, o, d, rec, &tl.tests)) return Lp + Tp * miss_color(cam, d);
+        const Material<T> &m = w.mats[rec.mat];
+        if (m.kind == RRT_MAT_DIFFUSE_LIGHT) return Lp + Tp * m.albedo;
+        Vec3<T> att, dir;
+        if (!scatter(w, rng, d, rec, att, dir)) return Lp;
+        if (k >= 5u) {
+            const T p = rr_probability(att);
+            if (rng.random_double<T>() > p) return Lp;
+            Tp = (Tp * att) * (T(1) / p);
+        } else {
+            Tp = Tp * att;
+        }
+        o = rec.p;
+        d = dir;
+    }
+    return Lp;
+}
+
+// Camera::get_ray (camera.rs:152-169, the_next_week/camera.rs:148-163)
+template <class T>
+void get_ray(const Cam<T> &cam, PathRng &rng, uint32_t i, uint32_t j, Vec3<T> &o, Vec3<T> &d) {
+    const T ox = rng.random_double<T>() - L(0.5);
+    const T oy = rng.random_double<T>() - L(0.5);
+    const Vec3<T> pixel_sample = cam.p00 + ((T)i + ox) * cam.du + ((T)j + oy) * cam.dv;
+    if (cam.radius <= T(0)) {
+        o = cam.center;
+    } else {
+        const Vec3<T> p = random_in_unit_disk<T>(rng);
+        o = cam.center + (p[0] * cam.disk_u) + (p[1] * cam.disk_v);
+    }
+    d = pixel_sample - o;
+    if (cam.flags & RRT_FLAG_RAY_TIME) (void)rng.random_double<T>();
+}
+
+template <class T>
+int render(const RrtCamera *c, const RrtSphere *s, uint32_t n, const RrtMaterial *m, uint32_t nm, const RrtTexture *tex,
+           uint32_t ntex, uint32_t flags, int mode, uint32_t y0, uint32_t y1, uint32_t s0, uint32_t s1, int threads,
+           double *accum, uint64_t *rays_out, uint64_t *tests_out) {
+    World<T> w;
+    Cam<T> cam;
+    load_world(w, cam, c, s, n, m, nm, tex, ntex, flags);
+    if (y1 > cam.height) y1 = cam.height;
+    if (y0 > y1) return -1;
+    std::atomic<uint32_t> next_row{y0};
+    std::atomic<uint64_t> rays{0}, tests{0};
+    auto worker = [&]() {
+        Tally tl;
+        for (;;) {
+            const uint32_t j = next_row.fetch_add(1);  // rayon-like dynamic row scheduling (camera.rs:66-88)
+            if (j >= y1) break;
+            for (uint32_t i = 0; i < cam.width; ++i) {
+                const uint32_t pixel = j * cam.width + i;
+                const uint64_t key = splitmix64(((uint64_t)cam.seed << 32) ^ (uint64_t)pixel);
+                Vec3<T> sum = mk(T(0), T(0), T(0));
+                for (uint32_t sidx = s0; sidx < s1; ++sidx) {
+                    PathRng rng{splitmix64(key + sidx)};
+                    Vec3<T> o, d;
+                    get_ray(cam, rng, i, j, o, d);
+                    sum = sum + (mode == 1 ? ray_color_books(w, cam, rng, o, d, (int)cam.max_depth, tl)
+                                           : ray_color_twin(w, cam, rng, o, d, tl));
+                }
+                double *px = accum + ((size_t)(j - y0) * cam.width + i) * 4;
+                px[0] = (double)sum.x();
+                px[1] = (double)sum.y();
+                px[2] = (double)sum.z();
+                px[3] = (double)(s1 - s0);
+            }
+        }
+        rays += tl.rays;
+        tests += tl.tests;
+    };
+    if (threads <= 1) {
+        worker();
+    } else {
+        std::vector<std::thread> th;
+        for (int t = 0; t < threads; ++t) th.emplace_back(worker);
+        for (auto &t : th) t.join();
+    }
+    if (rays_out) *rays_out = rays.load();
+    if (tests_out) *tests_out = tests.load();
+    return 0;
+}
+
+// ---- gpu::build_in_one_weekend_scene restated (gpu/mod.rs:199-298 draw order) -------------------
+struct Xoshiro256pp {
+    uint64_t s[4];
+    static uint64_t rotl(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
+    explicit Xoshiro256pp(uint64_t seed) {  // SeedableRng::seed_from_u64 via SplitMix64
+        for (int i = 0; i < 4; ++i) {
+            seed += 0x9e3779b97f4a7c15ull;
+            uint64_t z = seed;
+            z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+            z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+            s[i] = z ^ (z >> 31);
+        }
+    }
+    uint64_t next_u64() {
+        const uint64_t r = rotl(s[0] + s[3], 23) + s[0];
+        const uint64_t t = s[1] << 17;
+        s[2] ^= s[0];
+        s[3] ^= s[1];
+        s[1] ^= s[2];
+        s[0] ^= s[3];
+        s[2] ^= t;
+        s[3] = rotl(s[3], 45);
+        return r;
+    }
+    uint32_t next_u32() { return (uint32_t)(next_u64() >> 32); }
+};
+
+}  // namespace
+
+extern "C" {
+
+// mode 0 = TWIN (f32, kernel order), 1 = BOOKS (f64, recursive). Renders rows [y0,y1),
+// samples [s0,s1) into accum[(y1-y0)*W*4] (double; TWIN values are exact f32 sums).
+int oracle_render(const RrtCamera *cam, const RrtSphere *s, uint32_t n, const RrtMaterial *m, uint32_t nm,
+                  const RrtTexture *tex, uint32_t ntex, uint32_t flags, int mode, uint32_t y0, uint32_t y1,
+                  uint32_t s0, uint32_t s1, int threads, double *accum, uint64_t *rays, uint64_t *sphere_tests) {
+    if (!cam || !accum) return -1;
+    if (mode == 1) return render<double>(cam, s, n, m, nm, tex, ntex, flags, 1, y0, y1, s0, s1, threads, accum, rays, sphere_tests);
+    return render<float>(cam, s, n, m, nm, tex, ntex, flags, 0, y0, y1, s0, s1, threads, accum, rays, sphere_tests);
+}
+
+// gpu::build_in_one_weekend_scene's sphere/material list (no overrides, camera seed out).
+int oracle_rtow_scene(uint64_t seed, int grid_half, float *center_radius, uint32_t *mat_index, float *albedo_fuzz,
+                      uint32_t *kind, float *ref_idx, uint32_t cap, uint32_t *n_out, uint32_t *sample_seed) {
+    std::vector<float> cr, af, ri;
+    std::vector<uint32_t> mi, kd;
+    auto add = [&](float x, float y, float z, float r, uint32_t k, float a0, float a1, float a2, float fz, float rf) {
+        cr.insert(cr.end(), {x, y, z, r});
+        mi.push_back((uint32_t)kd.size());
+        kd.push_back(k);
+        af.insert(af.end(), {a0, a1, a2, fz});
+        ri.push_back(rf);
+    };
+    Xoshiro256pp rng(seed);
+    auto f32 = [&]() { return (float)(rng.next_u32() >> 8) * (1.0f / 16777216.0f); };
+    auto f64 = [&]() { return (double)(rng.next_u64() >> 11) * (1.0 / 9007199254740992.0); };
+    auto range05_1 = [&]() {
+        for (;;) {
+            uint32_t bits = (rng.next_u32() >> 9) | 0x3f800000u;
+            float v;
+            std::memcpy(&v, &bits, 4);
+            const float r = (v - 1.0f) * 0.5f + 0.5f;
+            if (r < 1.0f) return r;
+        }
+    };
+    add(0.0f, -1000.0f, 0.0f, 1000.0f, 0, 0.5f, 0.5f, 0.5f, 0.0f, 1.0f);
+    for (int a = -grid_half; a < grid_half; ++a)
+        for (int b = -grid_half; b < grid_half; ++b) {
+            const float choose = f32();
+            const double cx = (double)a + 0.9 * f64();
+            const double cz = (double)b + 0.9 * f64();
+            const double dx = cx - 4.0, dy = 0.2 - 0.2, dz = cz - 0.0;
+            if (std::sqrt(dx * dx + dy * dy + dz * dz) > 0.9) {
+                if (choose < 0.8f) {
+                    float al[3];
+                    for (int c = 0; c < 3; ++c) { const float p = f32(); const float q = f32(); al[c] = p * q; }
+                    add((float)cx, (float)0.2, (float)cz, 0.2f, 0, al[0], al[1], al[2], 0.0f, 1.0f);
+                } else if (choose < 0.95f) {
+                    float al[3];
+                    for (int c = 0; c < 3; ++c) al[c] = range05_1();
+                    const float fz = f32() * 0.5f;
+                    add((float)cx, (float)0.2, (float)cz, 0.2f, 1, al[0], al[1], al[2], fz, 1.0f);
+                } else {
+                    add((float)cx, (float)0.2, (float)cz, 0.2f, 2, 1.0f, 1.0f, 1.0f, 0.0f, 1.5f);
+                }
+            }
+        }
+    add(0.0f, 1.0f, 0.0f, 1.0f, 2, 1.0f, 1.0f, 1.0f, 0.0f, 1.5f);
+    add(-4.0f, 1.0f, 0.0f, 1.0f, 0, 0.4f, 0.2f, 0.1f, 0.0f, 1.0f);
+    add(4.0f, 1.0f, 0.0f, 1.0f, 1, 0.7f, 0.6f, 0.5f, 0.0f, 1.0f);
+    const uint32_t n = (uint32_t)kd.size();
+    *n_out = n;
+    if (sample_seed) *sample_seed = rng.next_u32();
+    if (cap < n) return cap == 0 ? 0 : -1;
+    std::memcpy(center_radius, cr.data(), cr.size() * 4);
+    std::memcpy(mat_index, mi.data(), mi.size() * 4);
+    std::memcpy(albedo_fuzz, af.data(), af.size() * 4);
+    std::memcpy(kind, kd.data(), kd.size() * 4);
+    std::memcpy(ref_idx, ri.data(), ri.size() * 4);
+    return 0;
+}
+
+// color.rs:6-32 write_color (f64): returns the three i32 bytes for one pixel.
+void oracle_write_color(const double *pixel_color_scaled, int32_t *rgb) {
+    for (int c = 0; c < 3; ++c) {
+        double x = pixel_color_scaled[c];
+        x = x > 0.0 ? std::sqrt(x) : 0.0;            // linear_to_gamma
+        const double cl = x < 0.0 ? 0.0 : (x > 0.999 ? 0.999 : x);  // Interval::clamp (NaN passes)
+        const double v = 256.0 * cl;
+        rgb[c] = (v != v) ? 0 : (int32_t)v;          // Rust `as i32`: NaN -> 0
+    }
+}
+
+// render_io.rs:8-26 quantiser (f32) for W*H RGBA accum -> rgb8.
+void oracle_quantize_render_io(uint32_t n_pixels, const float *accum, uint32_t spp, uint8_t *rgb8) {
+    const float scale = spp > 0 ? 1.0f / (float)spp : 0.0f;
+    for (uint32_t i = 0; i < n_pixels; ++i)
+        for (int c = 0; c < 3; ++c) {
+            float r = accum[i * 4 + c] * scale;
+            if (!std::isfinite(r)) r = 0.0f;
+            r = std::sqrt(r > 0.0f ? r : 0.0f);
+            if (r < 0.0f) r = 0.0f;
+            if (r > 0.999f) r = 0.999f;
+            rgb8[i * 3 + c] = (uint8_t)(r * 256.0f);
+        }
+}
+
+// ---- known-answer hooks for the restated primitives (T = float when f32 != 0) ----------------
+int oracle_sphere_hit(int f32, const double *center, double radius, const double *o, const double *d, double tmin,
+                      double tmax, double *t_out, double *normal_out, int *front_out) {
+    auto run = [&](auto tag) -> int {
+        using T = decltype(tag);
+        World<T> w;
+        const Vec3<T> c = mk((T)center[0], (T)center[1], (T)center[2]);
+        const T r = std::max((T)radius, T(0));
+        w.spheres.push_back(Sphere<T>{c, r, 0, from_points(c - mk(r, r, r), c + mk(r, r, r))});
+        const Vec3<T> O = mk((T)o[0], (T)o[1], (T)o[2]), D = mk((T)d[0], (T)d[1], (T)d[2]);
+        T t;
+        if (!w.hit_sphere(0, O, D, Interval<T>{(T)tmin, (T)tmax}, t, nullptr)) return 0;
+        const Vec3<T> p = O + t * D;
+        const Vec3<T> out = (p - c) / r;
+        const bool front = dot(D, out) < T(0);
+        const Vec3<T> n = front ? out : -out;
+        *t_out = t;
+        for (int i = 0; i < 3; ++i) normal_out[i] = n[i];
+        *front_out = front;
+        return 1;
+    };
+    return f32 ? run(0.0f) : run(0.0);
+}
+
+int oracle_aabb_hit(int f32, const double *lo, const double *hi, const double *o, const double *d, double tmin, double tmax) {
+    auto run = [&](auto tag) -> int {
+        using T = decltype(tag);
+        Aabb<T> b;
+        for (int i = 0; i < 3; ++i) b.ax[i] = Interval<T>{(T)lo[i], (T)hi[i]};
+        return aabb_hit(b, mk((T)o[0], (T)o[1], (T)o[2]), mk((T)d[0], (T)d[1], (T)d[2]), Interval<T>{(T)tmin, (T)tmax});
+    };
+    return f32 ? run(0.0f) : run(0.0);
+}
+
+void oracle_reflect_refract(int f32, const double *v, const double *n, double eta, double *refl, double *refr,
+                            double *schlick_cos_eta) {
+    auto run = [&](auto tag) {
+        using T = decltype(tag);
+        const Vec3<T> V = mk((T)v[0], (T)v[1], (T)v[2]), N = mk((T)n[0], (T)n[1], (T)n[2]);
+        const Vec3<T> a = reflect(V, N), b = refract(V, N, (T)eta);
+        for (int i = 0; i < 3; ++i) { refl[i] = a[i]; refr[i] = b[i]; }
+        const T cosine = (T)schlick_cos_eta[0], rix = (T)schlick_cos_eta[1];
+        T r0 = (T(1) - rix) / (T(1) + rix);
+        r0 = r0 * r0;
+        const T x = T(1) - cosine, x2 = x * x, x4 = x2 * x2;
+        schlick_cos_eta[2] = r0 + (T(1) - r0) * (x * x4);
+    };
+    if (f32) run(0.0f); else run(0.0);
+}
+
+// The first `count` u32 draws of path (seed, pixel, sample).
+void oracle_path_stream(uint32_t seed, uint32_t pixel, uint32_t sample, uint32_t count, uint32_t *out) {
+    PathRng rng{splitmix64(splitmix64(((uint64_t)seed << 32) ^ (uint64_t)pixel) + sample)};
+    for (uint32_t i = 0; i < count; ++i) out[i] = rng.next();
+}
+
+void oracle_acos_atan2_f32(float x, float y, float *acos_out, float *atan2_out) {
+    *acos_out = cephes_acosf(x);
+    *atan2_out = cephes_atan2f(y, x);
+}
+
+}  // extern "C"

@@ -1,0 +1,133 @@
+// rrt — host CLI mirroring the reference's src/main.rs (flags :17-56, dispatch :58-98)
+// and config::OVERRIDES (config.rs:50-62), calling librrt_hip.so through its C-ABI.
+//
+//   rrt [--backend hip|cuda|gpu] [--gpu|--cuda] [in_one_weekend] [overrides...] > image.ppm
+//
+// The reference's compile-time OVERRIDES become runtime flags with the same field names
+// (defaults = the committed OVERRIDES: image_width 2160, samples_per_pixel 5000,
+// max_depth 100). `cuda`/`gpu` are accepted as aliases of `hip` so existing command lines
+// keep working; there is no CPU renderer in this backend (the reference's books path is
+// the CPU renderer) and no silent fallback.
+#include "../../include/rrt_hip.h"
+
+#include <cctype>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+static std::string normalize_book_name(const std::string &name) {  // main.rs:7-12
+    std::string out;
+    for (char c : name)
+        if (std::isalnum((unsigned char)c)) out += (char)std::tolower((unsigned char)c);
+    return out;
+}
+
+static bool parse3(const char *s, double *v) { return std::sscanf(s, "%lf,%lf,%lf", &v[0], &v[1], &v[2]) == 3; }
+
+static void usage() {
+    std::fprintf(stderr,
+                 "Usage: rrt [--backend hip|cuda|gpu] <book> [scene] [--image_width N] [--samples_per_pixel N]\n"
+                 "           [--max_depth N] [--aspect_ratio X] [--vfov X] [--lookfrom x,y,z] [--lookat x,y,z]\n"
+                 "           [--vup x,y,z] [--defocus_angle X] [--focus_dist X] [--background r,g,b]\n"
+                 "           [--gpus N] [--seed S] [--grid_half G] [-o out.ppm]\n"
+                 "books: in_one_weekend\n");
+}
+
+int main(int argc, char **argv) {
+    std::string backend = "hip";
+    std::vector<std::string> positional;
+    RrtOverrides ov;
+    std::memset(&ov, 0, sizeof(ov));
+    ov.has_image_width = 1;  // config.rs:50-62 committed values
+    ov.image_width = 2160;
+    ov.has_samples_per_pixel = 1;
+    ov.samples_per_pixel = 5000;
+    ov.has_max_depth = 1;
+    ov.max_depth = 100;
+    uint32_t gpus = 1;
+    uint64_t seed = 0x5EED1234ull;
+    int grid_half = 11;
+    std::string out = "-";
+
+    for (int i = 1; i < argc; ++i) {
+        std::string a = argv[i];
+        auto next = [&](const char *what) -> const char * {
+            if (i + 1 >= argc) {
+                std::fprintf(stderr, "%s expects a value\n", what);
+                std::exit(2);
+            }
+            return argv[++i];
+        };
+        if (a == "--gpu" || a == "--cuda" || a == "--hip") backend = "hip";
+        else if (a == "--cpu") backend = "cpu";
+        else if (a == "--backend") backend = next("--backend");
+        else if (a.rfind("--backend=", 0) == 0) backend = a.substr(10);
+        else if (a == "--image_width") { ov.has_image_width = 1; ov.image_width = std::atoi(next("--image_width")); }
+        else if (a == "--samples_per_pixel") { ov.has_samples_per_pixel = 1; ov.samples_per_pixel = std::atoi(next("--samples_per_pixel")); }
+        else if (a == "--max_depth") { ov.has_max_depth = 1; ov.max_depth = std::atoi(next("--max_depth")); }
+        else if (a == "--aspect_ratio") { ov.has_aspect_ratio = 1; ov.aspect_ratio = std::atof(next("--aspect_ratio")); }
+        else if (a == "--vfov") { ov.has_vfov = 1; ov.vfov = std::atof(next("--vfov")); }
+        else if (a == "--lookfrom") { ov.has_lookfrom = parse3(next("--lookfrom"), ov.lookfrom); }
+        else if (a == "--lookat") { ov.has_lookat = parse3(next("--lookat"), ov.lookat); }
+        else if (a == "--vup") { ov.has_vup = parse3(next("--vup"), ov.vup); }
+        else if (a == "--defocus_angle") { ov.has_defocus_angle = 1; ov.defocus_angle = std::atof(next("--defocus_angle")); }
+        else if (a == "--focus_dist") { ov.has_focus_dist = 1; ov.focus_dist = std::atof(next("--focus_dist")); }
+        else if (a == "--background") { ov.has_background = parse3(next("--background"), ov.background); }
+        else if (a == "--gpus") gpus = (uint32_t)std::atoi(next("--gpus"));
+        else if (a == "--seed") seed = std::strtoull(next("--seed"), nullptr, 0);
+        else if (a == "--grid_half") grid_half = std::atoi(next("--grid_half"));
+        else if (a == "-o") out = next("-o");
+        else if (a == "-h" || a == "--help") { usage(); return 0; }
+        else positional.push_back(a);
+    }
+    for (auto &c : backend) c = (char)std::tolower((unsigned char)c);
+    const std::string book = normalize_book_name(positional.empty() ? "in_one_weekend" : positional[0]);
+    int32_t ndev = 0;
+    rrt_device_count(&ndev);
+    std::fprintf(stderr, "HIP devices: %d\n", ndev);  // main.rs:15 prints the rayon thread count
+
+    if (backend == "cpu") {
+        std::fprintf(stderr, "The CPU books renderer is the reference's (cargo run -- %s); this binary is the HIP backend.\n",
+                     positional.empty() ? "in_one_weekend" : positional[0].c_str());
+        return 2;
+    }
+    if (backend != "hip" && backend != "cuda" && backend != "gpu") {
+        std::fprintf(stderr, "unknown backend '%s': expected hip (aliases: cuda, gpu)\n", backend.c_str());
+        return 2;
+    }
+    if (!(book == "inoneweekend" || book == "oneweekend" || book == "weekend")) {  // main.rs:59-70
+        std::fprintf(stderr, "HIP backend currently supports in_one_weekend only.\n");
+        return 2;
+    }
+
+    RrtCamera cam;
+    uint32_t n = 0;
+    if (rrt_build_in_one_weekend_scene(&ov, seed, grid_half, &cam, nullptr, nullptr, 0, &n)) {
+        std::fprintf(stderr, "HIP render failed: %s\n", rrt_hip_last_error());
+        return 1;
+    }
+    std::vector<RrtSphere> spheres(n);
+    std::vector<RrtMaterial> materials(n);
+    if (rrt_build_in_one_weekend_scene(&ov, seed, grid_half, &cam, spheres.data(), materials.data(), n, &n)) {
+        std::fprintf(stderr, "HIP render failed: %s\n", rrt_hip_last_error());
+        return 1;
+    }
+    const uint32_t w = (uint32_t)cam.params_f[1], h = (uint32_t)cam.params_f[2];
+    const uint32_t spp = (uint32_t)(cam.params_f[3] < 1.0f ? 1.0f : cam.params_f[3]);
+    std::vector<float> accum((size_t)w * h * 4);
+    const auto t0 = std::chrono::steady_clock::now();
+    if (rrt_hip_render(&cam, spheres.data(), n, materials.data(), n, nullptr, 0, spp, gpus, 0, accum.data())) {
+        std::fprintf(stderr, "HIP render failed: %s\n", rrt_hip_last_error());  // main.rs:60-65
+        return 1;
+    }
+    const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    std::fprintf(stderr, "rendered %ux%u @ %u spp, %u spheres, %u GPU(s) in %.3f s\n", w, h, spp, n, gpus, secs);
+    if (rrt_write_ppm_from_accum(w, h, accum.data(), spp, out.c_str())) {
+        std::fprintf(stderr, "HIP render failed: %s\n", rrt_hip_last_error());
+        return 1;
+    }
+    return 0;
+}

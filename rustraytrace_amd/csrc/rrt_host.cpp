@@ -1,0 +1,876 @@
+// rrt_host.cpp — host runtime of librrt_hip.so: the C-ABI of include/rrt_hip.h.
+//
+//   scene builder     == gpu::build_in_one_weekend_scene   (src/gpu/mod.rs:124-301)
+//   BVH build         binned SAH per BvhNode::build       (src/books/in_one_weekend/bvh.rs:21-156)
+//   one-shot render   replaces cuda::imp::render          (src/cuda/mod.rs:342-439)
+//   PPM writer        == render_io::write_ppm_from_accum  (src/render_io.rs:3-31)
+//
+// Device memory is owned by RrtScene; the one-shot entry frees everything before it
+// returns (ownership contract of SURVEY §8b). No CPU rendering fallback exists here:
+// without a HIP device every render entry fails with RRT_E_NODEV.
+#include "rrt_internal.h"
+#include "../../include/rrt_hip.h"
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr, what)                                                                   \
+    do {                                                                                      \
+        hipError_t e__ = (expr);                                                              \
+        if (e__ != hipSuccess)                                                                \
+            return fail(RRT_E_HIP, std::string(what) + " failed: " + hipGetErrorString(e__)); \
+    } while (0)
+
+// ------------------------------------------------------------------------------------
+// rand 0.8.5 SmallRng (= Xoshiro256++ on 64-bit) with seed_from_u64's SplitMix64 fill,
+// and the Standard / UniformFloat float conversions it applies (Cargo.lock:810-812).
+// Restated from the published algorithms (the crate is not in this image: unpinned).
+// ------------------------------------------------------------------------------------
+struct SmallRng {
+    uint64_t s[4];
+    static uint64_t rotl(uint64_t x, int k) { return (x << k) | (x >> (64 - k)); }
+    explicit SmallRng(uint64_t state) {
+        const uint64_t phi = 0x9e3779b97f4a7c15ull;
+        for (int i = 0; i < 4; ++i) {
+            state += phi;
+            uint64_t z = state;
+            z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+            z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+            s[i] = z ^ (z >> 31);
+        }
+    }
+    uint64_t next_u64() {
+        const uint64_t result = rotl(s[0] + s[3], 23) + s[0];
+        const uint64_t t = s[1] << 17;
+        s[2] ^= s[0];
+        s[3] ^= s[1];
+        s[1] ^= s[2];
+        s[0] ^= s[3];
+        s[2] ^= t;
+        s[3] = rotl(s[3], 45);
+        return result;
+    }
+    uint32_t next_u32() { return (uint32_t)(next_u64() >> 32); }
+    float gen_f32() { return (float)(next_u32() >> 8) * (1.0f / 16777216.0f); }          // Standard f32
+    double gen_f64() { return (double)(next_u64() >> 11) * (1.0 / 9007199254740992.0); }  // Standard f64
+    float gen_range_f32(float lo, float hi) {  // UniformFloat<f32>::sample_single
+        const float scale = hi - lo;
+        for (;;) {
+            uint32_t bits = (next_u32() >> 9) | (127u << 23);
+            float v12;
+            std::memcpy(&v12, &bits, 4);
+            const float res = (v12 - 1.0f) * scale + lo;
+            if (res < hi) return res;
+        }
+    }
+};
+
+struct D3 {
+    double x, y, z;
+};
+D3 d3(double x, double y, double z) { return D3{x, y, z}; }
+D3 operator+(D3 a, D3 b) { return d3(a.x + b.x, a.y + b.y, a.z + b.z); }
+D3 operator-(D3 a, D3 b) { return d3(a.x - b.x, a.y - b.y, a.z - b.z); }
+D3 operator*(D3 a, double s) { return d3(a.x * s, a.y * s, a.z * s); }
+D3 operator/(D3 a, double s) { return d3(a.x / s, a.y / s, a.z / s); }  // gpu/mod.rs:89-95 divides
+double length(D3 v) { return std::sqrt(v.x * v.x + v.y * v.y + v.z * v.z); }
+D3 cross(D3 a, D3 b) { return d3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
+D3 unit_vector(D3 v) { return v / length(v); }
+double degrees_to_radians(double deg) { return deg * M_PI / 180.0; }
+
+void put4(float *dst, float a, float b, float c, float d) {
+    dst[0] = a;
+    dst[1] = b;
+    dst[2] = c;
+    dst[3] = d;
+}
+
+// ------------------------------------------------------------------------------------
+// BVH: binned SAH exactly as bvh.rs:21-156 chooses splits (12 buckets, longest axis of
+// the node bbox, stable-sort+median fallbacks), with leaves of <= max_leaf spheres, then
+// flattened into 64-B GNodes with both child boxes in the parent.
+// ------------------------------------------------------------------------------------
+struct Interval {
+    double min, max;
+    double size() const { return max - min; }
+};
+struct Aabb {
+    Interval ax[3];
+};
+const double kInf = std::numeric_limits<double>::infinity();
+
+Interval iv_union(Interval a, Interval b) {  // interval.rs:44-49
+    return Interval{a.min <= b.min ? a.min : b.min, a.max >= b.max ? a.max : b.max};
+}
+Aabb pad(Aabb b) {  // aabb.rs:104-115
+    const double delta = 0.0001;
+    for (int i = 0; i < 3; ++i)
+        if (b.ax[i].size() < delta) b.ax[i] = Interval{b.ax[i].min - delta / 2.0, b.ax[i].max + delta / 2.0};
+    return b;
+}
+Aabb aabb_empty() { return Aabb{{{kInf, -kInf}, {kInf, -kInf}, {kInf, -kInf}}}; }
+Aabb aabb_union(const Aabb &a, const Aabb &b) {
+    return pad(Aabb{{iv_union(a.ax[0], b.ax[0]), iv_union(a.ax[1], b.ax[1]), iv_union(a.ax[2], b.ax[2])}});
+}
+int longest_axis(const Aabb &b) {  // aabb.rs:87-95
+    if (b.ax[0].size() > b.ax[1].size()) return b.ax[0].size() > b.ax[2].size() ? 0 : 2;
+    return b.ax[1].size() > b.ax[2].size() ? 1 : 2;
+}
+double surface_area(const Aabb &b) {
+    const double a = b.ax[0].size(), c1 = b.ax[1].size(), c2 = b.ax[2].size();
+    return 2.0 * (a * c1 + a * c2 + c1 * c2);
+}
+
+float f32_down(double d) {
+    float f = (float)d;
+    if ((double)f > d) f = std::nextafter(f, -std::numeric_limits<float>::infinity());
+    return f;
+}
+float f32_up(double d) {
+    float f = (float)d;
+    if ((double)f < d) f = std::nextafter(f, std::numeric_limits<float>::infinity());
+    return f;
+}
+
+struct Builder {
+    const std::vector<Aabb> &boxes;
+    std::vector<uint32_t> objs;
+    std::vector<rrt::GNode> nodes;
+    uint32_t max_leaf;
+    uint32_t max_depth = 0;
+    uint32_t n_leaves = 0;
+    uint32_t max_leaf_seen = 0;
+
+    struct Ref {
+        bool leaf;
+        int32_t index;  // node index or first primitive
+        int32_t count;
+        Aabb box;
+    };
+
+    Builder(const std::vector<Aabb> &b, uint32_t leaf) : boxes(b), max_leaf(leaf) {
+        objs.resize(b.size());
+        for (size_t i = 0; i < b.size(); ++i) objs[i] = (uint32_t)i;
+    }
+
+    double centroid(uint32_t o, int axis) const {
+        return 0.5 * (boxes[o].ax[axis].min + boxes[o].ax[axis].max);
+    }
+
+    void sort_by_min(size_t lo, size_t hi, int axis) {  // Rust slice::sort_by is stable
+        std::stable_sort(objs.begin() + lo, objs.begin() + hi, [&](uint32_t a, uint32_t b) {
+            return boxes[a].ax[axis].min < boxes[b].ax[axis].min;
+        });
+    }
+
+    // bvh.rs:34-152: returns the split point (absolute index) for objs[lo, hi)
+    size_t split(size_t lo, size_t hi, const Aabb &bbox) {
+        const size_t span = hi - lo;
+        constexpr int kBuckets = 12;
+        const int axis = longest_axis(bbox);
+        double cmin = kInf, cmax = -kInf;
+        for (size_t i = lo; i < hi; ++i) {
+            const double c = centroid(objs[i], axis);
+            if (c < cmin) cmin = c;
+            if (c > cmax) cmax = c;
+        }
+        if (std::fabs(cmax - cmin) < 1e-12) {
+            sort_by_min(lo, hi, axis);
+            return lo + span / 2;
+        }
+        auto bucket_of = [&](uint32_t o) {
+            size_t idx = (size_t)((centroid(o, axis) - cmin) / (cmax - cmin) * (double)kBuckets);
+            return idx >= (size_t)kBuckets ? (size_t)kBuckets - 1 : idx;
+        };
+        size_t count[kBuckets] = {0};
+        Aabb bb[kBuckets];
+        for (int i = 0; i < kBuckets; ++i) bb[i] = aabb_empty();
+        for (size_t i = lo; i < hi; ++i) {
+            const size_t b = bucket_of(objs[i]);
+            count[b]++;
+            bb[b] = aabb_union(bb[b], boxes[objs[i]]);
+        }
+        Aabb right_bb[kBuckets];
+        size_t right_cnt[kBuckets];
+        Aabb acc = aabb_empty();
+        size_t acc_n = 0;
+        for (int i = kBuckets - 1; i >= 0; --i) {
+            acc_n += count[i];
+            acc = aabb_union(acc, bb[i]);
+            right_bb[i] = acc;
+            right_cnt[i] = acc_n;
+        }
+        Aabb left = aabb_empty();
+        size_t left_n = 0;
+        double best = kInf;
+        size_t best_split = 0;
+        for (int i = 0; i < kBuckets - 1; ++i) {
+            left_n += count[i];
+            left = aabb_union(left, bb[i]);
+            if (left_n == 0 || right_cnt[i + 1] == 0) continue;
+            const double cost = surface_area(left) * (double)left_n + surface_area(right_bb[i + 1]) * (double)right_cnt[i + 1];
+            if (cost < best) {
+                best = cost;
+                best_split = (size_t)i;
+            }
+        }
+        if (!std::isfinite(best)) {
+            sort_by_min(lo, hi, axis);
+            return lo + span / 2;
+        }
+        size_t mid = 0;
+        for (size_t i = 0; i < span; ++i) {
+            if (bucket_of(objs[lo + i]) <= best_split) {
+                std::swap(objs[lo + i], objs[lo + mid]);
+                ++mid;
+            }
+        }
+        if (mid == 0 || mid == span) {
+            sort_by_min(lo, hi, axis);
+            return lo + span / 2;
+        }
+        return lo + mid;
+    }
+
+    Ref build(size_t lo, size_t hi, uint32_t depth) {
+        Aabb bbox = aabb_empty();
+        for (size_t i = lo; i < hi; ++i) bbox = aabb_union(bbox, boxes[objs[i]]);
+        if (depth > max_depth) max_depth = depth;
+        const size_t span = hi - lo;
+        if (span <= max_leaf) {
+            n_leaves++;
+            if (span > max_leaf_seen) max_leaf_seen = (uint32_t)span;
+            return Ref{true, (int32_t)lo, (int32_t)span, bbox};
+        }
+        const size_t mid = split(lo, hi, bbox);
+        const int32_t me = (int32_t)nodes.size();
+        nodes.push_back(rrt::GNode{});
+        Ref l = build(lo, mid, depth + 1);
+        Ref r = build(mid, hi, depth + 1);
+        set_node(me, l, r);
+        return Ref{false, me, 0, bbox};
+    }
+
+    void set_node(int32_t me, const Ref &l, const Ref &r) {
+        rrt::GNode &n = nodes[me];
+        auto lo = [](const Ref &c, int a) { return f32_down(c.box.ax[a].min); };
+        auto hi = [](const Ref &c, int a) { return f32_up(c.box.ax[a].max); };
+        n.b0 = make_float4(lo(l, 0), hi(l, 0), lo(l, 1), hi(l, 1));
+        n.b1 = make_float4(lo(l, 2), hi(l, 2), lo(r, 0), hi(r, 0));
+        n.b2 = make_float4(lo(r, 1), hi(r, 1), lo(r, 2), hi(r, 2));
+        n.link = make_int4(l.index, r.index, l.leaf ? l.count : 0, r.leaf ? r.count : 0);
+    }
+};
+
+// A child that no ray can enter: a point box at 1e30 (rejected for every direction,
+// including zero components where the slab test produces +-inf).
+Builder::Ref never_hit() {
+    Aabb b;
+    for (int i = 0; i < 3; ++i) b.ax[i] = Interval{1e30, 1e30};
+    return Builder::Ref{true, 0, 0, b};
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------
+struct RrtScene {
+    int device = 0;
+    rrt::GNode *d_nodes = nullptr;
+    float4 *d_prim_cr = nullptr;
+    uint32_t *d_prim_mat = nullptr;
+    rrt::GMaterial *d_mats = nullptr;
+    uint8_t *d_tex_pool = nullptr;
+    rrt::GTexture *d_texs = nullptr;
+    unsigned long long *d_counters = nullptr;       // 5 x u64, render launches
+    unsigned long long *d_work_counters = nullptr;  // 5 x u64, instrumented launches
+    rrt::KParams base{};
+    RrtBvhInfo info{};
+};
+
+namespace {
+
+void free_scene(RrtScene *s) {
+    if (!s) return;
+    (void)hipSetDevice(s->device);
+    (void)hipFree(s->d_nodes);
+    (void)hipFree(s->d_prim_cr);
+    (void)hipFree(s->d_prim_mat);
+    (void)hipFree(s->d_mats);
+    (void)hipFree(s->d_tex_pool);
+    (void)hipFree(s->d_texs);
+    (void)hipFree(s->d_counters);
+    (void)hipFree(s->d_work_counters);
+    delete s;
+}
+
+template <class T>
+int upload(T **dst, const T *src, size_t n, const char *what) {
+    const size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
+    HIP_TRY(hipMalloc((void **)dst, bytes), std::string("hipMalloc ") + what);
+    if (n) HIP_TRY(hipMemcpy(*dst, src, n * sizeof(T), hipMemcpyHostToDevice), std::string("copy ") + what);
+    return RRT_OK;
+}
+
+uint32_t tile_rows_of(uint32_t height, const RrtTile &t) {
+    uint32_t rows = 0;
+    const uint32_t bands = (height + t.band_rows - 1) / t.band_rows;
+    for (uint32_t b = t.rank; b < bands; b += t.n_ranks) rows += std::min(t.band_rows, height - b * t.band_rows);
+    return rows;
+}
+
+int check_tile(const RrtScene *s, const RrtTile *t) {
+    if (!s || !t) return fail(RRT_E_INVALID, "null scene or tile");
+    if (t->band_rows == 0 || t->n_ranks == 0 || t->rank >= t->n_ranks)
+        return fail(RRT_E_INVALID, "tile: band_rows and n_ranks must be > 0 and rank < n_ranks");
+    if (t->sample_end < t->sample_begin) return fail(RRT_E_INVALID, "tile: sample_end < sample_begin");
+    return RRT_OK;
+}
+
+int fill_params(RrtScene *s, const RrtTile *t, float *d_accum, rrt::KParams &p) {
+    p = s->base;
+    p.accum = reinterpret_cast<float4 *>(d_accum);
+    p.tile_rows = tile_rows_of(p.height, *t);
+    p.band_rows = t->band_rows;
+    p.rank = t->rank;
+    p.n_ranks = t->n_ranks;
+    p.sample_begin = t->sample_begin;
+    p.sample_end = t->sample_end;
+    p.tiles_x = (p.width + 7u) / 8u;
+    p.n_work_tiles = p.tiles_x * ((p.tile_rows + 7u) / 8u);
+    return RRT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *rrt_hip_last_error(void) { return g_err.c_str(); }
+uint32_t rrt_hip_abi_version(void) { return RRT_ABI_VERSION; }
+
+int32_t rrt_device_count(int32_t *count) {
+    if (!count) return fail(RRT_E_INVALID, "null count");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    *count = n;
+    return RRT_OK;
+}
+
+int32_t rrt_scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint32_t n_spheres,
+                         const RrtMaterial *materials, uint32_t n_materials, const RrtTexture *textures,
+                         uint32_t n_textures, uint32_t flags, int32_t device, RrtScene **out) {
+    if (!cam || !out) return fail(RRT_E_INVALID, "null camera or out pointer");
+    if (n_spheres && !spheres) return fail(RRT_E_INVALID, "null spheres");
+    if (n_materials && !materials) return fail(RRT_E_INVALID, "null materials");
+    if (n_textures && !textures) return fail(RRT_E_INVALID, "null textures");
+    *out = nullptr;
+    const float wf = cam->params_f[1], hf = cam->params_f[2];
+    if (!(wf >= 1.0f) || !(hf >= 1.0f) || wf > 65536.0f || hf > 65536.0f)
+        return fail(RRT_E_INVALID, "camera params_f[1..2] (width/height) out of range");
+    for (uint32_t i = 0; i < n_spheres; ++i)
+        if (spheres[i].material_index >= n_materials)
+            return fail(RRT_E_INVALID, "sphere " + std::to_string(i) + " material_index out of range");
+    for (uint32_t i = 0; i < n_materials; ++i) {
+        if (materials[i].kind > RRT_MAT_DIFFUSE_LIGHT)
+            return fail(RRT_E_INVALID, "material " + std::to_string(i) + " has unknown kind");
+        if (materials[i].kind == RRT_MAT_TEXTURED_LAMBERTIAN && materials[i]._pad[0] >= n_textures)
+            return fail(RRT_E_INVALID, "material " + std::to_string(i) + " texture index out of range");
+    }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(RRT_E_NODEV, "no HIP device available");
+    if (device < 0 || device >= ndev) return fail(RRT_E_INVALID, "device index out of range");
+
+    // ---- BVH over the sphere bounding boxes (sphere.rs:16-21: r = max(radius, 0)) ----
+    std::vector<Aabb> boxes(n_spheres);
+    for (uint32_t i = 0; i < n_spheres; ++i) {
+        const double r = std::max((double)spheres[i].center_radius[3], 0.0);
+        Aabb b;
+        for (int a = 0; a < 3; ++a) {
+            const double c = spheres[i].center_radius[a];
+            b.ax[a] = Interval{c - r, c + r};
+        }
+        boxes[i] = pad(b);
+    }
+    Builder bld(boxes, 2);
+    if (n_spheres == 0) {
+        bld.nodes.push_back(rrt::GNode{});
+        bld.set_node(0, never_hit(), never_hit());
+    } else {
+        Builder::Ref root = bld.build(0, n_spheres, 0);
+        if (root.leaf) {
+            bld.nodes.push_back(rrt::GNode{});
+            bld.set_node(0, root, never_hit());
+            bld.max_depth = 1;
+        }
+    }
+    if (bld.max_depth + 1 > (uint32_t)rrt::kStackDepth)
+        return fail(RRT_E_INVALID, "BVH depth " + std::to_string(bld.max_depth) + " exceeds the LDS stack");
+
+    std::vector<float4> prim_cr(n_spheres);
+    std::vector<uint32_t> prim_mat(n_spheres);
+    for (uint32_t i = 0; i < n_spheres; ++i) {
+        const RrtSphere &sp = spheres[bld.objs[i]];
+        prim_cr[i] = make_float4(sp.center_radius[0], sp.center_radius[1], sp.center_radius[2],
+                                 std::max(sp.center_radius[3], 0.0f));
+        prim_mat[i] = sp.material_index;
+    }
+    std::vector<rrt::GMaterial> mats(n_materials);
+    for (uint32_t i = 0; i < n_materials; ++i) {
+        const RrtMaterial &m = materials[i];
+        float fuzz = m.albedo_fuzz[3];
+        if (m.kind == RRT_MAT_METAL) fuzz = fuzz < 1.0f ? fuzz : 1.0f;  // material.rs:48-50
+        int ref_bits;
+        std::memcpy(&ref_bits, &m.ref_idx, 4);
+        mats[i].a = make_float4(m.albedo_fuzz[0], m.albedo_fuzz[1], m.albedo_fuzz[2], fuzz);
+        mats[i].b = make_int4((int)m.kind, ref_bits, (int)m._pad[0], 0);
+    }
+    std::vector<rrt::GTexture> texs(n_textures);
+    size_t pool = 0;
+    for (uint32_t i = 0; i < n_textures; ++i) {
+        const RrtTexture &t = textures[i];
+        if (t.width < 0 || t.height < 0 || ((size_t)t.width * t.height > 0 && !t.rgb8))
+            return fail(RRT_E_INVALID, "texture " + std::to_string(i) + " invalid");
+        texs[i] = rrt::GTexture{(int32_t)pool, t.width, t.height, 0};
+        pool += (size_t)t.width * t.height * 3;
+    }
+    if (pool > (size_t)INT32_MAX) return fail(RRT_E_INVALID, "texture pool exceeds 2 GiB");
+    std::vector<uint8_t> tex_pool(pool);
+    for (uint32_t i = 0; i < n_textures; ++i)
+        if ((size_t)textures[i].width * textures[i].height)
+            std::memcpy(tex_pool.data() + texs[i].offset, textures[i].rgb8, (size_t)textures[i].width * textures[i].height * 3);
+
+    RrtScene *s = new RrtScene();
+    s->device = device;
+    int rc = RRT_OK;
+    do {
+        if (hipSetDevice(device) != hipSuccess) { rc = fail(RRT_E_HIP, "hipSetDevice failed"); break; }
+        if ((rc = upload(&s->d_nodes, bld.nodes.data(), bld.nodes.size(), "nodes"))) break;
+        if ((rc = upload(&s->d_prim_cr, prim_cr.data(), prim_cr.size(), "spheres"))) break;
+        if ((rc = upload(&s->d_prim_mat, prim_mat.data(), prim_mat.size(), "sphere materials"))) break;
+        if ((rc = upload(&s->d_mats, mats.data(), mats.size(), "materials"))) break;
+        if ((rc = upload(&s->d_tex_pool, tex_pool.data(), tex_pool.size(), "textures"))) break;
+        if ((rc = upload(&s->d_texs, texs.data(), texs.size(), "texture table"))) break;
+        if (hipMalloc((void **)&s->d_counters, 8 * sizeof(unsigned long long)) != hipSuccess ||
+            hipMalloc((void **)&s->d_work_counters, 8 * sizeof(unsigned long long)) != hipSuccess) {
+            rc = fail(RRT_E_NOMEM, "hipMalloc counters failed");
+            break;
+        }
+        if (hipMemset(s->d_counters, 0, 8 * sizeof(unsigned long long)) != hipSuccess ||
+            hipMemset(s->d_work_counters, 0, 8 * sizeof(unsigned long long)) != hipSuccess) {
+            rc = fail(RRT_E_HIP, "hipMemset counters failed");
+            break;
+        }
+    } while (0);
+    if (rc) {
+        free_scene(s);
+        return rc;
+    }
+
+    rrt::KParams &p = s->base;
+    p.nodes = s->d_nodes;
+    p.prim_cr = s->d_prim_cr;
+    p.prim_mat = s->d_prim_mat;
+    p.mats = s->d_mats;
+    p.tex_pool = s->d_tex_pool;
+    p.texs = s->d_texs;
+    p.counters = s->d_counters;
+    const float radius = cam->params_f[0];
+    for (int i = 0; i < 3; ++i) {
+        p.p00[i] = cam->pixel00[i];
+        p.du[i] = cam->pixel_delta_u[i];
+        p.dv[i] = cam->pixel_delta_v[i];
+        p.center[i] = cam->origin[i];
+        p.disk_u[i] = cam->u[i] * radius;  // defocus_disk_u = u * defocus_radius (camera.rs:136-138)
+        p.disk_v[i] = cam->v[i] * radius;
+        p.background[i] = cam->background[i];
+    }
+    p.defocus_radius = radius;
+    p.max_depth = cam->params_u[0];
+    p.seed = cam->params_u[1];
+    p.bg_mode = cam->params_u[3];
+    p.flags = flags;
+    p.width = (uint32_t)wf;
+    p.height = (uint32_t)hf;
+
+    RrtBvhInfo &bi = s->info;
+    bi.n_nodes = (uint32_t)bld.nodes.size();
+    bi.n_leaves = bld.n_leaves;
+    bi.max_depth = bld.max_depth;
+    bi.max_leaf_size = bld.max_leaf_seen;
+    bi.node_bytes = bld.nodes.size() * sizeof(rrt::GNode);
+    bi.prim_bytes = (uint64_t)n_spheres * (sizeof(float4) + sizeof(uint32_t));
+    *out = s;
+    return RRT_OK;
+}
+
+int32_t rrt_scene_destroy(RrtScene *scene) {
+    free_scene(scene);
+    return RRT_OK;
+}
+
+int32_t rrt_scene_bvh_info(const RrtScene *scene, RrtBvhInfo *out) {
+    if (!scene || !out) return fail(RRT_E_INVALID, "null scene or out");
+    *out = scene->info;
+    return RRT_OK;
+}
+
+int32_t rrt_tile_rows(const RrtScene *scene, const RrtTile *tile, uint32_t *rows_out) {
+    if (int rc = check_tile(scene, tile)) return rc;
+    if (!rows_out) return fail(RRT_E_INVALID, "null rows_out");
+    *rows_out = tile_rows_of(scene->base.height, *tile);
+    return RRT_OK;
+}
+
+int32_t rrt_tile_row_index(const RrtScene *scene, const RrtTile *tile, uint32_t local_row, uint32_t *row_out) {
+    if (int rc = check_tile(scene, tile)) return rc;
+    if (!row_out) return fail(RRT_E_INVALID, "null row_out");
+    if (local_row >= tile_rows_of(scene->base.height, *tile)) return fail(RRT_E_INVALID, "local_row out of range");
+    const uint32_t band = local_row / tile->band_rows;
+    *row_out = (band * tile->n_ranks + tile->rank) * tile->band_rows + local_row % tile->band_rows;
+    return RRT_OK;
+}
+
+int32_t rrt_render_tile_async(RrtScene *scene, const RrtTile *tile, float *d_accum, void *stream) {
+    if (int rc = check_tile(scene, tile)) return rc;
+    rrt::KParams p;
+    fill_params(scene, tile, d_accum, p);
+    if (p.tile_rows && !d_accum) return fail(RRT_E_INVALID, "null d_accum");
+    HIP_TRY(hipSetDevice(scene->device), "hipSetDevice");
+    HIP_TRY(rrt::launch_render(p, (hipStream_t)stream), "render kernel launch");
+    return RRT_OK;
+}
+
+int32_t rrt_scene_read_counters(RrtScene *scene, RrtCounters *out) {
+    if (!scene || !out) return fail(RRT_E_INVALID, "null scene or out");
+    unsigned long long c[8];
+    HIP_TRY(hipSetDevice(scene->device), "hipSetDevice");
+    HIP_TRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    HIP_TRY(hipMemcpy(c, scene->d_counters, sizeof(c), hipMemcpyDeviceToHost), "copy counters");
+    *out = RrtCounters{c[0], c[1], c[2], c[3], c[4]};
+    return RRT_OK;
+}
+
+int32_t rrt_scene_reset_counters(RrtScene *scene) {
+    if (!scene) return fail(RRT_E_INVALID, "null scene");
+    HIP_TRY(hipSetDevice(scene->device), "hipSetDevice");
+    HIP_TRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    HIP_TRY(hipMemset(scene->d_counters, 0, 8 * sizeof(unsigned long long)), "reset counters");
+    return RRT_OK;
+}
+
+int32_t rrt_scene_count_work(RrtScene *scene, const RrtTile *tile, RrtCounters *out) {
+    if (int rc = check_tile(scene, tile)) return rc;
+    if (!out) return fail(RRT_E_INVALID, "null out");
+    rrt::KParams p;
+    fill_params(scene, tile, nullptr, p);
+    HIP_TRY(hipSetDevice(scene->device), "hipSetDevice");
+    float4 *scratch = nullptr;
+    HIP_TRY(hipMalloc((void **)&scratch, std::max<size_t>((size_t)p.tile_rows * p.width, 1) * sizeof(float4)),
+            "hipMalloc scratch accum");
+    p.accum = scratch;
+    p.counters = scene->d_work_counters;
+    hipError_t e = hipMemset(scene->d_work_counters, 0, 8 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = rrt::launch_render_counting(p, nullptr);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    unsigned long long c[8] = {0};
+    if (e == hipSuccess) e = hipMemcpy(c, scene->d_work_counters, sizeof(c), hipMemcpyDeviceToHost);
+    (void)hipFree(scratch);
+    if (e != hipSuccess) return fail(RRT_E_HIP, std::string("counting render failed: ") + hipGetErrorString(e));
+    *out = RrtCounters{c[0], c[1], c[2], c[3], c[4]};
+    return RRT_OK;
+}
+
+// ---- one-shot drop-in (cuda/mod.rs:342-439) ---------------------------------------------
+int32_t rrt_hip_render(const RrtCamera *cam, const RrtSphere *spheres, uint32_t n_spheres,
+                       const RrtMaterial *materials, uint32_t n_materials, const RrtTexture *textures,
+                       uint32_t n_textures, uint32_t total_spp, uint32_t n_gpus, uint32_t flags,
+                       float *accum_out) {
+    if (!cam || !accum_out) return fail(RRT_E_INVALID, "null camera or accum_out");
+    if (total_spp == 0) total_spp = (uint32_t)std::max(cam->params_f[3], 1.0f);  // cuda/mod.rs:384
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(RRT_E_NODEV, "no HIP device available");
+    if (n_gpus == 0) n_gpus = 1;
+    if ((int)n_gpus > ndev)
+        return fail(RRT_E_INVALID, "n_gpus=" + std::to_string(n_gpus) + " > visible devices " + std::to_string(ndev));
+    const uint32_t width = (uint32_t)cam->params_f[1];
+    const uint32_t height = (uint32_t)cam->params_f[2];
+
+    std::mutex mu;
+    std::string first_err;
+    int first_rc = RRT_OK;
+    std::atomic<uint32_t> done{0};
+    auto worker = [&](uint32_t g) {
+        auto set_err = [&](int rc) {
+            std::lock_guard<std::mutex> lk(mu);
+            if (first_rc == RRT_OK) {
+                first_rc = rc;
+                first_err = g_err;
+            }
+        };
+        RrtScene *scene = nullptr;
+        int rc = rrt_scene_create(cam, spheres, n_spheres, materials, n_materials, textures, n_textures, flags,
+                                  (int32_t)g, &scene);
+        if (rc) return set_err(rc);
+        const RrtTile tile{16u, g, n_gpus, 0u, total_spp};
+        const uint32_t rows = tile_rows_of(height, tile);
+        float *d_accum = nullptr;
+        std::vector<float> host((size_t)rows * width * 4);
+        hipError_t e = hipMalloc((void **)&d_accum, std::max<size_t>(host.size(), 4) * sizeof(float));
+        if (e != hipSuccess) {
+            rrt_scene_destroy(scene);
+            g_err = std::string("hipMalloc accum failed: ") + hipGetErrorString(e);
+            return set_err(RRT_E_NOMEM);
+        }
+        rc = rrt_render_tile_async(scene, &tile, d_accum, nullptr);
+        if (!rc) {
+            e = hipDeviceSynchronize();
+            if (e == hipSuccess) e = hipMemcpy(host.data(), d_accum, host.size() * sizeof(float), hipMemcpyDeviceToHost);
+            if (e != hipSuccess) {
+                g_err = std::string("render failed: ") + hipGetErrorString(e);
+                rc = RRT_E_HIP;
+            }
+        }
+        (void)hipFree(d_accum);
+        rrt_scene_destroy(scene);
+        if (rc) return set_err(rc);
+        for (uint32_t lr = 0; lr < rows; ++lr) {
+            const uint32_t band = lr / tile.band_rows;
+            const uint32_t y = (band * tile.n_ranks + tile.rank) * tile.band_rows + lr % tile.band_rows;
+            std::memcpy(accum_out + (size_t)y * width * 4, host.data() + (size_t)lr * width * 4, (size_t)width * 16);
+        }
+        const uint32_t d = ++done;
+        if (!(flags & RRT_FLAG_QUIET)) {
+            std::lock_guard<std::mutex> lk(mu);
+            std::fprintf(stderr, "\rHIP progress: %u/%u GPUs (%.1f%%)", d, n_gpus, 100.0 * d / n_gpus);
+            if (d == n_gpus) std::fprintf(stderr, "\n");
+        }
+    };
+    if (n_gpus == 1) {
+        worker(0);
+    } else {
+        std::vector<std::thread> th;
+        for (uint32_t g = 0; g < n_gpus; ++g) th.emplace_back(worker, g);
+        for (auto &t : th) t.join();
+    }
+    if (first_rc) return fail(first_rc, first_err);
+    return RRT_OK;
+}
+
+// ---- scene builder (gpu/mod.rs:124-301) ------------------------------------------------
+int32_t rrt_apply_overrides(const RrtOverrides *o, int32_t book, double *aspect_ratio, int32_t *image_width,
+                            int32_t *samples_per_pixel, int32_t *max_depth, double *vfov, double *lookfrom,
+                            double *lookat, double *vup, double *defocus_angle, double *focus_dist,
+                            double *background, int32_t *has_background) {
+    if (!o) return RRT_OK;
+    if (o->has_aspect_ratio && aspect_ratio) *aspect_ratio = o->aspect_ratio;
+    if (o->has_image_width && image_width) *image_width = o->image_width;
+    if (o->has_samples_per_pixel && samples_per_pixel) *samples_per_pixel = o->samples_per_pixel;
+    if (o->has_max_depth && max_depth) *max_depth = o->max_depth;
+    if (o->has_vfov && vfov) *vfov = o->vfov;
+    if (o->has_lookfrom && lookfrom) std::memcpy(lookfrom, o->lookfrom, 24);
+    if (o->has_lookat && lookat) std::memcpy(lookat, o->lookat, 24);
+    if (o->has_vup && vup) std::memcpy(vup, o->vup, 24);
+    if (o->has_defocus_angle && defocus_angle) *defocus_angle = o->defocus_angle;
+    if (o->has_focus_dist && focus_dist) *focus_dist = o->focus_dist;
+    // book 1 ignores `background` (in_one_weekend/mod.rs:23-55); book 2 and the GPU
+    // scene builder apply it (the_next_week/mod.rs:62-64, gpu/mod.rs:169-172).
+    if (book != 1 && o->has_background && background) {
+        std::memcpy(background, o->background, 24);
+        if (has_background) *has_background = 1;
+    }
+    return RRT_OK;
+}
+
+int32_t rrt_make_camera(double aspect_ratio, int32_t image_width, int32_t samples_per_pixel, int32_t max_depth,
+                        double vfov, const double *lookfrom_, const double *lookat_, const double *vup_,
+                        double defocus_angle, double focus_dist, const double *background, uint32_t sample_seed,
+                        uint32_t n_spheres, RrtCamera *cam) {
+    if (!lookfrom_ || !lookat_ || !vup_ || !cam) return fail(RRT_E_INVALID, "null camera argument");
+    if (image_width < 1) return fail(RRT_E_INVALID, "image_width must be >= 1");
+    int32_t image_height = (int32_t)((double)image_width / aspect_ratio);  // gpu/mod.rs:174-177
+    if (image_height < 1) image_height = 1;
+    const D3 lookfrom = d3(lookfrom_[0], lookfrom_[1], lookfrom_[2]);
+    const D3 lookat = d3(lookat_[0], lookat_[1], lookat_[2]);
+    const D3 vup = d3(vup_[0], vup_[1], vup_[2]);
+    const double theta = degrees_to_radians(vfov);
+    const double h = std::tan(theta / 2.0);
+    const double viewport_height = 2.0 * h * focus_dist;
+    const double viewport_width = viewport_height * ((double)image_width / (double)image_height);
+    const D3 w = unit_vector(lookfrom - lookat);
+    const D3 u = unit_vector(cross(vup, w));
+    const D3 v = cross(w, u);
+    const D3 viewport_u = u * viewport_width;
+    const D3 viewport_v = v * -viewport_height;
+    const D3 pixel_delta_u = viewport_u / (double)image_width;
+    const D3 pixel_delta_v = viewport_v / (double)image_height;
+    const D3 upper_left = lookfrom - (w * focus_dist) - viewport_u / 2.0 - viewport_v / 2.0;
+    const D3 pixel00 = upper_left + (pixel_delta_u + pixel_delta_v) * 0.5;
+    const double defocus_radius = focus_dist * std::tan(degrees_to_radians(defocus_angle / 2.0));
+
+    std::memset(cam, 0, sizeof(*cam));
+    put4(cam->origin, (float)lookfrom.x, (float)lookfrom.y, (float)lookfrom.z, 0.0f);
+    put4(cam->pixel00, (float)pixel00.x, (float)pixel00.y, (float)pixel00.z, 0.0f);
+    put4(cam->pixel_delta_u, (float)pixel_delta_u.x, (float)pixel_delta_u.y, (float)pixel_delta_u.z, 0.0f);
+    put4(cam->pixel_delta_v, (float)pixel_delta_v.x, (float)pixel_delta_v.y, (float)pixel_delta_v.z, 0.0f);
+    put4(cam->u, (float)u.x, (float)u.y, (float)u.z, 0.0f);
+    put4(cam->v, (float)v.x, (float)v.y, (float)v.z, 0.0f);
+    if (background) put4(cam->background, (float)background[0], (float)background[1], (float)background[2], 0.0f);
+    put4(cam->params_f, (float)defocus_radius, (float)image_width, (float)image_height, (float)samples_per_pixel);
+    cam->params_u[0] = (uint32_t)max_depth;
+    cam->params_u[1] = sample_seed;
+    cam->params_u[2] = n_spheres;
+    cam->params_u[3] = background ? 1u : 0u;
+    return RRT_OK;
+}
+
+int32_t rrt_build_in_one_weekend_scene(const RrtOverrides *ov, uint64_t seed, int32_t grid_half, RrtCamera *cam,
+                                       RrtSphere *spheres, RrtMaterial *materials, uint32_t sphere_cap,
+                                       uint32_t *n_spheres) {
+    if (!n_spheres) return fail(RRT_E_INVALID, "null n_spheres");
+    if (grid_half < 0 || grid_half > 1000) return fail(RRT_E_INVALID, "grid_half out of range");
+    double aspect_ratio = 16.0 / 9.0;
+    int32_t image_width = 1200, samples_per_pixel = 10, max_depth = 20;
+    double vfov = 20.0;
+    double lookfrom[3] = {13.0, 2.0, 3.0}, lookat[3] = {0.0, 0.0, 0.0}, vup[3] = {0.0, 1.0, 0.0};
+    double defocus_angle = 0.6, focus_dist = 10.0;
+    double background[3] = {0.0, 0.0, 0.0};
+    int32_t has_bg = 0;
+    rrt_apply_overrides(ov, 0, &aspect_ratio, &image_width, &samples_per_pixel, &max_depth, &vfov, lookfrom, lookat,
+                        vup, &defocus_angle, &focus_dist, background, &has_bg);
+
+    std::vector<RrtSphere> sph;
+    std::vector<RrtMaterial> mat;
+    auto add_material = [&](uint32_t kind, float r, float g, float b, float fuzz, float ref_idx) {
+        RrtMaterial m{};
+        put4(m.albedo_fuzz, r, g, b, fuzz);
+        m.kind = kind;
+        m.ref_idx = ref_idx;
+        mat.push_back(m);
+        return (uint32_t)(mat.size() - 1);
+    };
+    auto add_sphere = [&](float x, float y, float z, float r, uint32_t m) {
+        RrtSphere s{};
+        put4(s.center_radius, x, y, z, r);
+        s.material_index = m;
+        sph.push_back(s);
+    };
+    SmallRng rng(seed);
+    add_sphere(0.0f, -1000.0f, 0.0f, 1000.0f, add_material(0, 0.5f, 0.5f, 0.5f, 0.0f, 1.0f));
+    for (int a = -grid_half; a < grid_half; ++a) {
+        for (int b = -grid_half; b < grid_half; ++b) {
+            const float choose_mat = rng.gen_f32();
+            const double cx = (double)a + 0.9 * rng.gen_f64();
+            const double cz = (double)b + 0.9 * rng.gen_f64();
+            const D3 center = d3(cx, 0.2, cz);
+            if (length(center - d3(4.0, 0.2, 0.0)) > 0.9) {
+                uint32_t m;
+                if (choose_mat < 0.8f) {
+                    float alb[3];
+                    for (int c = 0; c < 3; ++c) {
+                        const float p = rng.gen_f32();
+                        const float q = rng.gen_f32();
+                        alb[c] = p * q;
+                    }
+                    m = add_material(0, alb[0], alb[1], alb[2], 0.0f, 1.0f);
+                } else if (choose_mat < 0.95f) {
+                    float alb[3];
+                    for (int c = 0; c < 3; ++c) alb[c] = rng.gen_range_f32(0.5f, 1.0f);
+                    const float fuzz = rng.gen_f32() * 0.5f;
+                    m = add_material(1, alb[0], alb[1], alb[2], fuzz, 1.0f);
+                } else {
+                    m = add_material(2, 1.0f, 1.0f, 1.0f, 0.0f, 1.5f);
+                }
+                add_sphere((float)center.x, (float)center.y, (float)center.z, 0.2f, m);
+            }
+        }
+    }
+    add_sphere(0.0f, 1.0f, 0.0f, 1.0f, add_material(2, 1.0f, 1.0f, 1.0f, 0.0f, 1.5f));
+    add_sphere(-4.0f, 1.0f, 0.0f, 1.0f, add_material(0, 0.4f, 0.2f, 0.1f, 0.0f, 1.0f));
+    add_sphere(4.0f, 1.0f, 0.0f, 1.0f, add_material(1, 0.7f, 0.6f, 0.5f, 0.0f, 1.0f));
+    const uint32_t sample_seed = rng.next_u32();
+
+    *n_spheres = (uint32_t)sph.size();
+    if (cam) {
+        int rc = rrt_make_camera(aspect_ratio, image_width, samples_per_pixel, max_depth, vfov, lookfrom, lookat, vup,
+                                 defocus_angle, focus_dist, has_bg ? background : nullptr, sample_seed,
+                                 (uint32_t)sph.size(), cam);
+        if (rc) return rc;
+    }
+    if (sphere_cap == 0) return RRT_OK;
+    if (sphere_cap < sph.size() || !spheres || !materials)
+        return fail(RRT_E_INVALID, "sphere_cap too small (need " + std::to_string(sph.size()) + ")");
+    std::memcpy(spheres, sph.data(), sph.size() * sizeof(RrtSphere));
+    std::memcpy(materials, mat.data(), mat.size() * sizeof(RrtMaterial));
+    return RRT_OK;
+}
+
+// ---- render_io.rs:3-31 -------------------------------------------------------------------
+static inline uint8_t quantize_channel(float x, float scale) {
+    float r = x * scale;
+    if (!std::isfinite(r)) r = 0.0f;
+    r = std::sqrt(r < 0.0f ? 0.0f : r);
+    if (r < 0.0f) r = 0.0f;  // f32::clamp(0.0, 0.999)
+    if (r > 0.999f) r = 0.999f;
+    return (uint8_t)(int)(r * 256.0f);
+}
+
+int32_t rrt_quantize_accum(uint32_t width, uint32_t height, const float *accum, uint32_t spp, uint8_t *rgb8) {
+    if ((!accum || !rgb8) && (size_t)width * height) return fail(RRT_E_INVALID, "null accum or rgb8");
+    const float scale = spp > 0 ? 1.0f / (float)spp : 0.0f;
+    const size_t n = (size_t)width * height;
+    for (size_t i = 0; i < n; ++i)
+        for (int c = 0; c < 3; ++c) rgb8[i * 3 + c] = quantize_channel(accum[i * 4 + c], scale);
+    return RRT_OK;
+}
+
+int32_t rrt_format_ppm_from_accum(uint32_t width, uint32_t height, const float *accum, uint32_t spp, char *buf,
+                                  size_t cap, size_t *written) {
+    if (!written) return fail(RRT_E_INVALID, "null written");
+    if (!accum && (size_t)width * height) return fail(RRT_E_INVALID, "null accum");
+    std::string out;
+    out.reserve((size_t)width * height * 12 + 32);
+    out += "P3\n" + std::to_string(width) + " " + std::to_string(height) + "\n255\n";
+    const float scale = spp > 0 ? 1.0f / (float)spp : 0.0f;
+    char line[16];
+    for (size_t i = 0, n = (size_t)width * height; i < n; ++i) {
+        const int len = std::snprintf(line, sizeof(line), "%u %u %u\n", quantize_channel(accum[i * 4], scale),
+                                      quantize_channel(accum[i * 4 + 1], scale), quantize_channel(accum[i * 4 + 2], scale));
+        out.append(line, (size_t)len);
+    }
+    *written = out.size();
+    if (cap == 0) return RRT_OK;
+    if (!buf || cap < out.size()) return fail(RRT_E_INVALID, "buffer too small");
+    std::memcpy(buf, out.data(), out.size());
+    return RRT_OK;
+}
+
+int32_t rrt_write_ppm_from_accum(uint32_t width, uint32_t height, const float *accum, uint32_t spp, const char *path) {
+    size_t n = 0;
+    if (int rc = rrt_format_ppm_from_accum(width, height, accum, spp, nullptr, 0, &n)) return rc;
+    std::vector<char> buf(n);
+    if (int rc = rrt_format_ppm_from_accum(width, height, accum, spp, buf.data(), n, &n)) return rc;
+    FILE *f = (!path || std::strcmp(path, "-") == 0) ? stdout : std::fopen(path, "wb");
+    if (!f) return fail(RRT_E_IO, std::string("cannot open ") + path);
+    const size_t w = std::fwrite(buf.data(), 1, n, f);
+    if (f == stdout) std::fflush(f);
+    else std::fclose(f);
+    if (w != n) return fail(RRT_E_IO, "short write");
+    return RRT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,87 @@
+// rrt_internal.h — layouts shared by the host runtime (rrt_host.cpp) and the gfx950
+// megakernel (rrt_kernel.hip). Not part of the public C-ABI (include/rrt_hip.h).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rrt {
+
+// BVH2 node, 64 B, both children's boxes stored in the parent so one node fetch
+// (4 x dwordx4) tests both children. Boxes are f32, rounded outward from the f64
+// SAH build (bvh.rs:21-156 criterion) so they conservatively contain the spheres.
+//   b0 = c0.lo.x c0.hi.x c0.lo.y c0.hi.y
+//   b1 = c0.lo.z c0.hi.z c1.lo.x c1.hi.x
+//   b2 = c1.lo.y c1.hi.y c1.lo.z c1.hi.z
+//   link.x/.y = child ref (internal: node index; leaf: first primitive)
+//   link.z/.w = child primitive count (0 = internal node)
+struct alignas(16) GNode {
+    float4 b0;
+    float4 b1;
+    float4 b2;
+    int4 link;
+};
+static_assert(sizeof(GNode) == 64, "GNode must be 64 B");
+
+// Material, SoA split into two 16-B records (kind-dependent payload).
+//   a = albedo.rgb (or emitted rgb for lights), fuzz (pre-clamped to <= 1, material.rs:49)
+//   b = kind, ref_idx bits, texture index, 0
+struct alignas(16) GMaterial {
+    float4 a;
+    int4 b;
+};
+
+struct GTexture {
+    int32_t offset;  // byte offset into the texture pool
+    int32_t width;
+    int32_t height;
+    int32_t pad;
+};
+
+// Everything the megakernel needs, passed by value (kernarg segment).
+struct KParams {
+    const GNode *nodes;
+    const float4 *prim_cr;       // sphere center.xyz, radius — in BVH leaf order
+    const uint32_t *prim_mat;    // material index per primitive (leaf order)
+    const GMaterial *mats;
+    const uint8_t *tex_pool;
+    const GTexture *texs;
+    float4 *accum;               // tile-local rows * width
+    unsigned long long *counters;  // RrtCounters layout (5 x u64)
+
+    // camera (f32, from the RrtCamera ABI; disk_u/v = u/v * defocus_radius in f32)
+    float p00[3];
+    float du[3];
+    float dv[3];
+    float center[3];
+    float disk_u[3];
+    float disk_v[3];
+    float background[3];
+    float defocus_radius;
+
+    uint32_t max_depth;
+    uint32_t seed;
+    uint32_t bg_mode;
+    uint32_t flags;
+
+    uint32_t width;
+    uint32_t height;
+    uint32_t tile_rows;     // rows owned by this tile
+    uint32_t band_rows;
+    uint32_t rank;
+    uint32_t n_ranks;
+    uint32_t sample_begin;
+    uint32_t sample_end;
+    uint32_t n_work_tiles;  // 8x8 pixel tiles in this tile
+    uint32_t tiles_x;
+};
+
+// Traversal stack depth held in LDS per lane (entries = max BVH depth - 1 suffices).
+constexpr int kStackDepth = 40;
+constexpr int kBlock = 256;
+
+// Launch wrappers implemented in rrt_kernel.hip.
+hipError_t launch_render(const KParams &p, hipStream_t stream);
+hipError_t launch_render_counting(const KParams &p, hipStream_t stream);
+
+}  // namespace rrt

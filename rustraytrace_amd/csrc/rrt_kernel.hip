@@ -1,0 +1,452 @@
+// rrt_kernel.hip — gfx950 (CDNA4) path-tracing megakernel.
+//
+// One lane owns one pixel and runs that pixel's samples [sample_begin, sample_end) in
+// order, regenerating a new camera ray in place whenever a path ends (path
+// regeneration), so no lane idles while others finish long paths and the per-pixel sum
+// is accumulated in fixed sample order (deterministic, no float atomics).
+// Each 64-lane wave covers one 8x8 pixel tile (coherent camera rays); a 256-thread block
+// holds 4 tiles. BVH2 traversal is iterative, nearest-child-first, with the node stack in
+// LDS laid out [depth][lane] (conflict-free: consecutive lanes hit consecutive banks).
+//
+// Semantics follow the reference's CPU "books" path (NOT src/cuda, Appendix A of SURVEY):
+//   camera ray       in_one_weekend/camera.rs:152-180  (+ time draw the_next_week/camera.rs:160)
+//   closest hit      camera.rs:187 over (0.001, +inf), sphere.rs:24-51 open interval
+//   Aabb slab test   aabb.rs:52-85
+//   scatter          material.rs:28-40 / 53-64 / 83-102, vec3.rs:181-189, 201-210
+//   Russian roulette camera.rs:189-200 (this bounce's attenuation, clamp [.05,.95])
+//   sky / background camera.rs:206-208 / the_next_week/camera.rs:179-181
+//   emission, texture the_next_week/material.rs:41-53,131-135, texture.rs:177-196, sphere.rs:46-52
+// in f32 with every operation in the reference's order and no contraction (built with
+// -ffp-contract=off and correctly rounded f32 div/sqrt) so the CPU oracle (oracle/) can
+// reproduce each sample bit for bit. Throughput is carried front-to-back
+// (T <- T*att[*1/p]); the reference multiplies back-to-front through its recursion —
+// equal in exact arithmetic (documented in DESIGN.md).
+#include "rrt_internal.h"
+
+namespace rrt {
+namespace {
+
+struct V3 {
+    float x, y, z;
+};
+
+__device__ __forceinline__ V3 v3(float x, float y, float z) { return V3{x, y, z}; }
+__device__ __forceinline__ V3 add(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ V3 sub(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ V3 mul(V3 a, V3 b) { return v3(a.x * b.x, a.y * b.y, a.z * b.z); }
+__device__ __forceinline__ V3 muls(V3 a, float s) { return v3(a.x * s, a.y * s, a.z * s); }
+// vec3.rs:156-158 dot = (u0*v0 + u1*v1) + u2*v2
+__device__ __forceinline__ float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+// vec3.rs:168-170 unit_vector = v * (1/len)  (Div<f64> is `(1.0/rhs) * self`, vec3.rs:142-148)
+__device__ __forceinline__ V3 unit(V3 v) {
+    const float inv = 1.0f / __builtin_sqrtf(dot(v, v));
+    return muls(v, inv);
+}
+
+// ---- RNG: PCG32 (XSH-RR 64/32) per path, keyed by (seed, pixel, sample) --------------------
+// Counter-based in effect: the i-th draw of a path is a pure function of
+// (seed, global pixel index, sample index, i); nothing depends on lane or launch shape.
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+    z += 0x9e3779b97f4a7c15ull;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ uint32_t pcg_next(uint64_t &s) {
+    const uint64_t old = s;
+    s = old * 6364136223846793005ull + 1442695040888963407ull;
+    const uint32_t xs = (uint32_t)(((old >> 18) ^ old) >> 27);
+    const uint32_t rot = (uint32_t)(old >> 59);
+    return (xs >> rot) | (xs << ((32u - rot) & 31u));
+}
+// random_double(): 24-bit uniform in [0,1) (exact in f32 and f64).
+__device__ __forceinline__ float rnd(uint64_t &s) { return (float)(pcg_next(s) >> 8) * 0x1.0p-24f; }
+// random_double_range(lo,hi) = u*(hi-lo) + lo  (rand 0.8 UniformFloat::sample_single order)
+__device__ __forceinline__ float rnd_range(uint64_t &s, float lo, float hi) { return rnd(s) * (hi - lo) + lo; }
+
+// vec3.rs:181-189 random_unit_vector: rejection in [-1,1)^3, accept 1e-160 < |p|^2 <= 1
+// (1e-160 underflows to 0 in f32: the one intentional f32 deviation).
+__device__ __forceinline__ V3 random_unit_vector(uint64_t &s) {
+    for (;;) {
+        const float px = rnd_range(s, -1.0f, 1.0f);
+        const float py = rnd_range(s, -1.0f, 1.0f);
+        const float pz = rnd_range(s, -1.0f, 1.0f);
+        const float lensq = px * px + py * py + pz * pz;
+        if (0.0f < lensq && lensq <= 1.0f) {
+            const float inv = 1.0f / __builtin_sqrtf(lensq);
+            return v3(px * inv, py * inv, pz * inv);
+        }
+    }
+}
+
+// vec3.rs:201-203 reflect = v - n*(2*dot(v,n))
+__device__ __forceinline__ V3 reflect(V3 v, V3 n) { return sub(v, muls(n, 2.0f * dot(v, n))); }
+
+// vec3.rs:205-210 refract
+__device__ __forceinline__ V3 refract(V3 uv, V3 n, float e) {
+    float c = -dot(uv, n);
+    c = (c < 1.0f) ? c : 1.0f;
+    const V3 perp = muls(add(uv, muls(n, c)), e);
+    const float k = __builtin_fabsf(1.0f - dot(perp, perp));
+    const V3 par = muls(n, -__builtin_sqrtf(k));
+    return add(perp, par);
+}
+
+// material.rs:75-80 Schlick; powi(5) expands to x*((x*x)*(x*x)).
+__device__ __forceinline__ float reflectance(float cosine, float ri) {
+    float r0 = (1.0f - ri) / (1.0f + ri);
+    r0 = r0 * r0;
+    const float x = 1.0f - cosine;
+    const float x2 = x * x;
+    const float x4 = x2 * x2;
+    const float x5 = x * x4;
+    return r0 + (1.0f - r0) * x5;
+}
+
+// ---- deterministic f32 acos / atan2 for sphere UV (sphere.rs:46-52) -------------------------
+// Cephes single-precision polynomials, only + - * / sqrt, replicated bit-for-bit by the oracle.
+constexpr float kPi = 3.14159265358979323846f;
+constexpr float kPiO2 = 1.57079632679489661923f;
+constexpr float kPiO4 = 0.78539816339744830962f;
+
+__device__ __forceinline__ float asin_core(float x) {  // |x| <= 0.5 polynomial, z = x*x
+    const float z = x * x;
+    return ((((4.2163199048e-2f * z + 2.4181311049e-2f) * z + 4.5470025998e-2f) * z + 7.4953002686e-2f) * z +
+            1.6666752422e-1f) * z * x + x;
+}
+__device__ __forceinline__ float rrt_acosf(float x) {
+    if (x < -0.5f) return kPi - 2.0f * asin_core(__builtin_sqrtf(0.5f * (1.0f + x)));
+    if (x > 0.5f) return 2.0f * asin_core(__builtin_sqrtf(0.5f * (1.0f - x)));
+    return kPiO2 - asin_core(x);
+}
+__device__ __forceinline__ float rrt_atanf(float x) {
+    float sgn = 1.0f;
+    if (x < 0.0f) { sgn = -1.0f; x = -x; }
+    float y = 0.0f;
+    if (x > 2.414213562373095f) { y = kPiO2; x = -1.0f / x; }
+    else if (x > 0.4142135623730950f) { y = kPiO4; x = (x - 1.0f) / (x + 1.0f); }
+    const float z = x * x;
+    y = y + ((((8.05374449538e-2f * z - 1.38776856032e-1f) * z + 1.99777106478e-1f) * z - 3.33329491539e-1f) * z * x + x);
+    return sgn * y;
+}
+__device__ __forceinline__ float rrt_atan2f(float y, float x) {
+    if (x == 0.0f) {
+        if (y > 0.0f) return kPiO2;
+        if (y < 0.0f) return -kPiO2;
+        return 0.0f;
+    }
+    float z = rrt_atanf(y / x);
+    if (x < 0.0f) z = (y < 0.0f) ? z - kPi : z + kPi;
+    return z;
+}
+
+// ---- Aabb::hit (aabb.rs:52-85), books branch structure incl. NaN behaviour -----------------
+__device__ __forceinline__ bool slab(float lo, float hi, float o, float adinv, float &tmin, float &tmax) {
+    const float t0 = (lo - o) * adinv;
+    const float t1 = (hi - o) * adinv;
+    if (t0 < t1) {
+        if (t0 > tmin) tmin = t0;
+        if (t1 < tmax) tmax = t1;
+    } else {
+        if (t1 > tmin) tmin = t1;
+        if (t0 < tmax) tmax = t0;
+    }
+    return !(tmax <= tmin);
+}
+__device__ __forceinline__ bool box_hit(float lx, float hx, float ly, float hy, float lz, float hz,
+                                        V3 o, V3 inv, float tmin, float tmax, float &tnear) {
+    if (!slab(lx, hx, o.x, inv.x, tmin, tmax)) return false;
+    if (!slab(ly, hy, o.y, inv.y, tmin, tmax)) return false;
+    if (!slab(lz, hz, o.z, inv.z, tmin, tmax)) return false;
+    tnear = tmin;
+    return true;
+}
+
+struct Counters {
+    uint32_t rays, paths, nodes, boxes, spheres;
+};
+
+// Sphere::hit (sphere.rs:24-51) root selection; returns true and shrinks `closest`.
+template <bool kCount>
+__device__ __forceinline__ void test_prims(const float4 *__restrict__ prim_cr, int first, int count, V3 o, V3 d,
+                                           float a, float &closest, int &hit_prim, Counters &cnt) {
+    for (int i = first; i < first + count; ++i) {
+        if (kCount) cnt.spheres++;
+        const float4 cr = prim_cr[i];
+        const V3 oc = v3(cr.x - o.x, cr.y - o.y, cr.z - o.z);
+        const float h = dot(d, oc);
+        const float c = dot(oc, oc) - cr.w * cr.w;
+        const float disc = h * h - a * c;
+        if (disc < 0.0f) continue;
+        const float sq = __builtin_sqrtf(disc);
+        float root = (h - sq) / a;
+        if (!(0.001f < root && root < closest)) {
+            root = (h + sq) / a;
+            if (!(0.001f < root && root < closest)) continue;
+        }
+        closest = root;
+        hit_prim = i;
+    }
+}
+
+template <bool kCount>
+__device__ __forceinline__ int trace(const KParams &P, int *__restrict__ stack, V3 o, V3 d, float &t_hit, Counters &cnt) {
+    const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    const float a = dot(d, d);
+    float closest = __builtin_inff();
+    int hit_prim = -1;
+    int node = 0;
+    int sp = 0;
+    for (;;) {
+        const GNode n = P.nodes[node];
+        if (kCount) { cnt.nodes++; cnt.boxes += 2; }
+        float tn0 = 0.0f, tn1 = 0.0f;
+        bool h0 = box_hit(n.b0.x, n.b0.y, n.b0.z, n.b0.w, n.b1.x, n.b1.y, o, inv, 0.001f, closest, tn0);
+        bool h1 = box_hit(n.b1.z, n.b1.w, n.b2.x, n.b2.y, n.b2.z, n.b2.w, o, inv, 0.001f, closest, tn1);
+        if (h0 && n.link.z > 0) {
+            test_prims<kCount>(P.prim_cr, n.link.x, n.link.z, o, d, a, closest, hit_prim, cnt);
+            h0 = false;
+        }
+        if (h1 && n.link.w > 0) {
+            test_prims<kCount>(P.prim_cr, n.link.y, n.link.w, o, d, a, closest, hit_prim, cnt);
+            h1 = false;
+        }
+        if (h0 && h1) {
+            const bool first1 = tn1 < tn0;
+            stack[sp * kBlock] = first1 ? n.link.x : n.link.y;
+            ++sp;
+            node = first1 ? n.link.y : n.link.x;
+        } else if (h0) {
+            node = n.link.x;
+        } else if (h1) {
+            node = n.link.y;
+        } else {
+            if (sp == 0) break;
+            --sp;
+            node = stack[sp * kBlock];
+        }
+    }
+    t_hit = closest;
+    return hit_prim;
+}
+
+struct PathState {
+    V3 o, d, T, L;
+    uint64_t rng;
+    uint32_t k;  // bounce index (camera ray = 0)
+};
+
+// Camera::get_ray (camera.rs:152-180) for global pixel (x, y) and the path's RNG.
+__device__ __forceinline__ void camera_ray(const KParams &P, uint32_t x, uint32_t y, PathState &ps) {
+    const float ox = rnd(ps.rng) - 0.5f;
+    const float oy = rnd(ps.rng) - 0.5f;
+    const float fi = (float)x + ox;
+    const float fj = (float)y + oy;
+    const V3 sample = v3(P.p00[0] + P.du[0] * fi + P.dv[0] * fj,
+                         P.p00[1] + P.du[1] * fi + P.dv[1] * fj,
+                         P.p00[2] + P.du[2] * fi + P.dv[2] * fj);
+    V3 origin = v3(P.center[0], P.center[1], P.center[2]);
+    if (P.defocus_radius > 0.0f) {
+        float px, py;
+        for (;;) {  // vec3.rs:172-179 random_in_unit_disk
+            px = rnd_range(ps.rng, -1.0f, 1.0f);
+            py = rnd_range(ps.rng, -1.0f, 1.0f);
+            if (px * px + py * py < 1.0f) break;
+        }
+        origin = v3(P.center[0] + P.disk_u[0] * px + P.disk_v[0] * py,
+                    P.center[1] + P.disk_u[1] * px + P.disk_v[1] * py,
+                    P.center[2] + P.disk_u[2] * px + P.disk_v[2] * py);
+    }
+    if (P.flags & 0x1u) (void)rnd(ps.rng);  // RRT_FLAG_RAY_TIME
+    ps.o = origin;
+    ps.d = sub(sample, origin);
+    ps.T = v3(1.0f, 1.0f, 1.0f);
+    ps.L = v3(0.0f, 0.0f, 0.0f);
+    ps.k = 0;
+}
+
+__device__ __forceinline__ V3 texel(const KParams &P, int tex, float u, float v) {
+    const GTexture t = P.texs[tex];
+    if (t.height <= 0) return v3(0.0f, 1.0f, 1.0f);  // texture.rs:179-181
+    u = (u < 0.0f) ? 0.0f : ((u > 1.0f) ? 1.0f : u);  // Interval::clamp
+    v = 1.0f - ((v < 0.0f) ? 0.0f : ((v > 1.0f) ? 1.0f : v));
+    int i = (int)(u * (float)t.width);
+    int j = (int)(v * (float)t.height);
+    i = (i < 0) ? 0 : ((i < t.width) ? i : t.width - 1);  // rtw_image.rs:326-334
+    j = (j < 0) ? 0 : ((j < t.height) ? j : t.height - 1);
+    const uint8_t *px = P.tex_pool + t.offset + ((size_t)j * t.width + i) * 3;
+    const float cs = 1.0f / 255.0f;
+    return v3(cs * (float)px[0], cs * (float)px[1], cs * (float)px[2]);
+}
+
+// One bounce: closest hit, then scatter / RR. Returns true when the path has ended.
+template <bool kCount>
+__device__ __forceinline__ bool bounce(const KParams &P, int *stack, PathState &ps, Counters &cnt) {
+    if (ps.k >= P.max_depth) return true;  // ray_color: depth <= 0 -> 0
+    float t;
+    if (kCount) cnt.rays++;
+    else cnt.rays++;
+    const int prim = trace<kCount>(P, stack, ps.o, ps.d, t, cnt);
+    if (prim < 0) {
+        V3 bg;
+        if (P.bg_mode == 1u) {
+            bg = v3(P.background[0], P.background[1], P.background[2]);
+        } else {
+            const V3 ud = unit(ps.d);
+            const float a = 0.5f * (ud.y + 1.0f);
+            bg = v3((1.0f - a) * 1.0f + a * 0.5f, (1.0f - a) * 1.0f + a * 0.7f, (1.0f - a) * 1.0f + a * 1.0f);
+        }
+        ps.L = add(ps.L, mul(ps.T, bg));
+        return true;
+    }
+    // HitRecord (sphere.rs:47-50, hittable.rs:20-32)
+    const float4 cr = P.prim_cr[prim];
+    const V3 p = v3(ps.o.x + ps.d.x * t, ps.o.y + ps.d.y * t, ps.o.z + ps.d.z * t);
+    const float inv_r = 1.0f / cr.w;
+    const V3 outward = v3((p.x - cr.x) * inv_r, (p.y - cr.y) * inv_r, (p.z - cr.z) * inv_r);
+    const bool front = dot(ps.d, outward) < 0.0f;
+    const V3 nrm = front ? outward : v3(-outward.x, -outward.y, -outward.z);
+    const GMaterial m = P.mats[P.prim_mat[prim]];
+    const int kind = m.b.x;
+    V3 att;
+    V3 dir;
+    if (kind == 4) {  // DiffuseLight: emitted, scatter None
+        ps.L = add(ps.L, mul(ps.T, v3(m.a.x, m.a.y, m.a.z)));
+        return true;
+    } else if (kind == 0 || kind == 3) {  // Lambertian (material.rs:28-40)
+        const V3 r = random_unit_vector(ps.rng);
+        dir = add(nrm, r);
+        if (__builtin_fabsf(dir.x) < 1e-8f && __builtin_fabsf(dir.y) < 1e-8f && __builtin_fabsf(dir.z) < 1e-8f) dir = nrm;
+        if (kind == 3) {
+            const float theta = rrt_acosf(-outward.y);
+            const float phi = rrt_atan2f(-outward.z, outward.x) + kPi;
+            att = texel(P, m.b.z, phi / (2.0f * kPi), theta / kPi);
+        } else {
+            att = v3(m.a.x, m.a.y, m.a.z);
+        }
+    } else if (kind == 1) {  // Metal (material.rs:53-64)
+        const V3 refl = unit(reflect(ps.d, nrm));
+        const V3 r = random_unit_vector(ps.rng);
+        dir = add(refl, muls(r, m.a.w));
+        if (!(dot(dir, nrm) > 0.0f)) return true;  // absorbed
+        att = v3(m.a.x, m.a.y, m.a.z);
+    } else {  // Dielectric (material.rs:83-102)
+        const float eta = __int_as_float(m.b.y);
+        const float ri = front ? (1.0f / eta) : eta;
+        const V3 ud = unit(ps.d);
+        float c = -dot(ud, nrm);
+        c = (c < 1.0f) ? c : 1.0f;
+        const float s = __builtin_sqrtf(1.0f - c * c);
+        const bool cannot = ri * s > 1.0f;
+        if (cannot || reflectance(c, ri) > rnd(ps.rng)) dir = reflect(ud, nrm);
+        else dir = refract(ud, nrm, ri);
+        att = v3(1.0f, 1.0f, 1.0f);
+    }
+    if (ps.k >= 5u) {  // camera.rs:189-200
+        float pr = att.x;
+        if (att.y > pr) pr = att.y;
+        if (att.z > pr) pr = att.z;
+        if (pr < 0.05f) pr = 0.05f;
+        if (pr > 0.95f) pr = 0.95f;
+        if (rnd(ps.rng) > pr) return true;
+        ps.T = muls(mul(ps.T, att), 1.0f / pr);
+    } else {
+        ps.T = mul(ps.T, att);
+    }
+    ps.o = p;
+    ps.d = dir;
+    ps.k++;
+    return false;
+}
+
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+template <bool kCount>
+__device__ __forceinline__ void render_body(const KParams &P) {
+    __shared__ int lds_stack[kStackDepth * kBlock];
+    int *stack = lds_stack + threadIdx.x;
+
+    const uint32_t wave = threadIdx.x >> 6;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t tile = blockIdx.x * (kBlock / 64) + wave;
+    Counters cnt = {0, 0, 0, 0, 0};
+    bool active = tile < P.n_work_tiles;
+    uint32_t x = 0, ly = 0;
+    if (active) {
+        const uint32_t tx = tile % P.tiles_x;
+        const uint32_t ty = tile / P.tiles_x;
+        x = tx * 8u + (lane & 7u);
+        ly = ty * 8u + (lane >> 3);
+        active = x < P.width && ly < P.tile_rows;
+    }
+    if (active) {
+        // tile-local row -> global image row (row bands dealt round-robin over ranks)
+        const uint32_t band = ly / P.band_rows;
+        const uint32_t y = (band * P.n_ranks + P.rank) * P.band_rows + ly % P.band_rows;
+        const uint32_t pixel = y * P.width + x;
+        const uint64_t key = splitmix64(((uint64_t)P.seed << 32) ^ (uint64_t)pixel);
+
+        V3 sum = v3(0.0f, 0.0f, 0.0f);
+        uint32_t s = P.sample_begin;
+        PathState ps;
+        if (s < P.sample_end) {
+            ps.rng = splitmix64(key + s);
+            camera_ray(P, x, y, ps);
+        }
+        while (s < P.sample_end) {
+            if (bounce<kCount>(P, stack, ps, cnt)) {
+                sum = add(sum, ps.L);  // pixel_color += ray_color(..) (camera.rs:73-76)
+                cnt.paths++;
+                ++s;
+                if (s < P.sample_end) {
+                    ps.rng = splitmix64(key + s);
+                    camera_ray(P, x, y, ps);
+                }
+            }
+        }
+        P.accum[(size_t)ly * P.width + x] = make_float4(sum.x, sum.y, sum.z, (float)(P.sample_end - P.sample_begin));
+    }
+    // one atomic per wave per counter
+    const uint32_t r = wave_sum_u32(cnt.rays);
+    const uint32_t pa = wave_sum_u32(cnt.paths);
+    uint32_t nv = 0, bt = 0, st = 0;
+    if (kCount) {
+        nv = wave_sum_u32(cnt.nodes);
+        bt = wave_sum_u32(cnt.boxes);
+        st = wave_sum_u32(cnt.spheres);
+    }
+    if (lane == 0) {
+        if (r) atomicAdd(&P.counters[0], (unsigned long long)r);
+        if (pa) atomicAdd(&P.counters[1], (unsigned long long)pa);
+        if (kCount) {
+            atomicAdd(&P.counters[2], (unsigned long long)nv);
+            atomicAdd(&P.counters[3], (unsigned long long)bt);
+            atomicAdd(&P.counters[4], (unsigned long long)st);
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void rrt_render(KParams P) { render_body<false>(P); }
+__global__ __launch_bounds__(kBlock) void rrt_render_counting(KParams P) { render_body<true>(P); }
+
+}  // namespace
+
+hipError_t launch_render(const KParams &p, hipStream_t stream) {
+    const uint32_t blocks = (p.n_work_tiles + (kBlock / 64) - 1) / (kBlock / 64);
+    if (blocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(rrt_render, dim3(blocks), dim3(kBlock), 0, stream, p);
+    return hipGetLastError();
+}
+
+hipError_t launch_render_counting(const KParams &p, hipStream_t stream) {
+    const uint32_t blocks = (p.n_work_tiles + (kBlock / 64) - 1) / (kBlock / 64);
+    if (blocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(rrt_render_counting, dim3(blocks), dim3(kBlock), 0, stream, p);
+    return hipGetLastError();
+}
+
+}  // namespace rrt

@@ -1,0 +1,156 @@
+"""Render entry points over the C-ABI, mirroring the reference's Rust surface:
+
+* `render_in_one_weekend()`  == cuda::render_in_one_weekend (cuda/mod.rs:337-340, 442-445)
+* `render(scene)`            == cuda::imp::render(camera, &spheres, &materials) (cuda/mod.rs:342-439)
+                                returning the RGBA accum instead of printing it
+* `write_ppm_from_accum`     == render_io::write_ppm_from_accum (render_io.rs:3-31)
+* `DeviceScene`              device-resident scene for benches / multi-rank hosts
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional
+
+import numpy as np
+
+from . import _lib
+from .scenes import SceneData, build_in_one_weekend_scene, COMMITTED_OVERRIDES
+
+
+def _textures(scene: SceneData):
+    if not scene.textures:
+        return None, 0, []
+    arr = (_lib.RrtTexture * len(scene.textures))()
+    keep = []
+    for i, t in enumerate(scene.textures):
+        t = np.ascontiguousarray(t, dtype=np.uint8)
+        assert t.ndim == 3 and t.shape[2] == 3, "textures are (H, W, 3) RGB8"
+        keep.append(t)
+        arr[i].rgb8 = t.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+        arr[i].height, arr[i].width = int(t.shape[0]), int(t.shape[1])
+    return arr, len(scene.textures), keep
+
+
+def render(scene: SceneData, spp: Optional[int] = None, n_gpus: int = 1, quiet: bool = True) -> np.ndarray:
+    """Render `scene` on `n_gpus` GPUs; returns the RGBA float32 accum (H, W, 4), w = sample count."""
+    lib = _lib.load()
+    accum = np.zeros((scene.height, scene.width, 4), dtype=np.float32)
+    tex, ntex, keep = _textures(scene)
+    flags = scene.flags | (_lib.FLAG_QUIET if quiet else 0)
+    _lib.check(lib.rrt_hip_render(_lib.ptr(scene.camera), _lib.ptr(scene.spheres), len(scene.spheres),
+                                  _lib.ptr(scene.materials), len(scene.materials),
+                                  ctypes.cast(tex, ctypes.c_void_p) if tex is not None else None, ntex,
+                                  int(spp or 0), int(n_gpus), flags, _lib.ptr(accum)))
+    del keep
+    return accum
+
+
+def render_in_one_weekend(path: str = "-", n_gpus: int = 1, overrides: Optional[dict] = None) -> None:
+    """cuda::render_in_one_weekend: RTOW scene under config::OVERRIDES -> P3 PPM on stdout (or `path`)."""
+    scene = build_in_one_weekend_scene(COMMITTED_OVERRIDES if overrides is None else overrides)
+    accum = render(scene, n_gpus=n_gpus, quiet=False)
+    write_ppm_from_accum(scene.width, scene.height, accum, scene.spp, path)
+
+
+def write_ppm_from_accum(width: int, height: int, accum: np.ndarray, samples_per_pixel: int, path: str = "-") -> None:
+    accum = np.ascontiguousarray(accum, dtype=np.float32)
+    assert accum.size == width * height * 4
+    _lib.check(_lib.load().rrt_write_ppm_from_accum(width, height, _lib.ptr(accum), samples_per_pixel,
+                                                    path.encode()))
+
+
+def format_ppm_from_accum(width: int, height: int, accum: np.ndarray, samples_per_pixel: int) -> bytes:
+    lib = _lib.load()
+    accum = np.ascontiguousarray(accum, dtype=np.float32)
+    assert accum.size == width * height * 4
+    n = ctypes.c_size_t(0)
+    _lib.check(lib.rrt_format_ppm_from_accum(width, height, _lib.ptr(accum), samples_per_pixel, None, 0,
+                                             ctypes.byref(n)))
+    buf = ctypes.create_string_buffer(n.value)
+    _lib.check(lib.rrt_format_ppm_from_accum(width, height, _lib.ptr(accum), samples_per_pixel, buf, n.value,
+                                             ctypes.byref(n)))
+    return buf.raw[: n.value]
+
+
+def quantize_accum(width: int, height: int, accum: np.ndarray, samples_per_pixel: int) -> np.ndarray:
+    accum = np.ascontiguousarray(accum, dtype=np.float32)
+    out = np.zeros((height, width, 3), dtype=np.uint8)
+    _lib.check(_lib.load().rrt_quantize_accum(width, height, _lib.ptr(accum), samples_per_pixel, _lib.ptr(out)))
+    return out
+
+
+def device_count() -> int:
+    n = ctypes.c_int32(0)
+    _lib.check(_lib.load().rrt_device_count(ctypes.byref(n)))
+    return n.value
+
+
+class DeviceScene:
+    """RrtScene*: scene + BVH resident on one device; renders tiles asynchronously on a stream."""
+
+    def __init__(self, scene: SceneData, device: int = 0):
+        lib = _lib.load()
+        self.scene = scene
+        self._lib = lib
+        self._h = ctypes.c_void_p()
+        tex, ntex, keep = _textures(scene)
+        _lib.check(lib.rrt_scene_create(_lib.ptr(scene.camera), _lib.ptr(scene.spheres), len(scene.spheres),
+                                        _lib.ptr(scene.materials), len(scene.materials),
+                                        ctypes.cast(tex, ctypes.c_void_p) if tex is not None else None, ntex,
+                                        scene.flags, int(device), ctypes.byref(self._h)))
+        del keep
+
+    def close(self):
+        if self._h:
+            self._lib.rrt_scene_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @staticmethod
+    def tile(band_rows=16, rank=0, n_ranks=1, sample_begin=0, sample_end=None, spp=None) -> _lib.RrtTile:
+        t = _lib.RrtTile()
+        t.band_rows, t.rank, t.n_ranks = band_rows, rank, n_ranks
+        t.sample_begin = sample_begin
+        t.sample_end = sample_end if sample_end is not None else (sample_begin + (spp or 0))
+        return t
+
+    def tile_rows(self, tile) -> int:
+        n = ctypes.c_uint32(0)
+        _lib.check(self._lib.rrt_tile_rows(self._h, ctypes.byref(tile), ctypes.byref(n)))
+        return n.value
+
+    def tile_row_indices(self, tile) -> np.ndarray:
+        rows = self.tile_rows(tile)
+        out = np.empty(rows, dtype=np.int64)
+        r = ctypes.c_uint32(0)
+        for i in range(rows):
+            _lib.check(self._lib.rrt_tile_row_index(self._h, ctypes.byref(tile), i, ctypes.byref(r)))
+            out[i] = r.value
+        return out
+
+    def render_tile_async(self, tile, d_accum_ptr: int, stream_ptr: int = 0) -> None:
+        _lib.check(self._lib.rrt_render_tile_async(self._h, ctypes.byref(tile), ctypes.c_void_p(d_accum_ptr),
+                                                   ctypes.c_void_p(stream_ptr)))
+
+    def counters(self) -> dict:
+        c = _lib.RrtCounters()
+        _lib.check(self._lib.rrt_scene_read_counters(self._h, ctypes.byref(c)))
+        return c.as_dict()
+
+    def reset_counters(self) -> None:
+        _lib.check(self._lib.rrt_scene_reset_counters(self._h))
+
+    def count_work(self, tile) -> dict:
+        c = _lib.RrtCounters()
+        _lib.check(self._lib.rrt_scene_count_work(self._h, ctypes.byref(tile), ctypes.byref(c)))
+        return c.as_dict()
+
+    def bvh_info(self) -> dict:
+        b = _lib.RrtBvhInfo()
+        _lib.check(self._lib.rrt_scene_bvh_info(self._h, ctypes.byref(b)))
+        return b.as_dict()

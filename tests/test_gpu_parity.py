@@ -1,0 +1,131 @@
+"""GPU parity: librrt_hip.so (through its C-ABI) vs the oracle's f32 TWIN restatement of the
+reference's books path (oracle/rrt_oracle.cpp). Tolerance: bit-exact accum (the north star's
+per-channel 1e-4 bound is asserted too, and is strictly weaker) and byte-identical PPM.
+
+Parity is "pinned" against the oracle; the oracle itself is pinned by tests/test_oracle.py
+(known-answer vectors, committed golden fixtures, and its f64 BOOKS mode).
+"""
+import numpy as np
+import pytest
+
+import rustraytrace_amd as rrt
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _torch():
+    import torch
+
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    return torch
+
+
+def gpu_tile(scene, band_rows=16, rank=0, n_ranks=1, s0=0, s1=None, count=False):
+    """Render one tile through the device-resident API; returns (accum[rows,W,4], rows, counters)."""
+    torch = _torch()
+    ds = rrt.DeviceScene(scene, device=0)
+    tile = ds.tile(band_rows, rank, n_ranks, s0, s1 if s1 is not None else scene.spp)
+    rows = ds.tile_rows(tile)
+    buf = torch.full((max(rows, 1), scene.width, 4), float("nan"), dtype=torch.float32, device="cuda:0")
+    ds.reset_counters()
+    stream = torch.cuda.current_stream()
+    ds.render_tile_async(tile, buf.data_ptr(), stream.cuda_stream)
+    torch.cuda.synchronize()
+    ctr = ds.counters()
+    work = ds.count_work(tile) if count else None
+    idx = ds.tile_row_indices(tile)
+    out = buf[:rows].cpu().numpy()
+    ds.close()
+    return out, idx, ctr, work
+
+
+def assert_bit_exact(gpu, ref, spp):
+    ref32 = ref.astype(np.float32)
+    assert np.array_equal(ref32.astype(np.float64), ref), "oracle TWIN sums must be exact f32"
+    diff = np.abs(gpu.astype(np.float64) - ref)
+    per_channel = diff[..., :3] / max(spp, 1)
+    assert per_channel.max() <= 1e-4  # north-star tolerance (before u8 quantisation)
+    assert diff.max() == 0.0, f"max |gpu - oracle| = {diff.max()} at {np.unravel_index(diff.argmax(), diff.shape)}"
+
+
+SMALL = [
+    ("C1", dict(image_width=64, samples_per_pixel=8)),
+    ("C2", dict(image_width=64, samples_per_pixel=8)),
+    ("C2", dict(image_width=96, samples_per_pixel=4, max_depth=6)),
+    ("C4", dict(image_width=64, samples_per_pixel=8)),
+    ("C5", dict(image_width=64, samples_per_pixel=4)),
+]
+
+
+@pytest.mark.parametrize("cfg,kw", SMALL, ids=[f"{c}-{k.get('image_width')}x{k.get('samples_per_pixel')}" for c, k in SMALL])
+def test_one_shot_matches_oracle(cfg, kw):
+    scene = rrt.config_scene(cfg, **kw)
+    gpu = rrt.render(scene)
+    ref, rays, _ = oracle.render(scene, oracle.TWIN)
+    assert_bit_exact(gpu, ref, scene.spp)
+    assert np.all(gpu[..., 3] == scene.spp)
+    a = rrt.format_ppm_from_accum(scene.width, scene.height, gpu, scene.spp)
+    b = rrt.format_ppm_from_accum(scene.width, scene.height, ref.astype(np.float32), scene.spp)
+    assert a == b
+
+
+@pytest.mark.parametrize("depth", [0, 1, 2, 5, 6, 50])
+def test_depth_and_roulette_boundaries(depth):
+    scene = rrt.rtow(image_width=48, samples_per_pixel=6, max_depth=depth)
+    gpu = rrt.render(scene)
+    ref, _, _ = oracle.render(scene, oracle.TWIN)
+    assert_bit_exact(gpu, ref, scene.spp)
+    if depth == 0:
+        assert np.all(gpu[..., :3] == 0)
+
+
+def test_ray_counts_match_oracle():
+    scene = rrt.rtow(image_width=64, samples_per_pixel=8, max_depth=20)
+    gpu, idx, ctr, work = gpu_tile(scene, count=True)
+    ref, rays, _ = oracle.render(scene, oracle.TWIN)
+    assert_bit_exact(gpu, ref, scene.spp)
+    assert ctr["rays"] == rays
+    assert ctr["paths"] == scene.width * scene.height * scene.spp
+    assert work["rays"] == rays and work["paths"] == ctr["paths"]
+    assert work["node_visits"] > 0 and work["sphere_tests"] > 0
+
+
+@pytest.mark.parametrize("n_ranks,band", [(2, 16), (3, 8), (8, 4)])
+def test_row_band_tiles_reassemble(n_ranks, band):
+    scene = rrt.rtow(image_width=40, samples_per_pixel=4, max_depth=10)
+    full = rrt.render(scene)
+    img = np.full_like(full, np.nan)
+    for r in range(n_ranks):
+        part, idx, _, _ = gpu_tile(scene, band_rows=band, rank=r, n_ranks=n_ranks)
+        img[idx] = part
+    assert np.array_equal(img, full)
+
+
+def test_sample_range_tile_matches_oracle():
+    scene = rrt.rtow(image_width=32, samples_per_pixel=16, max_depth=10)
+    gpu, idx, _, _ = gpu_tile(scene, s0=5, s1=13)
+    ref, _, _ = oracle.render(scene, oracle.TWIN, samples=(5, 13))
+    assert_bit_exact(gpu, ref, 8)
+    assert np.all(gpu[..., 3] == 8)
+
+
+def test_background_mode_and_no_defocus():
+    scene = rrt.build_in_one_weekend_scene(dict(image_width=48, samples_per_pixel=4, max_depth=8, defocus_angle=0.0,
+                                                background=(0.2, 0.3, 0.9)))
+    assert int(scene.camera["params_u"][0, 3]) == 1
+    gpu = rrt.render(scene)
+    ref, _, _ = oracle.render(scene, oracle.TWIN)
+    assert_bit_exact(gpu, ref, scene.spp)
+
+
+def test_multi_gpu_one_shot_equals_single():
+    torch = _torch()
+    n = torch.cuda.device_count()
+    scene = rrt.rtow(image_width=48, samples_per_pixel=4, max_depth=8)
+    a = rrt.render(scene, n_gpus=1)
+    if n >= 2:
+        b = rrt.render(scene, n_gpus=min(n, 8))
+        assert np.array_equal(a, b)
+    with pytest.raises(rrt.RrtError):
+        rrt.render(scene, n_gpus=n + 1)
