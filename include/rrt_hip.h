@@ -156,10 +156,10 @@ int32_t rrt_scene_create(const RrtCamera *cam,
                          uint32_t flags, int32_t device, RrtScene **out);
 int32_t rrt_scene_destroy(RrtScene *scene);
 
-/* Number of image rows `tile` owns (the tile's accum is rows*W float4). */
-int32_t rrt_tile_rows(const RrtScene *scene, const RrtTile *tile, uint32_t *rows_out);
+/* Number of image rows `tile` owns in an image of `height` rows (its accum is rows*W float4). */
+int32_t rrt_tile_rows(uint32_t height, const RrtTile *tile, uint32_t *rows_out);
 /* Global image row of the tile's local row `local_row`. */
-int32_t rrt_tile_row_index(const RrtScene *scene, const RrtTile *tile, uint32_t local_row, uint32_t *row_out);
+int32_t rrt_tile_row_index(uint32_t height, const RrtTile *tile, uint32_t local_row, uint32_t *row_out);
 
 /* Enqueue the render of `tile` on `stream` (a hipStream_t, NULL = default stream).
  * d_accum: device pointer to rows*W*4 floats, OVERWRITTEN with this tile's sums

@@ -140,6 +140,13 @@ def load() -> ctypes.CDLL:
             f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
             "(there is no CPU fallback for the HIP backend)"
         )
+    # One HIP runtime per process: torch bundles its own libamdhip64 (soname libamdhip64.so.7)
+    # which satisfies our DT_NEEDED when it is loaded first. Loaded the other way round,
+    # torch would map a second runtime and lose the device ("One runtime").
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = ctypes.CDLL(LIB_PATH)
     P = c_void_p
     sig = {
@@ -148,8 +155,8 @@ def load() -> ctypes.CDLL:
         "rrt_hip_abi_version": (c_uint32, []),
         "rrt_scene_create": (c_int32, [P, P, c_uint32, P, c_uint32, P, c_uint32, c_uint32, c_int32, P]),
         "rrt_scene_destroy": (c_int32, [P]),
-        "rrt_tile_rows": (c_int32, [P, P, P]),
-        "rrt_tile_row_index": (c_int32, [P, P, c_uint32, P]),
+        "rrt_tile_rows": (c_int32, [c_uint32, P, P]),
+        "rrt_tile_row_index": (c_int32, [c_uint32, P, c_uint32, P]),
         "rrt_render_tile_async": (c_int32, [P, P, P, P]),
         "rrt_scene_read_counters": (c_int32, [P, P]),
         "rrt_scene_reset_counters": (c_int32, [P]),

@@ -334,12 +334,17 @@ uint32_t tile_rows_of(uint32_t height, const RrtTile &t) {
     return rows;
 }
 
-int check_tile(const RrtScene *s, const RrtTile *t) {
-    if (!s || !t) return fail(RRT_E_INVALID, "null scene or tile");
+int check_tile_shape(const RrtTile *t) {
+    if (!t) return fail(RRT_E_INVALID, "null tile");
     if (t->band_rows == 0 || t->n_ranks == 0 || t->rank >= t->n_ranks)
         return fail(RRT_E_INVALID, "tile: band_rows and n_ranks must be > 0 and rank < n_ranks");
     if (t->sample_end < t->sample_begin) return fail(RRT_E_INVALID, "tile: sample_end < sample_begin");
     return RRT_OK;
+}
+
+int check_tile(const RrtScene *s, const RrtTile *t) {
+    if (!s) return fail(RRT_E_INVALID, "null scene");
+    return check_tile_shape(t);
 }
 
 int fill_params(RrtScene *s, const RrtTile *t, float *d_accum, rrt::KParams &p) {
@@ -529,17 +534,17 @@ int32_t rrt_scene_bvh_info(const RrtScene *scene, RrtBvhInfo *out) {
     return RRT_OK;
 }
 
-int32_t rrt_tile_rows(const RrtScene *scene, const RrtTile *tile, uint32_t *rows_out) {
-    if (int rc = check_tile(scene, tile)) return rc;
+int32_t rrt_tile_rows(uint32_t height, const RrtTile *tile, uint32_t *rows_out) {
+    if (int rc = check_tile_shape(tile)) return rc;
     if (!rows_out) return fail(RRT_E_INVALID, "null rows_out");
-    *rows_out = tile_rows_of(scene->base.height, *tile);
+    *rows_out = tile_rows_of(height, *tile);
     return RRT_OK;
 }
 
-int32_t rrt_tile_row_index(const RrtScene *scene, const RrtTile *tile, uint32_t local_row, uint32_t *row_out) {
-    if (int rc = check_tile(scene, tile)) return rc;
+int32_t rrt_tile_row_index(uint32_t height, const RrtTile *tile, uint32_t local_row, uint32_t *row_out) {
+    if (int rc = check_tile_shape(tile)) return rc;
     if (!row_out) return fail(RRT_E_INVALID, "null row_out");
-    if (local_row >= tile_rows_of(scene->base.height, *tile)) return fail(RRT_E_INVALID, "local_row out of range");
+    if (local_row >= tile_rows_of(height, *tile)) return fail(RRT_E_INVALID, "local_row out of range");
     const uint32_t band = local_row / tile->band_rows;
     *row_out = (band * tile->n_ranks + tile->rank) * tile->band_rows + local_row % tile->band_rows;
     return RRT_OK;

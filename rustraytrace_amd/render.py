@@ -85,6 +85,29 @@ def device_count() -> int:
     return n.value
 
 
+def tile_rows(height: int, tile) -> int:
+    n = ctypes.c_uint32(0)
+    _lib.check(_lib.load().rrt_tile_rows(height, ctypes.byref(tile), ctypes.byref(n)))
+    return n.value
+
+
+def tile_row_indices(height: int, tile) -> np.ndarray:
+    lib = _lib.load()
+    rows = tile_rows(height, tile)
+    out = np.empty(rows, dtype=np.int64)
+    r = ctypes.c_uint32(0)
+    for i in range(rows):
+        _lib.check(lib.rrt_tile_row_index(height, ctypes.byref(tile), i, ctypes.byref(r)))
+        out[i] = r.value
+    return out
+
+
+def make_tile(band_rows=16, rank=0, n_ranks=1, sample_begin=0, sample_end=0) -> _lib.RrtTile:
+    t = _lib.RrtTile()
+    t.band_rows, t.rank, t.n_ranks, t.sample_begin, t.sample_end = band_rows, rank, n_ranks, sample_begin, sample_end
+    return t
+
+
 class DeviceScene:
     """RrtScene*: scene + BVH resident on one device; renders tiles asynchronously on a stream."""
 
@@ -120,18 +143,10 @@ class DeviceScene:
         return t
 
     def tile_rows(self, tile) -> int:
-        n = ctypes.c_uint32(0)
-        _lib.check(self._lib.rrt_tile_rows(self._h, ctypes.byref(tile), ctypes.byref(n)))
-        return n.value
+        return tile_rows(self.scene.height, tile)
 
     def tile_row_indices(self, tile) -> np.ndarray:
-        rows = self.tile_rows(tile)
-        out = np.empty(rows, dtype=np.int64)
-        r = ctypes.c_uint32(0)
-        for i in range(rows):
-            _lib.check(self._lib.rrt_tile_row_index(self._h, ctypes.byref(tile), i, ctypes.byref(r)))
-            out[i] = r.value
-        return out
+        return tile_row_indices(self.scene.height, tile)
 
     def render_tile_async(self, tile, d_accum_ptr: int, stream_ptr: int = 0) -> None:
         _lib.check(self._lib.rrt_render_tile_async(self._h, ctypes.byref(tile), ctypes.c_void_p(d_accum_ptr),

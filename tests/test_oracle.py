@@ -1,0 +1,272 @@
+"""CPU tests pinning the oracle (oracle/rrt_oracle.cpp) before it is trusted as the parity
+checker. The reference has no tests or golden vectors, so the oracle is pinned by:
+  * analytic known-answer vectors for every restated primitive (sphere.rs, aabb.rs, vec3.rs,
+    material.rs, color.rs, render_io.rs),
+  * closed-form images (white furnace, sky-only),
+  * agreement of its two independent modes (f64 BOOKS recursion vs f32 TWIN),
+  * its independent restatement of gpu::build_in_one_weekend_scene vs the product's builder,
+  * the committed golden fixtures (regression pin; tests/golden/make_golden.py).
+"""
+import glob
+import hashlib
+import math
+import os
+
+import numpy as np
+import pytest
+
+import rustraytrace_amd as rrt
+from oracle import oracle
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+INF = float("inf")
+
+
+# ---- Sphere::hit (sphere.rs:24-51) ------------------------------------------------------------
+@pytest.mark.parametrize("f32", [0, 1])
+def test_sphere_hit_front(f32):
+    t, n, front = oracle.sphere_hit((0, 0, -5), 1.0, (0, 0, 0), (0, 0, -1), f32=f32)
+    assert t == 4.0 and front and list(n) == [0.0, 0.0, 1.0]
+    # unnormalised direction: t scales by 1/|d|
+    t, n, front = oracle.sphere_hit((0, 0, -5), 1.0, (0, 0, 0), (0, 0, -2), f32=f32)
+    assert t == 2.0
+
+
+@pytest.mark.parametrize("f32", [0, 1])
+def test_sphere_hit_inside_uses_far_root(f32):
+    t, n, front = oracle.sphere_hit((0, 0, -5), 1.0, (0, 0, -5), (0, 0, -1), f32=f32)
+    assert t == 1.0 and not front and list(n) == [0.0, 0.0, 1.0]  # normal flipped against the ray
+
+
+@pytest.mark.parametrize("f32", [0, 1])
+def test_sphere_hit_tangent_miss_behind(f32):
+    t, _, _ = oracle.sphere_hit((0, 1, -5), 1.0, (0, 0, 0), (0, 0, -1), f32=f32)  # disc == 0 accepted
+    assert t == 5.0
+    assert oracle.sphere_hit((0, 2, -5), 1.0, (0, 0, 0), (0, 0, -1), f32=f32) is None  # disc < 0
+    assert oracle.sphere_hit((0, 0, 5), 1.0, (0, 0, 0), (0, 0, -1), f32=f32) is None  # both roots behind
+
+
+@pytest.mark.parametrize("f32", [0, 1])
+def test_sphere_hit_open_interval(f32):
+    # interval.rs:30-32 surrounds is strict on both ends
+    assert oracle.sphere_hit((0, 0, -5), 1.0, (0, 0, 0), (0, 0, -1), tmax=4.0, f32=f32) is None
+    t, _, _ = oracle.sphere_hit((0, 0, -5), 1.0, (0, 0, 0), (0, 0, -1), tmin=4.0, f32=f32)
+    assert t == 6.0
+    # negative radius clamps to 0 (sphere.rs:17): only a ray through the centre point hits
+    assert oracle.sphere_hit((0, 0, -5), -1.0, (0, 0, 0), (0, 1, -1), f32=f32) is None
+
+
+# ---- Aabb::hit (aabb.rs:52-85) incl. 1/0 = inf and 0*inf = NaN branches ------------------------
+@pytest.mark.parametrize("f32", [0, 1])
+def test_aabb_axis_parallel(f32):
+    lo, hi = (-1, -1, -1), (1, 1, 1)
+    assert oracle.aabb_hit(lo, hi, (0, 0, -5), (0, 0, 1), f32=f32)
+    assert not oracle.aabb_hit(lo, hi, (0, 0, -5), (0, 0, -1), f32=f32)
+    assert oracle.aabb_hit(lo, hi, (0.5, 0, -5), (0, 0, 1), f32=f32)  # dx = 0, inside the x slab
+    assert not oracle.aabb_hit(lo, hi, (2, 0, -5), (0, 0, 1), f32=f32)  # dx = 0, outside
+    assert not oracle.aabb_hit(lo, hi, (0, 0, -5), (0, 0, 1), tmax=3.0, f32=f32)  # ends before the box
+    assert not oracle.aabb_hit(lo, hi, (0, 0, -5), (0, 0, 1), tmax=4.0, f32=f32)  # max <= min rejects
+
+
+@pytest.mark.parametrize("f32", [0, 1])
+def test_aabb_on_plane_nan_branch(f32):
+    lo, hi = (-1, -1, -1), (1, 1, 1)
+    # origin exactly on the x = lo plane with dx = +0: t0 = 0*inf = NaN, t1 = +inf -> min = inf: reject
+    assert not oracle.aabb_hit(lo, hi, (-1, 0, -5), (0.0, 0, 1), f32=f32)
+    # dx = -0: t0 = NaN, t1 = -inf -> neither bound moves: accept (books branch order)
+    assert oracle.aabb_hit(lo, hi, (-1, 0, -5), (-0.0, 0, 1), f32=f32)
+    # on the x = hi plane with dx = +0: t0 = -inf, t1 = NaN -> max = -inf: reject
+    assert not oracle.aabb_hit(lo, hi, (1, 0, -5), (0.0, 0, 1), f32=f32)
+
+
+# ---- vec3.rs reflect/refract, material.rs Schlick ---------------------------------------------
+@pytest.mark.parametrize("f32", [0, 1])
+def test_reflect_refract_schlick(f32):
+    refl, refr, sch = oracle.reflect_refract((1, -1, 0), (0, 1, 0), 1 / 1.5, 1.0, 1.5, f32=f32)
+    assert list(refl) == [1.0, 1.0, 0.0]
+    assert sch == pytest.approx(0.04, rel=1e-6)  # r0 = ((1-1.5)/(1+1.5))^2 at normal incidence
+    _, refr, sch = oracle.reflect_refract((0, -1, 0), (0, 1, 0), 1 / 1.5, 0.0, 1.5, f32=f32)
+    assert list(refr) == [0.0, -1.0, 0.0] and sch == 1.0  # straight through; grazing -> total
+    s = math.sqrt(0.5)
+    _, refr, _ = oracle.reflect_refract((s, -s, 0), (0, 1, 0), 1 / 1.5, 0.5, 1.0, f32=f32)
+    tol = 1e-6 if f32 else 1e-14
+    assert refr[0] == pytest.approx(s / 1.5, abs=tol)  # Snell: sin t = sin i / 1.5
+    assert refr[1] == pytest.approx(-math.sqrt(1 - 0.5 / 2.25), abs=tol)
+    _, _, sch = oracle.reflect_refract((0, -1, 0), (0, 1, 0), 1.0, 0.5, 1.0, f32=f32)
+    assert sch == 0.5 ** 5  # r0 = 0 -> (1 - cos)^5 via x*((x*x)*(x*x))
+
+
+# ---- quantisers: color.rs (f64) and render_io.rs (f32) ----------------------------------------
+def test_write_color_edges():
+    assert list(oracle.write_color([0.0, 0.25, 1.0])) == [0, 128, 255]
+    assert list(oracle.write_color([-1.0, float("nan"), INF])) == [0, 0, 255]  # inf -> 255 in books
+
+
+def test_render_io_quantiser_edges_match_product():
+    spp = 4
+    vals = np.array([0.0, 0.25, 1.0, 0.999 ** 2, INF, -INF, float("nan"), -0.5, 1e30, 4.0, 0.01, 3.99])
+    acc = np.zeros((len(vals), 4), np.float32)
+    acc[:, 0] = vals * spp
+    acc[:, 1] = vals
+    acc[:, 2] = 1.0
+    ref = oracle.quantize_render_io(acc, spp)
+    got = rrt.quantize_accum(len(vals), 1, acc, spp).reshape(-1, 3)
+    assert np.array_equal(ref, got)
+    assert list(ref[:7, 0]) == [0, 128, 255, 255, 0, 0, 0]  # non-finite -> 0 in render_io (unlike color.rs)
+    ppm = rrt.format_ppm_from_accum(len(vals), 1, acc, spp)
+    lines = ppm.decode().splitlines()
+    assert lines[:3] == ["P3", f"{len(vals)} 1", "255"]
+    assert [list(map(int, l.split())) for l in lines[3:]] == ref.tolist()
+
+
+# ---- camera / image height (camera.rs:102-150, gpu/mod.rs:174-198) ----------------------------
+@pytest.mark.parametrize("w,h", [(400, 225), (1920, 1080), (3840, 2160), (64, 36), (1, 1)])
+def test_image_height(w, h):
+    cam = rrt.make_camera(aspect_ratio=16 / 9, image_width=w)
+    assert int(cam["params_f"][0, 2]) == h
+
+
+def test_camera_matches_gpu_mod_rs_math():
+    W, H = 1920, 1080
+    cam = rrt.build_in_one_weekend_scene(dict(image_width=W, samples_per_pixel=512, max_depth=100)).camera
+    lookfrom, lookat, vup = np.array([13.0, 2, 3]), np.zeros(3), np.array([0.0, 1, 0])
+    h = math.tan(math.radians(20.0) / 2)  # degrees * PI / 180
+    vh = 2.0 * h * 10.0
+    vw = vh * (W / H)
+    w = (lookfrom - lookat) / np.linalg.norm(lookfrom - lookat)
+    u = np.cross(vup, w)
+    u = u / np.linalg.norm(u)
+    v = np.cross(w, u)
+    du, dv = u * vw / W, v * -vh / H
+    p00 = lookfrom - w * 10.0 - u * vw / 2 - v * -vh / 2 + (du + dv) * 0.5
+    np.testing.assert_allclose(cam["pixel00"][0, :3], p00, rtol=1e-6)
+    np.testing.assert_allclose(cam["pixel_delta_u"][0, :3], du, rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(cam["pixel_delta_v"][0, :3], dv, rtol=1e-6, atol=1e-9)
+    assert cam["params_f"][0, 0] == np.float32(10.0 * math.tan(math.radians(0.3)))
+    assert list(cam["params_u"][0]) == [100, cam["params_u"][0, 1], 486, 0]
+
+
+# ---- RNG stream and f32 transcendentals -------------------------------------------------------
+def test_path_stream_deterministic_and_uniform():
+    a = oracle.path_stream(0x1234, 77, 5, 4096)
+    assert np.array_equal(a, oracle.path_stream(0x1234, 77, 5, 4096))
+    assert not np.array_equal(a, oracle.path_stream(0x1234, 77, 6, 4096))
+    assert not np.array_equal(a, oracle.path_stream(0x1234, 78, 5, 4096))
+    u = (oracle.path_stream(7, 1, 2, 200000) >> 8) / 2.0 ** 24
+    assert abs(u.mean() - 0.5) < 0.005 and u.min() >= 0.0 and u.max() < 1.0
+    assert abs(np.histogram(u, bins=10)[0] / len(u) - 0.1).max() < 0.005
+
+
+def test_cephes_acos_atan2_accuracy():
+    for x in np.linspace(-1, 1, 2001, dtype=np.float32):
+        a, _ = oracle.acos_atan2_f32(float(x), 0.5)
+        assert abs(a - math.acos(float(x))) < 4e-7
+    for ang in np.linspace(-math.pi + 1e-3, math.pi - 1e-3, 997):
+        y, x = math.sin(ang), math.cos(ang)
+        _, t = oracle.acos_atan2_f32(np.float32(x), np.float32(y))
+        assert abs(t - math.atan2(np.float32(y), np.float32(x))) < 4e-7
+    assert oracle.acos_atan2_f32(0.0, 1.0)[1] == pytest.approx(math.pi / 2)
+    assert oracle.acos_atan2_f32(0.0, -1.0)[1] == pytest.approx(-math.pi / 2)
+
+
+# ---- scene builder: product vs independent restatement ----------------------------------------
+@pytest.mark.parametrize("grid_half,n", [(11, 486), (50, 10001)])
+def test_rtow_scene_restatements_agree(grid_half, n):
+    prod = rrt.build_in_one_weekend_scene(seed=0x5EED_1234, grid_half=grid_half)
+    ref = oracle.rtow_scene(0x5EED_1234, grid_half)
+    assert len(prod.spheres) == n
+    assert np.array_equal(prod.spheres["center_radius"], ref["center_radius"])
+    assert np.array_equal(prod.spheres["material_index"], ref["material_index"])
+    assert np.array_equal(prod.materials["albedo_fuzz"], ref["albedo_fuzz"])
+    assert np.array_equal(prod.materials["kind"], ref["kind"])
+    assert np.array_equal(prod.materials["ref_idx"], ref["ref_idx"])
+    assert int(prod.camera["params_u"][0, 1]) == ref["sample_seed"]
+
+
+def test_rtow_scene_material_mix():
+    s = rrt.build_in_one_weekend_scene()
+    kind = s.materials["kind"]
+    assert set(np.unique(kind)) == {0, 1, 2}
+    small = s.spheres["center_radius"][1:-3]
+    assert np.all(small[:, 3] == np.float32(0.2)) and np.all(small[:, 1] == np.float32(0.2))
+    d = np.hypot(small[:, 0] - 4.0, small[:, 2])
+    assert np.all(d > 0.9 - 1e-6)
+    metal = s.materials[kind == 1][:-1]
+    assert np.all(metal["albedo_fuzz"][:, :3] >= 0.5) and np.all(metal["albedo_fuzz"][:, 3] < 0.5)
+
+
+# ---- closed-form images -----------------------------------------------------------------------
+def _white_furnace(n_spheres=1, depth=10):
+    from rustraytrace_amd.scenes import SceneData, _material, _sphere, make_camera
+
+    mats = _material(0, (1.0, 1.0, 1.0))
+    sph = _sphere((0.0, 0.0, -1.0), 0.5, 0)
+    cam = make_camera(aspect_ratio=16 / 9, image_width=32, samples_per_pixel=8, max_depth=depth,
+                      background=(1.0, 1.0, 1.0), seed=99, n_spheres=1)
+    return SceneData(cam, sph, mats, name="white_furnace")
+
+
+@pytest.mark.parametrize("mode", [oracle.TWIN, oracle.BOOKS])
+def test_white_furnace_exact(mode):
+    # albedo-1 convex sphere under background 1: every path returns exactly 1 (no RR before bounce 5,
+    # a convex sphere is left after one bounce), so every pixel sums to exactly spp.
+    sc = _white_furnace()
+    acc, rays, _ = oracle.render(sc, mode)
+    assert np.all(acc[..., :3] == sc.spp)
+    assert rays >= sc.width * sc.height * sc.spp
+
+
+def test_sky_only_twin_books_agree():
+    from rustraytrace_amd.scenes import SceneData, make_camera
+
+    cam = make_camera(aspect_ratio=16 / 9, image_width=40, samples_per_pixel=4, max_depth=5, seed=3,
+                      defocus_angle=2.0, lookfrom=(0, 1, 0), lookat=(0, 1, -1))
+    sc = SceneData(cam, np.zeros(0, rrt._lib.SPHERE_DTYPE), np.zeros(0, rrt._lib.MATERIAL_DTYPE))
+    t, rt, _ = oracle.render(sc, oracle.TWIN)
+    b, rb, _ = oracle.render(sc, oracle.BOOKS)
+    assert rt == rb == 40 * 22 * 4
+    np.testing.assert_allclose(t[..., :3], b[..., :3], rtol=2e-6)
+
+
+def test_books_vs_twin_statistical():
+    # Same scene and the same random stream; f64 recursion vs f32 forward throughput. Individual
+    # paths diverge where an f32/f64 rounding flips a discrete decision, so the bar is statistical.
+    sc = rrt.rtow(image_width=48, samples_per_pixel=16, max_depth=20)
+    t, rt, _ = oracle.render(sc, oracle.TWIN, threads=8)
+    b, rb, _ = oracle.render(sc, oracle.BOOKS, threads=8)
+    per_chan = np.abs(t - b)[..., :3] / sc.spp
+    assert (per_chan <= 1e-4).mean() > 0.85
+    assert abs(t[..., :3].mean() - b[..., :3].mean()) / b[..., :3].mean() < 0.01
+    assert abs(rt - rb) / rb < 0.01
+
+
+# ---- golden fixtures (regression pin of the oracle) -------------------------------------------
+GOLDENS = sorted(glob.glob(os.path.join(GOLDEN, "*.npz")))
+
+
+def _golden_scene(name):
+    import sys
+
+    sys.path.insert(0, GOLDEN)
+    from make_golden import CASES, scene_sha
+
+    cfg, kw = CASES[name]
+    sc = rrt.config_scene(cfg, **kw)
+    return sc, scene_sha(sc)
+
+
+@pytest.mark.parametrize("path", GOLDENS, ids=[os.path.basename(p) for p in GOLDENS])
+def test_oracle_reproduces_golden(path):
+    name = os.path.basename(path)[:-4]
+    z = np.load(path, allow_pickle=False)
+    sc, sha = _golden_scene(name)
+    assert sha == str(z["scene_sha256"]), "scene builder output changed"
+    acc, rays, _ = oracle.render(sc, oracle.TWIN, threads=4)
+    assert np.array_equal(acc.astype(np.float32), z["accum"])
+    assert rays == int(z["rays"])
+    ppm = rrt.format_ppm_from_accum(sc.width, sc.height, z["accum"], sc.spp)
+    assert ppm == z["ppm"].tobytes()
+
+
+def test_goldens_present():
+    assert len(GOLDENS) >= 5
