@@ -15,6 +15,7 @@
 #include <atomic>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -423,7 +424,7 @@ int32_t rrt_scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint32_
             bld.max_depth = 1;
         }
     }
-    if (bld.max_depth + 1 > (uint32_t)rrt::kStackDepth)
+    if (bld.max_depth + 1 > (uint32_t)rrt::kMaxStackDepth)
         return fail(RRT_E_INVALID, "BVH depth " + std::to_string(bld.max_depth) + " exceeds the LDS stack");
 
     std::vector<float4> prim_cr(n_spheres);
@@ -511,6 +512,12 @@ int32_t rrt_scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint32_
     p.flags = flags;
     p.width = (uint32_t)wf;
     p.height = (uint32_t)hf;
+    p.n_nodes = (uint32_t)bld.nodes.size();
+    p.n_prims = n_spheres;
+    p.stack_depth = bld.max_depth + 1;
+    const size_t scene_bytes = bld.nodes.size() * sizeof(rrt::GNode) + (size_t)n_spheres * sizeof(float4);
+    p.scene_in_lds = scene_bytes <= rrt::kLdsSceneBudget && p.stack_depth <= 32;
+    if (const char *e = std::getenv("RRT_SCENE_IN_LDS")) p.scene_in_lds = p.scene_in_lds && std::atoi(e) != 0;
 
     RrtBvhInfo &bi = s->info;
     bi.n_nodes = (uint32_t)bld.nodes.size();

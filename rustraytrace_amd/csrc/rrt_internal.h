@@ -74,11 +74,18 @@ struct KParams {
     uint32_t sample_end;
     uint32_t n_work_tiles;  // 8x8 pixel tiles in this tile
     uint32_t tiles_x;
+
+    uint32_t n_nodes;
+    uint32_t n_prims;
+    uint32_t stack_depth;   // entries needed (BVH depth + 1)
+    uint32_t scene_in_lds;  // stage nodes + spheres in LDS per block
 };
 
-// Traversal stack depth held in LDS per lane (entries = max BVH depth - 1 suffices).
-constexpr int kStackDepth = 40;
+// Traversal stack entries held in LDS per lane: up to 64 (BVH depth <= 63).
+constexpr int kMaxStackDepth = 64;
 constexpr int kBlock = 256;
+// Per-block LDS budget for staging the scene (BVH nodes + spheres) next to the stack.
+constexpr size_t kLdsSceneBudget = 40 * 1024;
 
 // Launch wrappers implemented in rrt_kernel.hip.
 hipError_t launch_render(const KParams &p, hipStream_t stream);

@@ -140,26 +140,31 @@ __device__ __forceinline__ float rrt_atan2f(float y, float x) {
     return z;
 }
 
-// ---- Aabb::hit (aabb.rs:52-85), books branch structure incl. NaN behaviour -----------------
-__device__ __forceinline__ bool slab(float lo, float hi, float o, float adinv, float &tmin, float &tmax) {
+// ---- Aabb::hit (aabb.rs:52-85), branch-free and decision-identical ---------------------------
+// The reference updates the interval per axis with `if t0 < t1 {min<-t0 if t0>min; max<-t1 if
+// t1<max} else {min<-t1 if t1>min; max<-t0 if t0<max}` and returns false as soon as
+// max <= min. Here: near/far are selected with the same `t0 < t1` test, then min/max are
+// updated with IEEE maxNum/minNum (v_max_f32 / v_min_f32), which return the non-NaN operand:
+// exactly the reference's `if x > min` / `if x < max` (a NaN near/far leaves the bound alone,
+// as the reference's false comparison does; ties differ only in the sign of a zero). min and
+// max are never NaN, so testing max <= min once after all three axes equals the per-axis
+// early return (the interval only shrinks). tnear = the entry distance, for child ordering.
+__device__ __forceinline__ void slab(float lo, float hi, float o, float adinv, float &tmin, float &tmax) {
     const float t0 = (lo - o) * adinv;
     const float t1 = (hi - o) * adinv;
-    if (t0 < t1) {
-        if (t0 > tmin) tmin = t0;
-        if (t1 < tmax) tmax = t1;
-    } else {
-        if (t1 > tmin) tmin = t1;
-        if (t0 < tmax) tmax = t0;
-    }
-    return !(tmax <= tmin);
+    const bool lt = t0 < t1;
+    const float nr = lt ? t0 : t1;
+    const float fr = lt ? t1 : t0;
+    tmin = __builtin_fmaxf(tmin, nr);
+    tmax = __builtin_fminf(tmax, fr);
 }
 __device__ __forceinline__ bool box_hit(float lx, float hx, float ly, float hy, float lz, float hz,
                                         V3 o, V3 inv, float tmin, float tmax, float &tnear) {
-    if (!slab(lx, hx, o.x, inv.x, tmin, tmax)) return false;
-    if (!slab(ly, hy, o.y, inv.y, tmin, tmax)) return false;
-    if (!slab(lz, hz, o.z, inv.z, tmin, tmax)) return false;
+    slab(lx, hx, o.x, inv.x, tmin, tmax);
+    slab(ly, hy, o.y, inv.y, tmin, tmax);
+    slab(lz, hz, o.z, inv.z, tmin, tmax);
     tnear = tmin;
-    return true;
+    return !(tmax <= tmin);
 }
 
 struct Counters {
@@ -189,8 +194,26 @@ __device__ __forceinline__ void test_prims(const float4 *__restrict__ prim_cr, i
     }
 }
 
-template <bool kCount>
-__device__ __forceinline__ int trace(const KParams &P, int *__restrict__ stack, V3 o, V3 d, float &t_hit, Counters &cnt) {
+// Traversal stack in LDS. 16-bit entries: the dword at (depth, wave, k) holds lanes k and
+// k+32, which the LDS serves in different cycles (2 x 32-lane groups), so no bank conflicts.
+template <typename StackT>
+struct LdsStack {
+    StackT *base;
+    __device__ __forceinline__ void init(StackT *lds, uint32_t tid) {
+        if constexpr (sizeof(StackT) == 2) {
+            const uint32_t lane = tid & 63u;
+            base = lds + (tid & ~63u) + ((lane & 31u) << 1) + (lane >> 5);
+        } else {
+            base = lds + tid;
+        }
+    }
+    __device__ __forceinline__ void store(int sp, int v) { base[sp * kBlock] = (StackT)v; }
+    __device__ __forceinline__ int load(int sp) const { return (int)base[sp * kBlock]; }
+};
+
+template <bool kCount, typename Stack>
+__device__ __forceinline__ int trace(const GNode *__restrict__ nodes, const float4 *__restrict__ prims, Stack &stack,
+                                     V3 o, V3 d, float &t_hit, Counters &cnt) {
     const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     const float a = dot(d, d);
     float closest = __builtin_inff();
@@ -198,22 +221,22 @@ __device__ __forceinline__ int trace(const KParams &P, int *__restrict__ stack, 
     int node = 0;
     int sp = 0;
     for (;;) {
-        const GNode n = P.nodes[node];
+        const GNode n = nodes[node];
         if (kCount) { cnt.nodes++; cnt.boxes += 2; }
         float tn0 = 0.0f, tn1 = 0.0f;
         bool h0 = box_hit(n.b0.x, n.b0.y, n.b0.z, n.b0.w, n.b1.x, n.b1.y, o, inv, 0.001f, closest, tn0);
         bool h1 = box_hit(n.b1.z, n.b1.w, n.b2.x, n.b2.y, n.b2.z, n.b2.w, o, inv, 0.001f, closest, tn1);
         if (h0 && n.link.z > 0) {
-            test_prims<kCount>(P.prim_cr, n.link.x, n.link.z, o, d, a, closest, hit_prim, cnt);
+            test_prims<kCount>(prims, n.link.x, n.link.z, o, d, a, closest, hit_prim, cnt);
             h0 = false;
         }
         if (h1 && n.link.w > 0) {
-            test_prims<kCount>(P.prim_cr, n.link.y, n.link.w, o, d, a, closest, hit_prim, cnt);
+            test_prims<kCount>(prims, n.link.y, n.link.w, o, d, a, closest, hit_prim, cnt);
             h1 = false;
         }
         if (h0 && h1) {
             const bool first1 = tn1 < tn0;
-            stack[sp * kBlock] = first1 ? n.link.x : n.link.y;
+            stack.store(sp, first1 ? n.link.x : n.link.y);
             ++sp;
             node = first1 ? n.link.y : n.link.x;
         } else if (h0) {
@@ -223,7 +246,7 @@ __device__ __forceinline__ int trace(const KParams &P, int *__restrict__ stack, 
         } else {
             if (sp == 0) break;
             --sp;
-            node = stack[sp * kBlock];
+            node = stack.load(sp);
         }
     }
     t_hit = closest;
@@ -280,13 +303,13 @@ __device__ __forceinline__ V3 texel(const KParams &P, int tex, float u, float v)
 }
 
 // One bounce: closest hit, then scatter / RR. Returns true when the path has ended.
-template <bool kCount>
-__device__ __forceinline__ bool bounce(const KParams &P, int *stack, PathState &ps, Counters &cnt) {
+template <bool kCount, typename Stack>
+__device__ __forceinline__ bool bounce(const KParams &P, const GNode *nodes, const float4 *prims, Stack &stack,
+                                       PathState &ps, Counters &cnt) {
     if (ps.k >= P.max_depth) return true;  // ray_color: depth <= 0 -> 0
     float t;
-    if (kCount) cnt.rays++;
-    else cnt.rays++;
-    const int prim = trace<kCount>(P, stack, ps.o, ps.d, t, cnt);
+    cnt.rays++;
+    const int prim = trace<kCount>(nodes, prims, stack, ps.o, ps.d, t, cnt);
     if (prim < 0) {
         V3 bg;
         if (P.bg_mode == 1u) {
@@ -300,7 +323,7 @@ __device__ __forceinline__ bool bounce(const KParams &P, int *stack, PathState &
         return true;
     }
     // HitRecord (sphere.rs:47-50, hittable.rs:20-32)
-    const float4 cr = P.prim_cr[prim];
+    const float4 cr = prims[prim];
     const V3 p = v3(ps.o.x + ps.d.x * t, ps.o.y + ps.d.y * t, ps.o.z + ps.d.z * t);
     const float inv_r = 1.0f / cr.w;
     const V3 outward = v3((p.x - cr.x) * inv_r, (p.y - cr.y) * inv_r, (p.z - cr.z) * inv_r);
@@ -365,10 +388,27 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
     return v;
 }
 
-template <bool kCount>
+template <int kStack, bool kLds, bool kCount, typename StackT>
 __device__ __forceinline__ void render_body(const KParams &P) {
-    __shared__ int lds_stack[kStackDepth * kBlock];
-    int *stack = lds_stack + threadIdx.x;
+    extern __shared__ uint4 lds_dyn[];
+    // LDS layout: [traversal stack: kStack x kBlock x StackT][nodes][primitives]
+    StackT *lds_stack = reinterpret_cast<StackT *>(lds_dyn);
+    const GNode *nodes = P.nodes;
+    const float4 *prims = P.prim_cr;
+    if constexpr (kLds) {
+        // Stage the whole BVH + spheres (KB-sized) in LDS once per block.
+        uint4 *dst = lds_dyn + (kStack * kBlock * sizeof(StackT)) / 16;
+        const uint4 *src_n = reinterpret_cast<const uint4 *>(P.nodes);
+        const uint32_t nn = P.n_nodes * 4u;
+        for (uint32_t i = threadIdx.x; i < nn; i += kBlock) dst[i] = src_n[i];
+        const uint4 *src_p = reinterpret_cast<const uint4 *>(P.prim_cr);
+        for (uint32_t i = threadIdx.x; i < P.n_prims; i += kBlock) dst[nn + i] = src_p[i];
+        __syncthreads();
+        nodes = reinterpret_cast<const GNode *>(dst);
+        prims = reinterpret_cast<const float4 *>(dst + nn);
+    }
+    LdsStack<StackT> stack;
+    stack.init(lds_stack, threadIdx.x);
 
     const uint32_t wave = threadIdx.x >> 6;
     const uint32_t lane = threadIdx.x & 63u;
@@ -398,7 +438,7 @@ __device__ __forceinline__ void render_body(const KParams &P) {
             camera_ray(P, x, y, ps);
         }
         while (s < P.sample_end) {
-            if (bounce<kCount>(P, stack, ps, cnt)) {
+            if (bounce<kCount>(P, nodes, prims, stack, ps, cnt)) {
                 sum = add(sum, ps.L);  // pixel_color += ray_color(..) (camera.rs:73-76)
                 cnt.paths++;
                 ++s;
@@ -430,23 +470,48 @@ __device__ __forceinline__ void render_body(const KParams &P) {
     }
 }
 
-__global__ __launch_bounds__(kBlock) void rrt_render(KParams P) { render_body<false>(P); }
-__global__ __launch_bounds__(kBlock) void rrt_render_counting(KParams P) { render_body<true>(P); }
+template <int kStack, bool kLds, bool kCount, typename StackT>
+__global__ __launch_bounds__(kBlock) void rrt_render(KParams P) {
+    render_body<kStack, kLds, kCount, StackT>(P);
+}
+
+template <int kStack, bool kLds, typename StackT>
+hipError_t launch_variant(const KParams &p, bool count, hipStream_t stream) {
+    const uint32_t blocks = (p.n_work_tiles + (kBlock / 64) - 1) / (kBlock / 64);
+    if (blocks == 0) return hipSuccess;
+    size_t lds = (size_t)kStack * kBlock * sizeof(StackT);
+    if (kLds) lds += (size_t)p.n_nodes * sizeof(GNode) + (size_t)p.n_prims * sizeof(float4);
+    if (count) hipLaunchKernelGGL((rrt_render<kStack, kLds, true, StackT>), dim3(blocks), dim3(kBlock), lds, stream, p);
+    else hipLaunchKernelGGL((rrt_render<kStack, kLds, false, StackT>), dim3(blocks), dim3(kBlock), lds, stream, p);
+    return hipGetLastError();
+}
 
 }  // namespace
 
-hipError_t launch_render(const KParams &p, hipStream_t stream) {
-    const uint32_t blocks = (p.n_work_tiles + (kBlock / 64) - 1) / (kBlock / 64);
-    if (blocks == 0) return hipSuccess;
-    hipLaunchKernelGGL(rrt_render, dim3(blocks), dim3(kBlock), 0, stream, p);
-    return hipGetLastError();
+size_t lds_scene_bytes(const KParams &p) {
+    return (size_t)p.n_nodes * sizeof(GNode) + (size_t)p.n_prims * sizeof(float4);
 }
 
-hipError_t launch_render_counting(const KParams &p, hipStream_t stream) {
-    const uint32_t blocks = (p.n_work_tiles + (kBlock / 64) - 1) / (kBlock / 64);
-    if (blocks == 0) return hipSuccess;
-    hipLaunchKernelGGL(rrt_render_counting, dim3(blocks), dim3(kBlock), 0, stream, p);
-    return hipGetLastError();
+hipError_t launch_render_kernel(const KParams &p, bool count, hipStream_t stream) {
+    // Variant choice: smallest LDS stack that holds the BVH depth; scene staged in LDS when the
+    // BVH + spheres fit the per-block budget (RTOW: ~26 KB), else read through L1/L2.
+    const bool lds = p.scene_in_lds != 0;
+    const bool wide = p.n_nodes > 65535u;
+    if (wide) {
+        if (p.stack_depth > 64) return hipErrorInvalidValue;
+        return launch_variant<64, false, uint32_t>(p, count, stream);
+    }
+    if (p.stack_depth <= 16) {
+        return lds ? launch_variant<16, true, uint16_t>(p, count, stream) : launch_variant<16, false, uint16_t>(p, count, stream);
+    }
+    if (p.stack_depth <= 32) {
+        return lds ? launch_variant<32, true, uint16_t>(p, count, stream) : launch_variant<32, false, uint16_t>(p, count, stream);
+    }
+    if (p.stack_depth <= 64) return launch_variant<64, false, uint16_t>(p, count, stream);
+    return hipErrorInvalidValue;
 }
+
+hipError_t launch_render(const KParams &p, hipStream_t stream) { return launch_render_kernel(p, false, stream); }
+hipError_t launch_render_counting(const KParams &p, hipStream_t stream) { return launch_render_kernel(p, true, stream); }
 
 }  // namespace rrt
