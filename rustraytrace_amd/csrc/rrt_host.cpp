@@ -412,7 +412,9 @@ int32_t rrt_scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint32_
         }
         boxes[i] = pad(b);
     }
-    Builder bld(boxes, 2);
+    uint32_t max_leaf = 2;
+    if (const char *e = std::getenv("RRT_MAX_LEAF")) max_leaf = (uint32_t)std::min(15, std::max(1, std::atoi(e)));
+    Builder bld(boxes, max_leaf);
     if (n_spheres == 0) {
         bld.nodes.push_back(rrt::GNode{});
         bld.set_node(0, never_hit(), never_hit());
@@ -518,6 +520,8 @@ int32_t rrt_scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint32_
     const size_t scene_bytes = bld.nodes.size() * sizeof(rrt::GNode) + (size_t)n_spheres * sizeof(float4);
     p.scene_in_lds = scene_bytes <= rrt::kLdsSceneBudget && p.stack_depth <= 32;
     if (const char *e = std::getenv("RRT_SCENE_IN_LDS")) p.scene_in_lds = p.scene_in_lds && std::atoi(e) != 0;
+    p.trav_frac = 64;
+    if (const char *e = std::getenv("RRT_TRAV_FRAC")) p.trav_frac = (uint32_t)std::min(256, std::max(0, std::atoi(e)));
 
     RrtBvhInfo &bi = s->info;
     bi.n_nodes = (uint32_t)bld.nodes.size();

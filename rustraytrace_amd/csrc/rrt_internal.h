@@ -79,6 +79,7 @@ struct KParams {
     uint32_t n_prims;
     uint32_t stack_depth;   // entries needed (BVH depth + 1)
     uint32_t scene_in_lds;  // stage nodes + spheres in LDS per block
+    uint32_t trav_frac;     // leave the traversal loop when <= live*trav_frac/256 lanes still traverse
 };
 
 // Traversal stack entries held in LDS per lane: up to 64 (BVH depth <= 63).

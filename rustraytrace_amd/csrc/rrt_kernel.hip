@@ -211,46 +211,59 @@ struct LdsStack {
     __device__ __forceinline__ int load(int sp) const { return (int)base[sp * kBlock]; }
 };
 
+// Resumable BVH2 traversal: one call = one node. The state lives in registers (+ the LDS stack)
+// so a wave can leave the traversal loop while some lanes are still mid-tree.
+struct Trav {
+    V3 inv;
+    float a;
+    float closest;
+    int hit_prim;
+    int node;
+    int sp;
+};
+
+__device__ __forceinline__ void trav_begin(Trav &t, V3 d) {
+    t.inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);  // aabb.rs:58 adinv, hoisted per ray (same values)
+    t.a = dot(d, d);                                  // sphere.rs:27, hoisted per ray
+    t.closest = __builtin_inff();                      // camera.rs:187 Interval(0.001, INFINITY)
+    t.hit_prim = -1;
+    t.node = 0;
+    t.sp = 0;
+}
+
+// Visits node t.node: tests both children, tests leaf spheres in place, descends into the
+// nearer internal child and pushes the farther one. Returns true when the traversal is done.
 template <bool kCount, typename Stack>
-__device__ __forceinline__ int trace(const GNode *__restrict__ nodes, const float4 *__restrict__ prims, Stack &stack,
-                                     V3 o, V3 d, float &t_hit, Counters &cnt) {
-    const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-    const float a = dot(d, d);
-    float closest = __builtin_inff();
-    int hit_prim = -1;
-    int node = 0;
-    int sp = 0;
-    for (;;) {
-        const GNode n = nodes[node];
-        if (kCount) { cnt.nodes++; cnt.boxes += 2; }
-        float tn0 = 0.0f, tn1 = 0.0f;
-        bool h0 = box_hit(n.b0.x, n.b0.y, n.b0.z, n.b0.w, n.b1.x, n.b1.y, o, inv, 0.001f, closest, tn0);
-        bool h1 = box_hit(n.b1.z, n.b1.w, n.b2.x, n.b2.y, n.b2.z, n.b2.w, o, inv, 0.001f, closest, tn1);
-        if (h0 && n.link.z > 0) {
-            test_prims<kCount>(prims, n.link.x, n.link.z, o, d, a, closest, hit_prim, cnt);
-            h0 = false;
-        }
-        if (h1 && n.link.w > 0) {
-            test_prims<kCount>(prims, n.link.y, n.link.w, o, d, a, closest, hit_prim, cnt);
-            h1 = false;
-        }
-        if (h0 && h1) {
-            const bool first1 = tn1 < tn0;
-            stack.store(sp, first1 ? n.link.x : n.link.y);
-            ++sp;
-            node = first1 ? n.link.y : n.link.x;
-        } else if (h0) {
-            node = n.link.x;
-        } else if (h1) {
-            node = n.link.y;
-        } else {
-            if (sp == 0) break;
-            --sp;
-            node = stack.load(sp);
-        }
+__device__ __forceinline__ bool trav_step(const GNode *__restrict__ nodes, const float4 *__restrict__ prims,
+                                          Stack &stack, V3 o, V3 d, Trav &t, Counters &cnt) {
+    const GNode n = nodes[t.node];
+    if (kCount) { cnt.nodes++; cnt.boxes += 2; }
+    float tn0 = 0.0f, tn1 = 0.0f;
+    bool h0 = box_hit(n.b0.x, n.b0.y, n.b0.z, n.b0.w, n.b1.x, n.b1.y, o, t.inv, 0.001f, t.closest, tn0);
+    bool h1 = box_hit(n.b1.z, n.b1.w, n.b2.x, n.b2.y, n.b2.z, n.b2.w, o, t.inv, 0.001f, t.closest, tn1);
+    if (h0 && n.link.z > 0) {
+        test_prims<kCount>(prims, n.link.x, n.link.z, o, d, t.a, t.closest, t.hit_prim, cnt);
+        h0 = false;
     }
-    t_hit = closest;
-    return hit_prim;
+    if (h1 && n.link.w > 0) {
+        test_prims<kCount>(prims, n.link.y, n.link.w, o, d, t.a, t.closest, t.hit_prim, cnt);
+        h1 = false;
+    }
+    if (h0 && h1) {
+        const bool first1 = tn1 < tn0;
+        stack.store(t.sp, first1 ? n.link.x : n.link.y);
+        ++t.sp;
+        t.node = first1 ? n.link.y : n.link.x;
+    } else if (h0) {
+        t.node = n.link.x;
+    } else if (h1) {
+        t.node = n.link.y;
+    } else {
+        if (t.sp == 0) return true;
+        --t.sp;
+        t.node = stack.load(t.sp);
+    }
+    return false;
 }
 
 struct PathState {
@@ -302,14 +315,9 @@ __device__ __forceinline__ V3 texel(const KParams &P, int tex, float u, float v)
     return v3(cs * (float)px[0], cs * (float)px[1], cs * (float)px[2]);
 }
 
-// One bounce: closest hit, then scatter / RR. Returns true when the path has ended.
-template <bool kCount, typename Stack>
-__device__ __forceinline__ bool bounce(const KParams &P, const GNode *nodes, const float4 *prims, Stack &stack,
-                                       PathState &ps, Counters &cnt) {
-    if (ps.k >= P.max_depth) return true;  // ray_color: depth <= 0 -> 0
-    float t;
-    cnt.rays++;
-    const int prim = trace<kCount>(nodes, prims, stack, ps.o, ps.d, t, cnt);
+// After the closest-hit query of the current segment (prim < 0: miss): background, or
+// emission / scatter / RR (camera.rs:182-209). Returns true when the path has ended.
+__device__ __forceinline__ bool shade(const KParams &P, const float4 *prims, PathState &ps, float t, int prim) {
     if (prim < 0) {
         V3 bg;
         if (P.bg_mode == 1u) {
@@ -433,18 +441,48 @@ __device__ __forceinline__ void render_body(const KParams &P) {
         V3 sum = v3(0.0f, 0.0f, 0.0f);
         uint32_t s = P.sample_begin;
         PathState ps;
+        Trav tr;
         if (s < P.sample_end) {
             ps.rng = splitmix64(key + s);
             camera_ray(P, x, y, ps);
         }
+        bool need_ray = true;  // the lane must start the next segment of its path
+        bool tracing = false;
         while (s < P.sample_end) {
-            if (bounce<kCount>(P, nodes, prims, stack, ps, cnt)) {
-                sum = add(sum, ps.L);  // pixel_color += ray_color(..) (camera.rs:73-76)
-                cnt.paths++;
-                ++s;
-                if (s < P.sample_end) {
-                    ps.rng = splitmix64(key + s);
-                    camera_ray(P, x, y, ps);
+            if (need_ray) {
+                if (ps.k >= P.max_depth) {  // ray_color: depth <= 0 -> 0 (no query)
+                    sum = add(sum, ps.L);
+                    cnt.paths++;
+                    ++s;
+                    if (s < P.sample_end) {
+                        ps.rng = splitmix64(key + s);
+                        camera_ray(P, x, y, ps);
+                    }
+                    continue;
+                }
+                trav_begin(tr, ps.d);
+                cnt.rays++;
+                need_ray = false;
+                tracing = true;
+            }
+            // Traverse until too few lanes of the wave are still in the tree, then let the
+            // finished lanes shade and fetch their next segment (wave-uniform ballot exit).
+            const uint32_t live = (uint32_t)__popcll(__ballot(1));
+            const uint32_t min_active = (live * P.trav_frac) >> 8;
+            for (;;) {
+                if (tracing && trav_step<kCount>(nodes, prims, stack, ps.o, ps.d, tr, cnt)) tracing = false;
+                if ((uint32_t)__popcll(__ballot(tracing)) <= min_active) break;
+            }
+            if (!tracing) {
+                need_ray = true;
+                if (shade(P, prims, ps, tr.closest, tr.hit_prim)) {
+                    sum = add(sum, ps.L);  // pixel_color += ray_color(..) (camera.rs:73-76)
+                    cnt.paths++;
+                    ++s;
+                    if (s < P.sample_end) {
+                        ps.rng = splitmix64(key + s);
+                        camera_ray(P, x, y, ps);
+                    }
                 }
             }
         }

@@ -1,0 +1,34 @@
+"""Render a config a few times through the device API (a short, fixed workload for rocprofv3)."""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="C2")
+    ap.add_argument("--spp", type=int, default=64)
+    ap.add_argument("--width", type=int, default=None)
+    ap.add_argument("--iters", type=int, default=2)
+    a = ap.parse_args()
+    import torch
+
+    import rustraytrace_amd as rrt
+
+    kw = dict(samples_per_pixel=a.spp)
+    if a.width:
+        kw["image_width"] = a.width
+    scene = rrt.config_scene(a.config, **kw)
+    ds = rrt.DeviceScene(scene)
+    tile = ds.tile(16, 0, 1, 0, scene.spp)
+    buf = torch.empty((scene.height, scene.width, 4), dtype=torch.float32, device="cuda:0")
+    for _ in range(a.iters):
+        ds.render_tile_async(tile, buf.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    print(a.config, scene.width, scene.height, scene.spp, ds.counters(), ds.bvh_info())
+
+
+if __name__ == "__main__":
+    main()
