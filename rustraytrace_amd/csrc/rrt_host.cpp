@@ -152,18 +152,16 @@ float f32_up(double d) {
 struct Builder {
     const std::vector<Aabb> &boxes;
     std::vector<uint32_t> objs;
-    std::vector<rrt::GNode> nodes;
     uint32_t max_leaf;
-    uint32_t max_depth = 0;
-    uint32_t n_leaves = 0;
-    uint32_t max_leaf_seen = 0;
 
-    struct Ref {
-        bool leaf;
-        int32_t index;  // node index or first primitive
-        int32_t count;
+    // Binary SAH tree (bvh.rs:16-156 split choice), leaves of <= max_leaf spheres.
+    struct BNode {
         Aabb box;
+        int32_t left = -1, right = -1;  // children (internal)
+        int32_t first = 0, count = 0;   // primitive range (leaf)
+        bool leaf = false;
     };
+    std::vector<BNode> bin;
 
     Builder(const std::vector<Aabb> &b, uint32_t leaf) : boxes(b), max_leaf(leaf) {
         objs.resize(b.size());
@@ -249,42 +247,189 @@ struct Builder {
         return lo + mid;
     }
 
-    Ref build(size_t lo, size_t hi, uint32_t depth) {
+    int32_t build(size_t lo, size_t hi) {
         Aabb bbox = aabb_empty();
         for (size_t i = lo; i < hi; ++i) bbox = aabb_union(bbox, boxes[objs[i]]);
-        if (depth > max_depth) max_depth = depth;
+        const int32_t me = (int32_t)bin.size();
+        bin.push_back(BNode{});
+        bin[me].box = bbox;
         const size_t span = hi - lo;
         if (span <= max_leaf) {
-            n_leaves++;
-            if (span > max_leaf_seen) max_leaf_seen = (uint32_t)span;
-            return Ref{true, (int32_t)lo, (int32_t)span, bbox};
+            bin[me].leaf = true;
+            bin[me].first = (int32_t)lo;
+            bin[me].count = (int32_t)span;
+            return me;
         }
         const size_t mid = split(lo, hi, bbox);
-        const int32_t me = (int32_t)nodes.size();
-        nodes.push_back(rrt::GNode{});
-        Ref l = build(lo, mid, depth + 1);
-        Ref r = build(mid, hi, depth + 1);
-        set_node(me, l, r);
-        return Ref{false, me, 0, bbox};
-    }
-
-    void set_node(int32_t me, const Ref &l, const Ref &r) {
-        rrt::GNode &n = nodes[me];
-        auto lo = [](const Ref &c, int a) { return f32_down(c.box.ax[a].min); };
-        auto hi = [](const Ref &c, int a) { return f32_up(c.box.ax[a].max); };
-        n.b0 = make_float4(lo(l, 0), hi(l, 0), lo(l, 1), hi(l, 1));
-        n.b1 = make_float4(lo(l, 2), hi(l, 2), lo(r, 0), hi(r, 0));
-        n.b2 = make_float4(lo(r, 1), hi(r, 1), lo(r, 2), hi(r, 2));
-        n.link = make_int4(l.index, r.index, l.leaf ? l.count : 0, r.leaf ? r.count : 0);
+        const int32_t l = build(lo, mid);
+        const int32_t r = build(mid, hi);
+        bin[me].left = l;
+        bin[me].right = r;
+        return me;
     }
 };
 
-// A child that no ray can enter: a point box at 1e30 (rejected for every direction,
+// Flattened device BVH (either width) plus the numbers the kernel needs.
+struct FlatBvh {
+    std::vector<uint8_t> bytes;
+    uint32_t n_nodes = 0, n_leaves = 0, max_depth = 0, max_leaf = 0, stack_need = 0, width = 2;
+};
+
+void put_box(float *lo, float *hi, const Aabb &b) {
+    for (int a = 0; a < 3; ++a) {
+        lo[a] = f32_down(b.ax[a].min);
+        hi[a] = f32_up(b.ax[a].max);
+    }
+}
+
+// A child slot no ray can enter: a point box at 1e30 (rejected for every direction,
 // including zero components where the slab test produces +-inf).
-Builder::Ref never_hit() {
+Aabb never_hit_box() {
     Aabb b;
     for (int i = 0; i < 3; ++i) b.ax[i] = Interval{1e30, 1e30};
-    return Builder::Ref{true, 0, 0, b};
+    return b;
+}
+
+// BVH2: the binary tree as is, root = node 0, both child boxes stored in the parent.
+FlatBvh flatten2(const Builder &bd, int32_t root) {
+    FlatBvh f;
+    std::vector<rrt::GNode> out;
+    struct Item { int32_t bin; int32_t slot; };
+    auto child_ref = [&](int32_t c, float *lo, float *hi, int32_t &ref, int32_t &cnt, std::vector<Item> &todo) {
+        const Builder::BNode &b = bd.bin[c];
+        put_box(lo, hi, b.leaf && b.count == 0 ? never_hit_box() : b.box);
+        if (b.leaf) {
+            ref = b.first;
+            cnt = b.count;
+            f.n_leaves++;
+            f.max_leaf = std::max<uint32_t>(f.max_leaf, (uint32_t)b.count);
+        } else {
+            ref = (int32_t)out.size();
+            cnt = 0;
+            out.push_back(rrt::GNode{});
+            todo.push_back(Item{c, ref});
+        }
+    };
+    std::vector<std::pair<Item, uint32_t>> stack;  // (item, depth)
+    out.push_back(rrt::GNode{});
+    std::vector<Item> todo;
+    const Builder::BNode &r = bd.bin[root];
+    if (r.leaf) {  // whole scene in one leaf: child 0 = the leaf, child 1 = never hit
+        float lo0[3], hi0[3], lo1[3], hi1[3];
+        int32_t ref0, cnt0;
+        child_ref(root, lo0, hi0, ref0, cnt0, todo);
+        put_box(lo1, hi1, never_hit_box());
+        rrt::GNode &n = out[0];
+        n.b0 = make_float4(lo0[0], hi0[0], lo0[1], hi0[1]);
+        n.b1 = make_float4(lo0[2], hi0[2], lo1[0], hi1[0]);
+        n.b2 = make_float4(lo1[1], hi1[1], lo1[2], hi1[2]);
+        n.link = make_int4(ref0, 0, cnt0, 0);
+        f.max_depth = 1;
+    } else {
+        stack.push_back({Item{root, 0}, 0});
+        while (!stack.empty()) {
+            auto [it, depth] = stack.back();
+            stack.pop_back();
+            f.max_depth = std::max(f.max_depth, depth + 1);
+            const Builder::BNode &b = bd.bin[it.bin];
+            float lo0[3], hi0[3], lo1[3], hi1[3];
+            int32_t ref0, cnt0, ref1, cnt1;
+            todo.clear();
+            child_ref(b.left, lo0, hi0, ref0, cnt0, todo);
+            child_ref(b.right, lo1, hi1, ref1, cnt1, todo);
+            rrt::GNode &n = out[it.slot];
+            n.b0 = make_float4(lo0[0], hi0[0], lo0[1], hi0[1]);
+            n.b1 = make_float4(lo0[2], hi0[2], lo1[0], hi1[0]);
+            n.b2 = make_float4(lo1[1], hi1[1], lo1[2], hi1[2]);
+            n.link = make_int4(ref0, ref1, cnt0, cnt1);
+            for (auto &t : todo) stack.push_back({t, depth + 1});
+        }
+    }
+    f.n_nodes = (uint32_t)out.size();
+    f.stack_need = f.max_depth + 1;
+    f.width = 2;
+    f.bytes.resize(out.size() * sizeof(rrt::GNode));
+    std::memcpy(f.bytes.data(), out.data(), f.bytes.size());
+    return f;
+}
+
+// BVH4: collapse the binary tree — each wide node adopts up to 4 descendants, repeatedly
+// opening the internal candidate with the largest surface area (the standard SAH-guided
+// collapse). Empty slots get the never-hit box.
+FlatBvh flatten4(const Builder &bd, int32_t root) {
+    FlatBvh f;
+    std::vector<rrt::GNode4> out;
+    struct Item { int32_t bin; int32_t slot; uint32_t depth; };
+    std::vector<Item> stack;
+    out.push_back(rrt::GNode4{});
+    stack.push_back(Item{root, 0, 0});
+    while (!stack.empty()) {
+        Item it = stack.back();
+        stack.pop_back();
+        f.max_depth = std::max(f.max_depth, it.depth + 1);
+        std::vector<int32_t> kids;
+        const Builder::BNode &b = bd.bin[it.bin];
+        if (b.leaf) kids.push_back(it.bin);
+        else { kids.push_back(b.left); kids.push_back(b.right); }
+        while (kids.size() < 4) {
+            int best = -1;
+            double best_area = -1.0;
+            for (size_t i = 0; i < kids.size(); ++i) {
+                const Builder::BNode &k = bd.bin[kids[i]];
+                if (k.leaf) continue;
+                const double area = surface_area(k.box);
+                if (area > best_area) { best_area = area; best = (int)i; }
+            }
+            if (best < 0) break;
+            const Builder::BNode &k = bd.bin[kids[best]];
+            kids[best] = k.left;
+            kids.insert(kids.begin() + best + 1, k.right);
+        }
+        float lo[4][3], hi[4][3];
+        int32_t child[4], count[4];
+        for (int c = 0; c < 4; ++c) {
+            if (c >= (int)kids.size()) {
+                put_box(lo[c], hi[c], never_hit_box());
+                child[c] = 0;
+                count[c] = 0;
+                continue;
+            }
+            const Builder::BNode &k = bd.bin[kids[c]];
+            if (k.leaf && k.count == 0) {  // empty scene: nothing to enter
+                put_box(lo[c], hi[c], never_hit_box());
+                child[c] = 0;
+                count[c] = 0;
+                continue;
+            }
+            put_box(lo[c], hi[c], k.box);
+            if (k.leaf) {
+                child[c] = k.first;
+                count[c] = k.count;
+                f.n_leaves++;
+                f.max_leaf = std::max<uint32_t>(f.max_leaf, (uint32_t)k.count);
+            } else {
+                child[c] = (int32_t)out.size();
+                count[c] = 0;
+                out.push_back(rrt::GNode4{});
+                stack.push_back(Item{kids[c], child[c], it.depth + 1});
+            }
+        }
+        rrt::GNode4 &n = out[it.slot];
+        n.lox = make_float4(lo[0][0], lo[1][0], lo[2][0], lo[3][0]);
+        n.hix = make_float4(hi[0][0], hi[1][0], hi[2][0], hi[3][0]);
+        n.loy = make_float4(lo[0][1], lo[1][1], lo[2][1], lo[3][1]);
+        n.hiy = make_float4(hi[0][1], hi[1][1], hi[2][1], hi[3][1]);
+        n.loz = make_float4(lo[0][2], lo[1][2], lo[2][2], lo[3][2]);
+        n.hiz = make_float4(hi[0][2], hi[1][2], hi[2][2], hi[3][2]);
+        n.child = make_int4(child[0], child[1], child[2], child[3]);
+        n.count = make_int4(count[0], count[1], count[2], count[3]);
+    }
+    f.n_nodes = (uint32_t)out.size();
+    f.stack_need = 3 * f.max_depth + 1;  // <= 3 pushes per level
+    f.width = 4;
+    f.bytes.resize(out.size() * sizeof(rrt::GNode4));
+    std::memcpy(f.bytes.data(), out.data(), f.bytes.size());
+    return f;
 }
 
 }  // namespace
@@ -292,7 +437,7 @@ Builder::Ref never_hit() {
 // ------------------------------------------------------------------------------------
 struct RrtScene {
     int device = 0;
-    rrt::GNode *d_nodes = nullptr;
+    uint8_t *d_nodes = nullptr;
     float4 *d_prim_cr = nullptr;
     uint32_t *d_prim_mat = nullptr;
     rrt::GMaterial *d_mats = nullptr;
@@ -412,22 +557,24 @@ int32_t rrt_scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint32_
         }
         boxes[i] = pad(b);
     }
-    uint32_t max_leaf = 2;
+    uint32_t max_leaf = 3;
     if (const char *e = std::getenv("RRT_MAX_LEAF")) max_leaf = (uint32_t)std::min(15, std::max(1, std::atoi(e)));
+    uint32_t width = 2;
+    if (const char *e = std::getenv("RRT_BVH_WIDTH")) width = std::atoi(e) == 4 ? 4 : 2;
     Builder bld(boxes, max_leaf);
-    if (n_spheres == 0) {
-        bld.nodes.push_back(rrt::GNode{});
-        bld.set_node(0, never_hit(), never_hit());
+    FlatBvh fb;
+    if (n_spheres == 0) {  // root with two never-hit children
+        Builder::BNode empty;
+        empty.box = never_hit_box();
+        empty.leaf = true;
+        bld.bin.push_back(empty);
+        fb = width == 4 ? flatten4(bld, 0) : flatten2(bld, 0);
     } else {
-        Builder::Ref root = bld.build(0, n_spheres, 0);
-        if (root.leaf) {
-            bld.nodes.push_back(rrt::GNode{});
-            bld.set_node(0, root, never_hit());
-            bld.max_depth = 1;
-        }
+        const int32_t root = bld.build(0, n_spheres);
+        fb = width == 4 ? flatten4(bld, root) : flatten2(bld, root);
     }
-    if (bld.max_depth + 1 > (uint32_t)rrt::kMaxStackDepth)
-        return fail(RRT_E_INVALID, "BVH depth " + std::to_string(bld.max_depth) + " exceeds the LDS stack");
+    if (fb.stack_need > (uint32_t)rrt::kMaxStackDepth)
+        return fail(RRT_E_INVALID, "BVH depth " + std::to_string(fb.max_depth) + " exceeds the LDS stack");
 
     std::vector<float4> prim_cr(n_spheres);
     std::vector<uint32_t> prim_mat(n_spheres);
@@ -467,7 +614,7 @@ int32_t rrt_scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint32_
     int rc = RRT_OK;
     do {
         if (hipSetDevice(device) != hipSuccess) { rc = fail(RRT_E_HIP, "hipSetDevice failed"); break; }
-        if ((rc = upload(&s->d_nodes, bld.nodes.data(), bld.nodes.size(), "nodes"))) break;
+        if ((rc = upload(&s->d_nodes, fb.bytes.data(), fb.bytes.size(), "nodes"))) break;
         if ((rc = upload(&s->d_prim_cr, prim_cr.data(), prim_cr.size(), "spheres"))) break;
         if ((rc = upload(&s->d_prim_mat, prim_mat.data(), prim_mat.size(), "sphere materials"))) break;
         if ((rc = upload(&s->d_mats, mats.data(), mats.size(), "materials"))) break;
@@ -514,21 +661,24 @@ int32_t rrt_scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint32_
     p.flags = flags;
     p.width = (uint32_t)wf;
     p.height = (uint32_t)hf;
-    p.n_nodes = (uint32_t)bld.nodes.size();
+    p.n_nodes = fb.n_nodes;
     p.n_prims = n_spheres;
-    p.stack_depth = bld.max_depth + 1;
-    const size_t scene_bytes = bld.nodes.size() * sizeof(rrt::GNode) + (size_t)n_spheres * sizeof(float4);
-    p.scene_in_lds = scene_bytes <= rrt::kLdsSceneBudget && p.stack_depth <= 32;
+    p.stack_depth = fb.stack_need;
+    p.bvh_width = fb.width;
+    const size_t scene_bytes = fb.bytes.size() + (size_t)n_spheres * sizeof(float4);
+    p.scene_in_lds = scene_bytes <= rrt::kLdsSceneBudget;
     if (const char *e = std::getenv("RRT_SCENE_IN_LDS")) p.scene_in_lds = p.scene_in_lds && std::atoi(e) != 0;
-    p.trav_frac = 64;
+    p.trav_frac = 32;
+    p.min_waves = 5;
+    if (const char *e = std::getenv("RRT_MIN_WAVES")) p.min_waves = (uint32_t)std::atoi(e);
     if (const char *e = std::getenv("RRT_TRAV_FRAC")) p.trav_frac = (uint32_t)std::min(256, std::max(0, std::atoi(e)));
 
     RrtBvhInfo &bi = s->info;
-    bi.n_nodes = (uint32_t)bld.nodes.size();
-    bi.n_leaves = bld.n_leaves;
-    bi.max_depth = bld.max_depth;
-    bi.max_leaf_size = bld.max_leaf_seen;
-    bi.node_bytes = bld.nodes.size() * sizeof(rrt::GNode);
+    bi.n_nodes = fb.n_nodes;
+    bi.n_leaves = fb.n_leaves;
+    bi.max_depth = fb.max_depth;
+    bi.max_leaf_size = fb.max_leaf;
+    bi.node_bytes = fb.bytes.size();
     bi.prim_bytes = (uint64_t)n_spheres * (sizeof(float4) + sizeof(uint32_t));
     *out = s;
     return RRT_OK;

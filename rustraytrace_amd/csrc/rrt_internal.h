@@ -23,6 +23,15 @@ struct alignas(16) GNode {
 };
 static_assert(sizeof(GNode) == 64, "GNode must be 64 B");
 
+// BVH4 node, 128 B: the boxes of 4 children as SoA float4s (child c in component c), the
+// child refs and primitive counts (0 = internal node). Collapsed from the binary SAH tree.
+struct alignas(16) GNode4 {
+    float4 lox, hix, loy, hiy, loz, hiz;
+    int4 child;
+    int4 count;
+};
+static_assert(sizeof(GNode4) == 128, "GNode4 must be 128 B");
+
 // Material, SoA split into two 16-B records (kind-dependent payload).
 //   a = albedo.rgb (or emitted rgb for lights), fuzz (pre-clamped to <= 1, material.rs:49)
 //   b = kind, ref_idx bits, texture index, 0
@@ -40,7 +49,7 @@ struct GTexture {
 
 // Everything the megakernel needs, passed by value (kernarg segment).
 struct KParams {
-    const GNode *nodes;
+    const void *nodes;           // GNode[] (bvh_width 2) or GNode4[] (bvh_width 4)
     const float4 *prim_cr;       // sphere center.xyz, radius — in BVH leaf order
     const uint32_t *prim_mat;    // material index per primitive (leaf order)
     const GMaterial *mats;
@@ -80,6 +89,8 @@ struct KParams {
     uint32_t stack_depth;   // entries needed (BVH depth + 1)
     uint32_t scene_in_lds;  // stage nodes + spheres in LDS per block
     uint32_t trav_frac;     // leave the traversal loop when <= live*trav_frac/256 lanes still traverse
+    uint32_t bvh_width;     // 2 or 4
+    uint32_t min_waves;     // launch-bounds occupancy request (waves per SIMD)
 };
 
 // Traversal stack entries held in LDS per lane: up to 64 (BVH depth <= 63).

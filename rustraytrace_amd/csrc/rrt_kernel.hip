@@ -23,6 +23,8 @@
 // equal in exact arithmetic (documented in DESIGN.md).
 #include "rrt_internal.h"
 
+#include <type_traits>
+
 namespace rrt {
 namespace {
 
@@ -140,31 +142,26 @@ __device__ __forceinline__ float rrt_atan2f(float y, float x) {
     return z;
 }
 
-// ---- Aabb::hit (aabb.rs:52-85), branch-free and decision-identical ---------------------------
-// The reference updates the interval per axis with `if t0 < t1 {min<-t0 if t0>min; max<-t1 if
-// t1<max} else {min<-t1 if t1>min; max<-t0 if t0<max}` and returns false as soon as
-// max <= min. Here: near/far are selected with the same `t0 < t1` test, then min/max are
-// updated with IEEE maxNum/minNum (v_max_f32 / v_min_f32), which return the non-NaN operand:
-// exactly the reference's `if x > min` / `if x < max` (a NaN near/far leaves the bound alone,
-// as the reference's false comparison does; ties differ only in the sign of a zero). min and
-// max are never NaN, so testing max <= min once after all three axes equals the per-axis
-// early return (the interval only shrinks). tnear = the entry distance, for child ordering.
-__device__ __forceinline__ void slab(float lo, float hi, float o, float adinv, float &tmin, float &tmax) {
-    const float t0 = (lo - o) * adinv;
-    const float t1 = (hi - o) * adinv;
-    const bool lt = t0 < t1;
-    const float nr = lt ? t0 : t1;
-    const float fr = lt ? t1 : t0;
-    tmin = __builtin_fmaxf(tmin, nr);
-    tmax = __builtin_fminf(tmax, fr);
-}
+// ---- ray/box slab test (role of Aabb::hit, aabb.rs:52-85) -----------------------------------
+// A box test only prunes: which sphere is hit, and at which t, is decided by the sphere test
+// alone (sphere.rs:24-51 against the running closest hit), so the slab arithmetic need not be
+// the reference's op for op. This is the standard GPU form: t = lo*inv - o*inv as one FMA per
+// plane, near/far via min/max, entry = max3, exit = min3. It can only differ from the
+// reference's slab in grazing cases at the last ulp, where the reference's own result already
+// depends on its BVH topology ("Parity"). A zero direction component gives
+// inv = +-inf and NaN plane distances, which min/max ignore: that axis then constrains
+// nothing (conservative: never a wrong rejection).
 __device__ __forceinline__ bool box_hit(float lx, float hx, float ly, float hy, float lz, float hz,
-                                        V3 o, V3 inv, float tmin, float tmax, float &tnear) {
-    slab(lx, hx, o.x, inv.x, tmin, tmax);
-    slab(ly, hy, o.y, inv.y, tmin, tmax);
-    slab(lz, hz, o.z, inv.z, tmin, tmax);
-    tnear = tmin;
-    return !(tmax <= tmin);
+                                        V3 inv, V3 oi, float tmin, float tmax, float &tnear) {
+    const float x0 = __builtin_fmaf(lx, inv.x, -oi.x), x1 = __builtin_fmaf(hx, inv.x, -oi.x);
+    const float y0 = __builtin_fmaf(ly, inv.y, -oi.y), y1 = __builtin_fmaf(hy, inv.y, -oi.y);
+    const float z0 = __builtin_fmaf(lz, inv.z, -oi.z), z1 = __builtin_fmaf(hz, inv.z, -oi.z);
+    const float nr = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(x0, x1), __builtin_fminf(y0, y1)),
+                                     __builtin_fmaxf(__builtin_fminf(z0, z1), tmin));
+    const float fr = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(x0, x1), __builtin_fmaxf(y0, y1)),
+                                     __builtin_fminf(__builtin_fmaxf(z0, z1), tmax));
+    tnear = nr;
+    return nr < fr;
 }
 
 struct Counters {
@@ -215,6 +212,7 @@ struct LdsStack {
 // so a wave can leave the traversal loop while some lanes are still mid-tree.
 struct Trav {
     V3 inv;
+    V3 oi;  // o * inv
     float a;
     float closest;
     int hit_prim;
@@ -222,8 +220,9 @@ struct Trav {
     int sp;
 };
 
-__device__ __forceinline__ void trav_begin(Trav &t, V3 d) {
-    t.inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);  // aabb.rs:58 adinv, hoisted per ray (same values)
+__device__ __forceinline__ void trav_begin(Trav &t, V3 o, V3 d) {
+    t.inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);  // aabb.rs:58 adinv, hoisted per ray
+    t.oi = v3(o.x * t.inv.x, o.y * t.inv.y, o.z * t.inv.z);
     t.a = dot(d, d);                                  // sphere.rs:27, hoisted per ray
     t.closest = __builtin_inff();                      // camera.rs:187 Interval(0.001, INFINITY)
     t.hit_prim = -1;
@@ -239,8 +238,8 @@ __device__ __forceinline__ bool trav_step(const GNode *__restrict__ nodes, const
     const GNode n = nodes[t.node];
     if (kCount) { cnt.nodes++; cnt.boxes += 2; }
     float tn0 = 0.0f, tn1 = 0.0f;
-    bool h0 = box_hit(n.b0.x, n.b0.y, n.b0.z, n.b0.w, n.b1.x, n.b1.y, o, t.inv, 0.001f, t.closest, tn0);
-    bool h1 = box_hit(n.b1.z, n.b1.w, n.b2.x, n.b2.y, n.b2.z, n.b2.w, o, t.inv, 0.001f, t.closest, tn1);
+    bool h0 = box_hit(n.b0.x, n.b0.y, n.b0.z, n.b0.w, n.b1.x, n.b1.y, t.inv, t.oi, 0.001f, t.closest, tn0);
+    bool h1 = box_hit(n.b1.z, n.b1.w, n.b2.x, n.b2.y, n.b2.z, n.b2.w, t.inv, t.oi, 0.001f, t.closest, tn1);
     if (h0 && n.link.z > 0) {
         test_prims<kCount>(prims, n.link.x, n.link.z, o, d, t.a, t.closest, t.hit_prim, cnt);
         h0 = false;
@@ -263,6 +262,65 @@ __device__ __forceinline__ bool trav_step(const GNode *__restrict__ nodes, const
         --t.sp;
         t.node = stack.load(t.sp);
     }
+    return false;
+}
+
+// BVH4 step: test the 4 child boxes, test leaf children's spheres in place, then descend
+// into the nearest internal child and push the others farthest-first (5-exchange sort).
+template <bool kCount, typename Stack>
+__device__ __forceinline__ bool trav_step4(const GNode4 *__restrict__ nodes, const float4 *__restrict__ prims,
+                                           Stack &stack, V3 o, V3 d, Trav &t, Counters &cnt) {
+    const GNode4 n = nodes[t.node];
+    if (kCount) { cnt.nodes++; cnt.boxes += 4; }
+    const float lox[4] = {n.lox.x, n.lox.y, n.lox.z, n.lox.w}, hix[4] = {n.hix.x, n.hix.y, n.hix.z, n.hix.w};
+    const float loy[4] = {n.loy.x, n.loy.y, n.loy.z, n.loy.w}, hiy[4] = {n.hiy.x, n.hiy.y, n.hiy.z, n.hiy.w};
+    const float loz[4] = {n.loz.x, n.loz.y, n.loz.z, n.loz.w}, hiz[4] = {n.hiz.x, n.hiz.y, n.hiz.z, n.hiz.w};
+    const int child[4] = {n.child.x, n.child.y, n.child.z, n.child.w};
+    const int count[4] = {n.count.x, n.count.y, n.count.z, n.count.w};
+    float key[4];
+    int idx[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        float tn = 0.0f;
+        const bool h = box_hit(lox[c], hix[c], loy[c], hiy[c], loz[c], hiz[c], t.inv, t.oi, 0.001f, t.closest, tn);
+        key[c] = h ? tn : __builtin_inff();
+        idx[c] = child[c];
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        if (count[c] > 0) {
+            if (key[c] < __builtin_inff()) test_prims<kCount>(prims, child[c], count[c], o, d, t.a, t.closest, t.hit_prim, cnt);
+            key[c] = __builtin_inff();
+        }
+    }
+    // a child whose entry lies beyond the (possibly shrunk) closest hit cannot contain a closer hit
+#pragma unroll
+    for (int c = 0; c < 4; ++c) key[c] = (key[c] < t.closest) ? key[c] : __builtin_inff();
+    auto cswap = [&](int i, int j) {
+        const bool sw = key[j] < key[i];
+        const float ki = key[i], kj = key[j];
+        const int ii = idx[i], ij = idx[j];
+        key[i] = sw ? kj : ki;
+        key[j] = sw ? ki : kj;
+        idx[i] = sw ? ij : ii;
+        idx[j] = sw ? ii : ij;
+    };
+    cswap(0, 1);
+    cswap(2, 3);
+    cswap(0, 2);
+    cswap(1, 3);
+    cswap(1, 2);
+    const float kInf = __builtin_inff();
+    if (key[3] < kInf) { stack.store(t.sp, idx[3]); ++t.sp; }
+    if (key[2] < kInf) { stack.store(t.sp, idx[2]); ++t.sp; }
+    if (key[1] < kInf) { stack.store(t.sp, idx[1]); ++t.sp; }
+    if (key[0] < kInf) {
+        t.node = idx[0];
+        return false;
+    }
+    if (t.sp == 0) return true;
+    --t.sp;
+    t.node = stack.load(t.sp);
     return false;
 }
 
@@ -396,23 +454,24 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
     return v;
 }
 
-template <int kStack, bool kLds, bool kCount, typename StackT>
+template <bool kLds, bool kCount, typename StackT, bool kWide>
 __device__ __forceinline__ void render_body(const KParams &P) {
     extern __shared__ uint4 lds_dyn[];
-    // LDS layout: [traversal stack: kStack x kBlock x StackT][nodes][primitives]
+    // LDS layout: [traversal stack: stack_depth x kBlock x StackT, 16-B aligned][nodes][primitives]
     StackT *lds_stack = reinterpret_cast<StackT *>(lds_dyn);
-    const GNode *nodes = P.nodes;
+    using Node = typename std::conditional<kWide, GNode4, GNode>::type;
+    const Node *nodes = reinterpret_cast<const Node *>(P.nodes);
     const float4 *prims = P.prim_cr;
     if constexpr (kLds) {
         // Stage the whole BVH + spheres (KB-sized) in LDS once per block.
-        uint4 *dst = lds_dyn + (kStack * kBlock * sizeof(StackT)) / 16;
+        uint4 *dst = lds_dyn + (P.stack_depth * kBlock * sizeof(StackT) + 15u) / 16u;
         const uint4 *src_n = reinterpret_cast<const uint4 *>(P.nodes);
-        const uint32_t nn = P.n_nodes * 4u;
+        const uint32_t nn = P.n_nodes * (uint32_t)(sizeof(Node) / 16);
         for (uint32_t i = threadIdx.x; i < nn; i += kBlock) dst[i] = src_n[i];
         const uint4 *src_p = reinterpret_cast<const uint4 *>(P.prim_cr);
         for (uint32_t i = threadIdx.x; i < P.n_prims; i += kBlock) dst[nn + i] = src_p[i];
         __syncthreads();
-        nodes = reinterpret_cast<const GNode *>(dst);
+        nodes = reinterpret_cast<const Node *>(dst);
         prims = reinterpret_cast<const float4 *>(dst + nn);
     }
     LdsStack<StackT> stack;
@@ -460,7 +519,7 @@ __device__ __forceinline__ void render_body(const KParams &P) {
                     }
                     continue;
                 }
-                trav_begin(tr, ps.d);
+                trav_begin(tr, ps.o, ps.d);
                 cnt.rays++;
                 need_ray = false;
                 tracing = true;
@@ -470,7 +529,12 @@ __device__ __forceinline__ void render_body(const KParams &P) {
             const uint32_t live = (uint32_t)__popcll(__ballot(1));
             const uint32_t min_active = (live * P.trav_frac) >> 8;
             for (;;) {
-                if (tracing && trav_step<kCount>(nodes, prims, stack, ps.o, ps.d, tr, cnt)) tracing = false;
+                if (tracing) {
+                    bool fin;
+                    if constexpr (kWide) fin = trav_step4<kCount>(nodes, prims, stack, ps.o, ps.d, tr, cnt);
+                    else fin = trav_step<kCount>(nodes, prims, stack, ps.o, ps.d, tr, cnt);
+                    if (fin) tracing = false;
+                }
                 if ((uint32_t)__popcll(__ballot(tracing)) <= min_active) break;
             }
             if (!tracing) {
@@ -508,20 +572,31 @@ __device__ __forceinline__ void render_body(const KParams &P) {
     }
 }
 
-template <int kStack, bool kLds, bool kCount, typename StackT>
-__global__ __launch_bounds__(kBlock) void rrt_render(KParams P) {
-    render_body<kStack, kLds, kCount, StackT>(P);
+template <bool kLds, bool kCount, typename StackT, bool kWide, int kWaves>
+__global__ __launch_bounds__(kBlock, kWaves) void rrt_render(KParams P) {
+    render_body<kLds, kCount, StackT, kWide>(P);
 }
 
-template <int kStack, bool kLds, typename StackT>
+template <bool kLds, typename StackT, bool kWide, int kWaves = 1>
 hipError_t launch_variant(const KParams &p, bool count, hipStream_t stream) {
     const uint32_t blocks = (p.n_work_tiles + (kBlock / 64) - 1) / (kBlock / 64);
     if (blocks == 0) return hipSuccess;
-    size_t lds = (size_t)kStack * kBlock * sizeof(StackT);
-    if (kLds) lds += (size_t)p.n_nodes * sizeof(GNode) + (size_t)p.n_prims * sizeof(float4);
-    if (count) hipLaunchKernelGGL((rrt_render<kStack, kLds, true, StackT>), dim3(blocks), dim3(kBlock), lds, stream, p);
-    else hipLaunchKernelGGL((rrt_render<kStack, kLds, false, StackT>), dim3(blocks), dim3(kBlock), lds, stream, p);
+    size_t lds = ((size_t)p.stack_depth * kBlock * sizeof(StackT) + 15u) / 16u * 16u;
+    if (kLds) lds += (size_t)p.n_nodes * (kWide ? sizeof(GNode4) : sizeof(GNode)) + (size_t)p.n_prims * sizeof(float4);
+    if (count)
+        hipLaunchKernelGGL((rrt_render<kLds, true, StackT, kWide, kWaves>), dim3(blocks), dim3(kBlock), lds, stream, p);
+    else
+        hipLaunchKernelGGL((rrt_render<kLds, false, StackT, kWide, kWaves>), dim3(blocks), dim3(kBlock), lds, stream, p);
     return hipGetLastError();
+}
+
+template <bool kWide>
+hipError_t launch_width(const KParams &p, bool count, hipStream_t stream) {
+    if (p.stack_depth > (uint32_t)kMaxStackDepth) return hipErrorInvalidValue;
+    if (p.n_nodes > 65535u) return launch_variant<false, uint32_t, kWide>(p, count, stream);
+    if (!kWide && p.scene_in_lds && p.min_waves >= 6) return launch_variant<true, uint16_t, kWide, 6>(p, count, stream);
+    return p.scene_in_lds ? launch_variant<true, uint16_t, kWide>(p, count, stream)
+                          : launch_variant<false, uint16_t, kWide>(p, count, stream);
 }
 
 }  // namespace
@@ -531,22 +606,9 @@ size_t lds_scene_bytes(const KParams &p) {
 }
 
 hipError_t launch_render_kernel(const KParams &p, bool count, hipStream_t stream) {
-    // Variant choice: smallest LDS stack that holds the BVH depth; scene staged in LDS when the
-    // BVH + spheres fit the per-block budget (RTOW: ~26 KB), else read through L1/L2.
-    const bool lds = p.scene_in_lds != 0;
-    const bool wide = p.n_nodes > 65535u;
-    if (wide) {
-        if (p.stack_depth > 64) return hipErrorInvalidValue;
-        return launch_variant<64, false, uint32_t>(p, count, stream);
-    }
-    if (p.stack_depth <= 16) {
-        return lds ? launch_variant<16, true, uint16_t>(p, count, stream) : launch_variant<16, false, uint16_t>(p, count, stream);
-    }
-    if (p.stack_depth <= 32) {
-        return lds ? launch_variant<32, true, uint16_t>(p, count, stream) : launch_variant<32, false, uint16_t>(p, count, stream);
-    }
-    if (p.stack_depth <= 64) return launch_variant<64, false, uint16_t>(p, count, stream);
-    return hipErrorInvalidValue;
+    // Variant choice: BVH width, smallest LDS stack that holds the traversal, and the scene
+    // staged in LDS when the BVH + spheres fit the per-block budget (RTOW: ~20-26 KB).
+    return p.bvh_width == 4 ? launch_width<true>(p, count, stream) : launch_width<false>(p, count, stream);
 }
 
 hipError_t launch_render(const KParams &p, hipStream_t stream) { return launch_render_kernel(p, false, stream); }
