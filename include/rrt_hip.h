@@ -181,8 +181,17 @@ typedef struct RrtBvhInfo {
     uint32_t max_leaf_size;
     uint64_t node_bytes;
     uint64_t prim_bytes;
+    uint32_t width;          /* 2: 64-B binary nodes, 4: 128-B 4-wide nodes */
+    uint32_t max_leaf_param; /* leaf size the builder was asked for */
 } RrtBvhInfo;
 int32_t rrt_scene_bvh_info(const RrtScene *scene, RrtBvhInfo *out);
+
+/* Host-only: the BVH rrt_scene_create would build for these spheres (width / max_leaf 0 =
+ * the defaults), as the device node array (64-B BVH2 or 128-B BVH4 nodes, layout in
+ * DESIGN.md) and the leaf-order permutation of the spheres. Call with nodes_cap 0 to size
+ * (info->node_bytes). Lets a checker walk exactly the tree the kernel walks. */
+int32_t rrt_build_bvh(const RrtSphere *spheres, uint32_t n_spheres, uint32_t width, uint32_t max_leaf,
+                      void *nodes_out, size_t nodes_cap, uint32_t *prim_order_out, RrtBvhInfo *info);
 
 /* ---- host-side callers of the boundary ------------------------------------------------ */
 

@@ -36,6 +36,9 @@ def load() -> ctypes.CDLL:
     lib.oracle_render.restype = c_int
     lib.oracle_render.argtypes = [P, P, c_uint32, P, c_uint32, P, c_uint32, c_uint32, c_int, c_uint32, c_uint32,
                                   c_uint32, c_uint32, c_int, P, P, P]
+    lib.oracle_render_kbvh.restype = c_int
+    lib.oracle_render_kbvh.argtypes = [P, P, c_uint32, P, c_uint32, P, c_uint32, c_uint32, P, c_uint32, c_uint32, P,
+                                       c_uint32, c_uint32, c_uint32, c_uint32, c_int, P, P, P]
     lib.oracle_rtow_scene.restype = c_int
     lib.oracle_rtow_scene.argtypes = [c_uint64, c_int, P, P, P, P, P, c_uint32, P, P]
     lib.oracle_write_color.restype = None
@@ -94,6 +97,33 @@ def render(scene, mode=TWIN, rows=None, samples=None, threads=1):
                            ctypes.byref(rays), ctypes.byref(tests))
     if rc != 0:
         raise RuntimeError(f"oracle_render failed ({rc})")
+    return accum, rays.value, tests.value
+
+
+def render_kbvh(scene, nodes, order, width, rows=None, samples=None, threads=1):
+    """TWIN arithmetic, closest hits by walking the kernel's own BVH in the kernel's order
+    (nodes/order from rustraytrace_amd.render.build_bvh). Same return as render()."""
+    lib = load()
+    W, H = int(scene.camera["params_f"][0, 1]), int(scene.camera["params_f"][0, 2])
+    spp = max(int(scene.camera["params_f"][0, 3]), 1)
+    y0, y1 = rows if rows is not None else (0, H)
+    s0, s1 = samples if samples is not None else (0, spp)
+    accum = np.zeros((y1 - y0, W, 4), dtype=np.float64)
+    keep = [np.ascontiguousarray(t, dtype=np.uint8) for t in scene.textures]
+    tex = (_Tex * max(len(keep), 1))()
+    for i, t in enumerate(keep):
+        tex[i].rgb8 = t.ctypes.data_as(POINTER(c_uint8))
+        tex[i].height, tex[i].width = t.shape[0], t.shape[1]
+    nodes = np.ascontiguousarray(nodes, dtype=np.uint8)
+    order = np.ascontiguousarray(order, dtype=np.uint32)
+    n_nodes = nodes.size // (64 if width == 2 else 128)
+    rays, tests = c_uint64(0), c_uint64(0)
+    rc = lib.oracle_render_kbvh(_p(scene.camera), _p(scene.spheres), len(scene.spheres), _p(scene.materials),
+                                len(scene.materials), ctypes.cast(tex, c_void_p) if keep else None, len(keep),
+                                int(scene.flags), _p(nodes), n_nodes, int(width), _p(order), y0, y1, s0, s1,
+                                int(threads), _p(accum), ctypes.byref(rays), ctypes.byref(tests))
+    if rc != 0:
+        raise RuntimeError(f"oracle_render_kbvh failed ({rc})")
     return accum, rays.value, tests.value
 
 

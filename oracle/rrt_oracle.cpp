@@ -395,6 +395,113 @@ template <class T> struct World {
     }
 };
 
+// ---- KBVH mode: the kernel's own flattened BVH walked in the kernel's order ----------------
+// (rustraytrace_amd/csrc/rrt_kernel.hip trav_step / trav_step4; layouts in rrt_internal.h).
+// Only IEEE-exact operations (div, fma, min, max) decide the traversal, so the CPU reproduces
+// every pruning and ordering decision of the GPU: with it, whole frames are bit-comparable even
+// where the closest-hit winner depends on BVH topology (near-ties and grazing rays).
+struct KTree {
+    uint32_t width = 0;
+    const uint8_t *nodes = nullptr;
+    uint32_t n_nodes = 0;
+    const uint32_t *order = nullptr;  // leaf-order primitive -> original sphere index
+};
+
+struct KRay {
+    float ix, iy, iz, oix, oiy, oiz;
+};
+
+inline bool kbox(float lx, float hx, float ly, float hy, float lz, float hz, const KRay &r, float tmin, float tmax,
+                 float &tnear) {
+    const float x0 = std::fmaf(lx, r.ix, -r.oix), x1 = std::fmaf(hx, r.ix, -r.oix);
+    const float y0 = std::fmaf(ly, r.iy, -r.oiy), y1 = std::fmaf(hy, r.iy, -r.oiy);
+    const float z0 = std::fmaf(lz, r.iz, -r.oiz), z1 = std::fmaf(hz, r.iz, -r.oiz);
+    const float nr = std::fmaxf(std::fmaxf(std::fminf(x0, x1), std::fminf(y0, y1)), std::fmaxf(std::fminf(z0, z1), tmin));
+    const float fr = std::fminf(std::fminf(std::fmaxf(x0, x1), std::fmaxf(y0, y1)), std::fminf(std::fmaxf(z0, z1), tmax));
+    tnear = nr;
+    return nr < fr;
+}
+
+bool kbvh_hit(const World<float> &w, const KTree &kt, Vec3<float> o, Vec3<float> d, Hit<float> &rec, uint64_t *tests) {
+    KRay r;
+    r.ix = 1.0f / d[0];
+    r.iy = 1.0f / d[1];
+    r.iz = 1.0f / d[2];
+    r.oix = o[0] * r.ix;
+    r.oiy = o[1] * r.iy;
+    r.oiz = o[2] * r.iz;
+    const float kTmin = 0.001f;
+    float closest = std::numeric_limits<float>::infinity();
+    int32_t hit = -1;
+    auto leaf = [&](int32_t first, int32_t count) {
+        for (int32_t i = first; i < first + count; ++i) {
+            float t;
+            if (w.hit_sphere((int32_t)kt.order[i], o, d, Interval<float>{kTmin, closest}, t, tests)) {
+                closest = t;
+                hit = i;
+            }
+        }
+    };
+    int32_t stack[128];
+    int sp = 0;
+    int32_t node = 0;
+    for (;;) {
+        if (kt.width == 2) {
+            const float *f = reinterpret_cast<const float *>(kt.nodes + (size_t)node * 64);
+            const int32_t *l = reinterpret_cast<const int32_t *>(kt.nodes + (size_t)node * 64 + 48);
+            float tn0 = 0.0f, tn1 = 0.0f;
+            bool h0 = kbox(f[0], f[1], f[2], f[3], f[4], f[5], r, kTmin, closest, tn0);
+            bool h1 = kbox(f[6], f[7], f[8], f[9], f[10], f[11], r, kTmin, closest, tn1);
+            if (h0 && l[2] > 0) { leaf(l[0], l[2]); h0 = false; }
+            if (h1 && l[3] > 0) { leaf(l[1], l[3]); h1 = false; }
+            if (h0 && h1) {
+                const bool first1 = tn1 < tn0;
+                stack[sp++] = first1 ? l[0] : l[1];
+                node = first1 ? l[1] : l[0];
+                continue;
+            }
+            if (h0) { node = l[0]; continue; }
+            if (h1) { node = l[1]; continue; }
+        } else {
+            const float *f = reinterpret_cast<const float *>(kt.nodes + (size_t)node * 128);
+            const int32_t *child = reinterpret_cast<const int32_t *>(kt.nodes + (size_t)node * 128 + 96);
+            const int32_t *count = child + 4;
+            const float inf = std::numeric_limits<float>::infinity();
+            float key[4];
+            int32_t idx[4];
+            for (int c = 0; c < 4; ++c) {
+                float tn = 0.0f;
+                const bool h = kbox(f[c], f[4 + c], f[8 + c], f[12 + c], f[16 + c], f[20 + c], r, kTmin, closest, tn);
+                key[c] = h ? tn : inf;
+                idx[c] = child[c];
+            }
+            for (int c = 0; c < 4; ++c)
+                if (count[c] > 0) {
+                    if (key[c] < inf) leaf(child[c], count[c]);
+                    key[c] = inf;
+                }
+            for (int c = 0; c < 4; ++c) key[c] = key[c] < closest ? key[c] : inf;
+            auto cswap = [&](int i, int j) {
+                if (key[j] < key[i]) { std::swap(key[i], key[j]); std::swap(idx[i], idx[j]); }
+            };
+            cswap(0, 1);
+            cswap(2, 3);
+            cswap(0, 2);
+            cswap(1, 3);
+            cswap(1, 2);
+            if (key[3] < inf) stack[sp++] = idx[3];
+            if (key[2] < inf) stack[sp++] = idx[2];
+            if (key[1] < inf) stack[sp++] = idx[1];
+            if (key[0] < inf) { node = idx[0]; continue; }
+        }
+        if (sp == 0) break;
+        node = stack[--sp];
+    }
+    if (hit < 0) return false;
+    rec = Hit<float>{closest, (int32_t)kt.order[hit]};
+    return true;
+}
+
 template <class T> struct Cam {
     Vec3<T> center, p00, du, dv, disk_u, disk_v, background;
     T radius;
@@ -452,10 +559,20 @@ template <class T> struct Record {
 };
 
 template <class T>
-bool world_hit(const World<T> &w, Vec3<T> o, Vec3<T> d, Record<T> &rec, uint64_t *tests) {  // camera.rs:187
-    if (w.root.index < 0) return false;
+bool world_hit(const World<T> &w, Vec3<T> o, Vec3<T> d, Record<T> &rec, uint64_t *tests,
+               const KTree *kt = nullptr) {  // camera.rs:187
     Hit<T> h;
-    if (!w.hit(w.root, o, d, Interval<T>{L(0.001), std::numeric_limits<T>::infinity()}, h, tests)) return false;
+    if constexpr (std::is_same_v<T, float>) {
+        if (kt) {
+            if (!kbvh_hit(w, *kt, o, d, h, tests)) return false;
+        } else {
+            if (w.root.index < 0) return false;
+            if (!w.hit(w.root, o, d, Interval<T>{L(0.001), std::numeric_limits<T>::infinity()}, h, tests)) return false;
+        }
+    } else {
+        if (w.root.index < 0) return false;
+        if (!w.hit(w.root, o, d, Interval<T>{L(0.001), std::numeric_limits<T>::infinity()}, h, tests)) return false;
+    }
     const Sphere<T> &s = w.spheres[h.sphere];
     rec.p = o + h.t * d;                         // Ray::at
     rec.outward = (rec.p - s.center) / s.radius;  // sphere.rs:48
@@ -585,12 +702,13 @@ Vec3<T> ray_color_books(const World<T> &w, const Cam<T> &cam, PathRng &rng, Vec3
 
 // TWIN: the same path, throughput front-to-back (the HIP kernel's order, rrt_kernel.hip).
 template <class T>
-Vec3<T> ray_color_twin(const World<T> &w, const Cam<T> &cam, PathRng &rng, Vec3<T> o, Vec3<T> d, Tally &tl) {
+Vec3<T> ray_color_twin(const World<T> &w, const Cam<T> &cam, PathRng &rng, Vec3<T> o, Vec3<T> d, Tally &tl,
+                       const KTree *kt = nullptr) {
     Vec3<T> Tp = mk(T(1), T(1), T(1)), Lp = mk(T(0), T(0), T(0));
     for (uint32_t k = 0; k < cam.max_depth; ++k) {
         tl.rays++;
         Record<T> rec;
-        if (!world_hit(w, o, d, rec, &tl.tests)) return Lp + Tp * miss_color(cam, d);
+        if (!world_hit(w, o, d, rec, &tl.tests, kt)) return Lp + Tp * miss_color(cam, d);
         const Material<T> &m = w.mats[rec.mat];
         if (m.kind == RRT_MAT_DIFFUSE_LIGHT) return Lp + Tp * m.albedo;
         Vec3<T> att, dir;
@@ -627,7 +745,7 @@ void get_ray(const Cam<T> &cam, PathRng &rng, uint32_t i, uint32_t j, Vec3<T> &o
 template <class T>
 int render(const RrtCamera *c, const RrtSphere *s, uint32_t n, const RrtMaterial *m, uint32_t nm, const RrtTexture *tex,
            uint32_t ntex, uint32_t flags, int mode, uint32_t y0, uint32_t y1, uint32_t s0, uint32_t s1, int threads,
-           double *accum, uint64_t *rays_out, uint64_t *tests_out) {
+           double *accum, uint64_t *rays_out, uint64_t *tests_out, const KTree *kt = nullptr) {
     World<T> w;
     Cam<T> cam;
     load_world(w, cam, c, s, n, m, nm, tex, ntex, flags);
@@ -649,7 +767,7 @@ int render(const RrtCamera *c, const RrtSphere *s, uint32_t n, const RrtMaterial
                     Vec3<T> o, d;
                     get_ray(cam, rng, i, j, o, d);
                     sum = sum + (mode == 1 ? ray_color_books(w, cam, rng, o, d, (int)cam.max_depth, tl)
-                                           : ray_color_twin(w, cam, rng, o, d, tl));
+                                           : ray_color_twin(w, cam, rng, o, d, tl, kt));
                 }
                 double *px = accum + ((size_t)(j - y0) * cam.width + i) * 4;
                 px[0] = (double)sum.x();
@@ -712,6 +830,21 @@ int oracle_render(const RrtCamera *cam, const RrtSphere *s, uint32_t n, const Rr
     if (!cam || !accum) return -1;
     if (mode == 1) return render<double>(cam, s, n, m, nm, tex, ntex, flags, 1, y0, y1, s0, s1, threads, accum, rays, sphere_tests);
     return render<float>(cam, s, n, m, nm, tex, ntex, flags, 0, y0, y1, s0, s1, threads, accum, rays, sphere_tests);
+}
+
+// mode 2 = KBVH: TWIN arithmetic, but closest hits found by walking the kernel's BVH
+// (rrt_build_bvh output: `nodes` of n_nodes x 64 B (width 2) or 128 B (width 4), `order`).
+int oracle_render_kbvh(const RrtCamera *cam, const RrtSphere *s, uint32_t n, const RrtMaterial *m, uint32_t nm,
+                       const RrtTexture *tex, uint32_t ntex, uint32_t flags, const void *nodes, uint32_t n_nodes,
+                       uint32_t width, const uint32_t *order, uint32_t y0, uint32_t y1, uint32_t s0, uint32_t s1,
+                       int threads, double *accum, uint64_t *rays, uint64_t *sphere_tests) {
+    if (!cam || !accum || !nodes || (width != 2 && width != 4)) return -1;
+    KTree kt;
+    kt.width = width;
+    kt.nodes = static_cast<const uint8_t *>(nodes);
+    kt.n_nodes = n_nodes;
+    kt.order = order;
+    return render<float>(cam, s, n, m, nm, tex, ntex, flags, 0, y0, y1, s0, s1, threads, accum, rays, sphere_tests, &kt);
 }
 
 // gpu::build_in_one_weekend_scene's sphere/material list (no overrides, camera seed out).

@@ -52,6 +52,7 @@ EXPORTED_SYMBOLS = (
     "rrt_scene_reset_counters",
     "rrt_scene_count_work",
     "rrt_scene_bvh_info",
+    "rrt_build_bvh",
     "rrt_build_in_one_weekend_scene",
     "rrt_make_camera",
     "rrt_apply_overrides",
@@ -113,6 +114,8 @@ class RrtBvhInfo(ctypes.Structure):
         ("max_leaf_size", c_uint32),
         ("node_bytes", c_uint64),
         ("prim_bytes", c_uint64),
+        ("width", c_uint32),
+        ("max_leaf_param", c_uint32),
     ]
 
     def as_dict(self):
@@ -162,6 +165,7 @@ def load() -> ctypes.CDLL:
         "rrt_scene_reset_counters": (c_int32, [P]),
         "rrt_scene_count_work": (c_int32, [P, P, P]),
         "rrt_scene_bvh_info": (c_int32, [P, P]),
+        "rrt_build_bvh": (c_int32, [P, c_uint32, c_uint32, c_uint32, P, c_size_t, P, P]),
         "rrt_build_in_one_weekend_scene": (c_int32, [P, c_uint64, c_int32, P, P, P, c_uint32, P]),
         "rrt_make_camera": (
             c_int32,

@@ -432,6 +432,45 @@ FlatBvh flatten4(const Builder &bd, int32_t root) {
     return f;
 }
 
+
+// Default BVH shape of scene creation (env knobs are for experiments).
+void bvh_defaults(uint32_t &width, uint32_t &max_leaf) {
+    max_leaf = 3;
+    if (const char *e = std::getenv("RRT_MAX_LEAF")) max_leaf = (uint32_t)std::min(15, std::max(1, std::atoi(e)));
+    width = 2;
+    if (const char *e = std::getenv("RRT_BVH_WIDTH")) width = std::atoi(e) == 4 ? 4 : 2;
+}
+
+// Sphere boxes (sphere.rs:16-21, aabb.rs:29-34: r = max(radius, 0), padded), SAH build,
+// flatten. order[i] = original index of the i-th primitive in leaf order.
+FlatBvh build_bvh(const RrtSphere *spheres, uint32_t n_spheres, uint32_t width, uint32_t max_leaf,
+                  std::vector<uint32_t> &order) {
+    std::vector<Aabb> boxes(n_spheres);
+    for (uint32_t i = 0; i < n_spheres; ++i) {
+        const double r = std::max((double)spheres[i].center_radius[3], 0.0);
+        Aabb b;
+        for (int a = 0; a < 3; ++a) {
+            const double c = spheres[i].center_radius[a];
+            b.ax[a] = Interval{c - r, c + r};
+        }
+        boxes[i] = pad(b);
+    }
+    Builder bld(boxes, max_leaf);
+    FlatBvh fb;
+    if (n_spheres == 0) {  // root with never-hit children
+        Builder::BNode empty;
+        empty.box = never_hit_box();
+        empty.leaf = true;
+        bld.bin.push_back(empty);
+        fb = width == 4 ? flatten4(bld, 0) : flatten2(bld, 0);
+    } else {
+        const int32_t root = bld.build(0, n_spheres);
+        fb = width == 4 ? flatten4(bld, root) : flatten2(bld, root);
+    }
+    order = bld.objs;
+    return fb;
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------------------------
@@ -546,40 +585,18 @@ int32_t rrt_scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint32_
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(RRT_E_NODEV, "no HIP device available");
     if (device < 0 || device >= ndev) return fail(RRT_E_INVALID, "device index out of range");
 
-    // ---- BVH over the sphere bounding boxes (sphere.rs:16-21: r = max(radius, 0)) ----
-    std::vector<Aabb> boxes(n_spheres);
-    for (uint32_t i = 0; i < n_spheres; ++i) {
-        const double r = std::max((double)spheres[i].center_radius[3], 0.0);
-        Aabb b;
-        for (int a = 0; a < 3; ++a) {
-            const double c = spheres[i].center_radius[a];
-            b.ax[a] = Interval{c - r, c + r};
-        }
-        boxes[i] = pad(b);
-    }
-    uint32_t max_leaf = 3;
-    if (const char *e = std::getenv("RRT_MAX_LEAF")) max_leaf = (uint32_t)std::min(15, std::max(1, std::atoi(e)));
-    uint32_t width = 2;
-    if (const char *e = std::getenv("RRT_BVH_WIDTH")) width = std::atoi(e) == 4 ? 4 : 2;
-    Builder bld(boxes, max_leaf);
-    FlatBvh fb;
-    if (n_spheres == 0) {  // root with two never-hit children
-        Builder::BNode empty;
-        empty.box = never_hit_box();
-        empty.leaf = true;
-        bld.bin.push_back(empty);
-        fb = width == 4 ? flatten4(bld, 0) : flatten2(bld, 0);
-    } else {
-        const int32_t root = bld.build(0, n_spheres);
-        fb = width == 4 ? flatten4(bld, root) : flatten2(bld, root);
-    }
+    // ---- BVH over the sphere bounding boxes ----
+    uint32_t width, max_leaf;
+    bvh_defaults(width, max_leaf);
+    std::vector<uint32_t> order;
+    const FlatBvh fb = build_bvh(spheres, n_spheres, width, max_leaf, order);
     if (fb.stack_need > (uint32_t)rrt::kMaxStackDepth)
         return fail(RRT_E_INVALID, "BVH depth " + std::to_string(fb.max_depth) + " exceeds the LDS stack");
 
     std::vector<float4> prim_cr(n_spheres);
     std::vector<uint32_t> prim_mat(n_spheres);
     for (uint32_t i = 0; i < n_spheres; ++i) {
-        const RrtSphere &sp = spheres[bld.objs[i]];
+        const RrtSphere &sp = spheres[order[i]];
         prim_cr[i] = make_float4(sp.center_radius[0], sp.center_radius[1], sp.center_radius[2],
                                  std::max(sp.center_radius[3], 0.0f));
         prim_mat[i] = sp.material_index;
@@ -679,8 +696,39 @@ int32_t rrt_scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint32_
     bi.max_depth = fb.max_depth;
     bi.max_leaf_size = fb.max_leaf;
     bi.node_bytes = fb.bytes.size();
+    bi.width = fb.width;
+    bi.max_leaf_param = max_leaf;
     bi.prim_bytes = (uint64_t)n_spheres * (sizeof(float4) + sizeof(uint32_t));
     *out = s;
+    return RRT_OK;
+}
+
+int32_t rrt_build_bvh(const RrtSphere *spheres, uint32_t n_spheres, uint32_t width, uint32_t max_leaf,
+                      void *nodes_out, size_t nodes_cap, uint32_t *prim_order_out, RrtBvhInfo *info) {
+    if (n_spheres && !spheres) return fail(RRT_E_INVALID, "null spheres");
+    uint32_t dw, dl;
+    bvh_defaults(dw, dl);
+    if (width == 0) width = dw;
+    if (max_leaf == 0) max_leaf = dl;
+    if ((width != 2 && width != 4) || max_leaf > 15) return fail(RRT_E_INVALID, "width must be 2 or 4, max_leaf <= 15");
+    std::vector<uint32_t> order;
+    const FlatBvh fb = build_bvh(spheres, n_spheres, width, max_leaf, order);
+    if (info) {
+        *info = RrtBvhInfo{};
+        info->n_nodes = fb.n_nodes;
+        info->n_leaves = fb.n_leaves;
+        info->max_depth = fb.max_depth;
+        info->max_leaf_size = fb.max_leaf;
+        info->node_bytes = fb.bytes.size();
+        info->prim_bytes = (uint64_t)n_spheres * (sizeof(float4) + sizeof(uint32_t));
+        info->width = fb.width;
+        info->max_leaf_param = max_leaf;
+    }
+    if (nodes_cap == 0) return RRT_OK;
+    if (!nodes_out || nodes_cap < fb.bytes.size() || (n_spheres && !prim_order_out))
+        return fail(RRT_E_INVALID, "nodes buffer too small (need " + std::to_string(fb.bytes.size()) + " bytes)");
+    std::memcpy(nodes_out, fb.bytes.data(), fb.bytes.size());
+    if (n_spheres) std::memcpy(prim_order_out, order.data(), order.size() * sizeof(uint32_t));
     return RRT_OK;
 }
 

@@ -102,6 +102,20 @@ def tile_row_indices(height: int, tile) -> np.ndarray:
     return out
 
 
+def build_bvh(scene: SceneData, width: int = 0, max_leaf: int = 0):
+    """The BVH rrt_scene_create builds for `scene` (host only): (node bytes uint8, leaf-order
+    permutation uint32, info dict). width/max_leaf 0 = the library defaults."""
+    lib = _lib.load()
+    info = _lib.RrtBvhInfo()
+    n = len(scene.spheres)
+    _lib.check(lib.rrt_build_bvh(_lib.ptr(scene.spheres), n, width, max_leaf, None, 0, None, ctypes.byref(info)))
+    nodes = np.zeros(info.node_bytes, dtype=np.uint8)
+    order = np.zeros(max(n, 1), dtype=np.uint32)
+    _lib.check(lib.rrt_build_bvh(_lib.ptr(scene.spheres), n, width, max_leaf, _lib.ptr(nodes), nodes.size,
+                                 _lib.ptr(order), ctypes.byref(info)))
+    return nodes, order[:n], info.as_dict()
+
+
 def make_tile(band_rows=16, rank=0, n_ranks=1, sample_begin=0, sample_end=0) -> _lib.RrtTile:
     t = _lib.RrtTile()
     t.band_rows, t.rank, t.n_ranks, t.sample_begin, t.sample_end = band_rows, rank, n_ranks, sample_begin, sample_end

@@ -1,6 +1,7 @@
-"""GPU tests at BASELINE.json's full sizes (C2..C5). The oracle cannot render whole frames in
-seconds, so full-size parity is checked through size-independent properties plus bit-exact
-oracle rows at full spp:
+"""GPU tests at BASELINE.json's full sizes (C2..C5). Full-size parity is checked through
+size-independent properties, bit-exact oracle rows at full spp, and whole frames against the
+oracle's KBVH mode (the kernel's own BVH walked in the kernel's order on the CPU, so even
+topology-dependent near-ties and grazing hits must agree):
   * every accum value finite and non-negative, w == spp for every pixel
   * determinism: a second launch is bit-identical (no atomics on the image)
   * selected full rows (sky and ground) bit-identical to the f32 oracle at full spp
@@ -16,6 +17,9 @@ import pytest
 
 import rustraytrace_amd as rrt
 from oracle import oracle
+from rustraytrace_amd.render import build_bvh
+
+THREADS = min(16, os.cpu_count() or 1)
 
 pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
@@ -49,9 +53,27 @@ def test_full_frame_properties_and_rows(cfg, rows):
     assert np.array_equal(a, b), "render is not deterministic"
     assert ctr["paths"] == scene.width * scene.height * scene.spp
     assert ctr["rays"] >= ctr["paths"]
+    nodes, order, info = build_bvh(scene)
     for y in rows:
-        ref, _, _ = oracle.render(scene, oracle.TWIN, rows=(y, y + 1), threads=1)
+        ref, _, _ = oracle.render_kbvh(scene, nodes, order, info["width"], rows=(y, y + 1), threads=THREADS)
         assert np.array_equal(a[y:y + 1].astype(np.float64), ref), f"{cfg} row {y} differs from the oracle"
+    ds.close()
+
+
+@pytest.mark.parametrize("spp", [8, 512])
+def test_c2_whole_frame_bit_exact(spp):
+    # Every pixel of the 1920x1080 C2 frame vs the CPU oracle (512 spp: the full BASELINE
+    # workload, ~2.7e9 rays on the CPU; tens of seconds on the GPU box's 16 host threads).
+    scene = rrt.config_scene("C2", samples_per_pixel=spp)
+    ds, tile, a, b, ctr = _render_full(scene)
+    nodes, order, info = build_bvh(scene)
+    ref, rays, _ = oracle.render_kbvh(scene, nodes, order, info["width"], threads=THREADS)
+    diff = np.abs(a.astype(np.float64) - ref)
+    assert (diff[..., :3] / spp).max() <= 1e-4  # north-star tolerance
+    assert diff.max() == 0.0, f"{int((diff > 0).any(-1).sum())} pixels differ"
+    assert ctr["rays"] == rays
+    ppm_gpu = rrt.format_ppm_from_accum(scene.width, scene.height, a, spp)
+    assert ppm_gpu == rrt.format_ppm_from_accum(scene.width, scene.height, ref.astype(np.float32), spp)
     ds.close()
 
 
@@ -81,7 +103,8 @@ def test_c3_tiles_match_oracle_rows():
         assert np.all(a[..., 3] == 2048) and np.isfinite(a).all()
         assert np.array_equal(a, b)
         y = int(idx[0])
-        ref, _, _ = oracle.render(scene, oracle.TWIN, rows=(y, y + 1), threads=1)
+        nodes, order, info = build_bvh(scene)
+        ref, _, _ = oracle.render_kbvh(scene, nodes, order, info["width"], rows=(y, y + 1), threads=THREADS)
         assert np.array_equal(a[0:1].astype(np.float64), ref)
         ds.close()
 

@@ -10,6 +10,7 @@ import pytest
 
 import rustraytrace_amd as rrt
 from oracle import oracle
+from rustraytrace_amd.render import build_bvh
 
 pytestmark = pytest.mark.gpu
 
@@ -62,8 +63,12 @@ SMALL = [
 def test_one_shot_matches_oracle(cfg, kw):
     scene = rrt.config_scene(cfg, **kw)
     gpu = rrt.render(scene)
-    ref, rays, _ = oracle.render(scene, oracle.TWIN)
+    ref, rays, _ = oracle.render(scene, oracle.TWIN)  # independent books-structured tree
     assert_bit_exact(gpu, ref, scene.spp)
+    nodes, order, info = build_bvh(scene)
+    kref, krays, _ = oracle.render_kbvh(scene, nodes, order, info["width"])  # the kernel's own tree
+    assert_bit_exact(gpu, kref, scene.spp)
+    assert krays == rays
     assert np.all(gpu[..., 3] == scene.spp)
     a = rrt.format_ppm_from_accum(scene.width, scene.height, gpu, scene.spp)
     b = rrt.format_ppm_from_accum(scene.width, scene.height, ref.astype(np.float32), scene.spp)

@@ -1,0 +1,54 @@
+"""Turn two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE; separate runs, as MI355X_MICROARCH.md
+§HBM prescribes) over one full-size render launch into profiles/traffic_<config>.json, which
+bench.py reports as roofline.traffic (HBM bytes per launch).
+
+FETCH_SIZE / WRITE_SIZE are in KiB and count the L2's memory-side requests. gfx950 caveat:
+FETCH_SIZE reads half the bytes of a wide 16-B/lane streaming read; this kernel's reads are
+L2-resident scene gathers and its only streaming traffic is the accum write, so the raw
+values are reported alongside the corrected upper bound (2 x FETCH_SIZE + WRITE_SIZE).
+    python tools/pmc_traffic.py <fetch_dir> <write_dir> <config> <width> <spp> <out_json>
+"""
+import csv
+import glob
+import hashlib
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def counter(d, name):
+    vals = []
+    for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(path)):
+            if "rrt_render" in r["Kernel_Name"] and r["Counter_Name"] == name:
+                vals.append(float(r["Counter_Value"]))
+    if not vals:
+        raise SystemExit(f"no {name} rows in {d}")
+    return sum(vals) / len(vals), len(vals)
+
+
+def main(fetch_dir, write_dir, config, width, spp, out):
+    fetch_kib, n1 = counter(fetch_dir, "FETCH_SIZE")
+    write_kib, n2 = counter(write_dir, "WRITE_SIZE")
+    so = os.path.join(ROOT, "rustraytrace_amd", "librrt_hip.so")
+    rec = {
+        "config": config,
+        "width": int(width),
+        "spp": int(spp),
+        "dispatches": [n1, n2],
+        "fetch_size_kib": fetch_kib,
+        "write_size_kib": write_kib,
+        "hbm_bytes_per_launch": int((fetch_kib + write_kib) * 1024),
+        "hbm_bytes_per_launch_fetch_corrected": int((2 * fetch_kib + write_kib) * 1024),
+        "lib_sha256": hashlib.sha256(open(so, "rb").read()).hexdigest(),
+        "note": "separate --pmc passes FETCH_SIZE / WRITE_SIZE on tools/prof_render.py (1 launch)",
+    }
+    with open(out, "w") as f:
+        json.dump(rec, f, indent=1)
+    print(json.dumps(rec))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])
