@@ -411,17 +411,30 @@ struct KRay {
     float ix, iy, iz, oix, oiy, oiz;
 };
 
-inline bool kbox(float lx, float hx, float ly, float hy, float lz, float hz, const KRay &r, float tmin, float tmax,
-                 float &tnear) {
-    const float x0 = std::fmaf(lx, r.ix, -r.oix), x1 = std::fmaf(hx, r.ix, -r.oix);
-    const float y0 = std::fmaf(ly, r.iy, -r.oiy), y1 = std::fmaf(hy, r.iy, -r.oiy);
-    const float z0 = std::fmaf(lz, r.iz, -r.oiz), z1 = std::fmaf(hz, r.iz, -r.oiz);
-    const float nr = std::fmaxf(std::fmaxf(std::fminf(x0, x1), std::fminf(y0, y1)), std::fmaxf(std::fminf(z0, z1), tmin));
-    const float fr = std::fminf(std::fminf(std::fmaxf(x0, x1), std::fmaxf(y0, y1)), std::fminf(std::fmaxf(z0, z1), tmax));
-    tnear = nr;
-    return nr < fr;
-}
+// IEEE-754 minNum/maxNum (the GPU's v_min_f32 / v_max_f32): a NaN operand yields the other.
+// Inline (libm fminf/fmaxf are calls on x86); zero signs may differ but every use compares
+// against tmin = 0.001 or orders strictly, so they cannot change a decision.
+static inline float min_num(float a, float b) { return (b != b) ? a : ((a != a) ? b : (a < b ? a : b)); }
+static inline float max_num(float a, float b) { return (b != b) ? a : ((a != a) ? b : (a > b ? a : b)); }
 
+// Kernel slab test (rrt_kernel.hip box_hit). A macro so the FMAs are emitted inside each
+// target clone of kbvh_hit (as vfmadd where the host has FMA3, else the libm call).
+#define KBOX(lx, hx, ly, hy, lz, hz, r, tmin, tmax, tnear, out)                                                  \
+    do {                                                                                                           \
+        const float x0_ = __builtin_fmaf(lx, r.ix, -r.oix), x1_ = __builtin_fmaf(hx, r.ix, -r.oix);              \
+        const float y0_ = __builtin_fmaf(ly, r.iy, -r.oiy), y1_ = __builtin_fmaf(hy, r.iy, -r.oiy);              \
+        const float z0_ = __builtin_fmaf(lz, r.iz, -r.oiz), z1_ = __builtin_fmaf(hz, r.iz, -r.oiz);              \
+        const float nr_ = max_num(max_num(min_num(x0_, x1_), min_num(y0_, y1_)),                                 \
+                                  max_num(min_num(z0_, z1_), tmin));                                               \
+        const float fr_ = min_num(min_num(max_num(x0_, x1_), max_num(y0_, y1_)),                                 \
+                                  min_num(max_num(z0_, z1_), tmax));                                               \
+        tnear = nr_;                                                                                               \
+        out = nr_ < fr_;                                                                                           \
+    } while (0)
+
+// std::fmaf is a slow libm call without -mfma: clone the traversal for FMA-capable hosts
+// (results are identical either way: fmaf is correctly rounded in both).
+__attribute__((target_clones("fma", "default")))
 bool kbvh_hit(const World<float> &w, const KTree &kt, Vec3<float> o, Vec3<float> d, Hit<float> &rec, uint64_t *tests) {
     KRay r;
     r.ix = 1.0f / d[0];
@@ -450,8 +463,9 @@ bool kbvh_hit(const World<float> &w, const KTree &kt, Vec3<float> o, Vec3<float>
             const float *f = reinterpret_cast<const float *>(kt.nodes + (size_t)node * 64);
             const int32_t *l = reinterpret_cast<const int32_t *>(kt.nodes + (size_t)node * 64 + 48);
             float tn0 = 0.0f, tn1 = 0.0f;
-            bool h0 = kbox(f[0], f[1], f[2], f[3], f[4], f[5], r, kTmin, closest, tn0);
-            bool h1 = kbox(f[6], f[7], f[8], f[9], f[10], f[11], r, kTmin, closest, tn1);
+            bool h0, h1;
+            KBOX(f[0], f[1], f[2], f[3], f[4], f[5], r, kTmin, closest, tn0, h0);
+            KBOX(f[6], f[7], f[8], f[9], f[10], f[11], r, kTmin, closest, tn1, h1);
             if (h0 && l[2] > 0) { leaf(l[0], l[2]); h0 = false; }
             if (h1 && l[3] > 0) { leaf(l[1], l[3]); h1 = false; }
             if (h0 && h1) {
@@ -471,7 +485,8 @@ bool kbvh_hit(const World<float> &w, const KTree &kt, Vec3<float> o, Vec3<float>
             int32_t idx[4];
             for (int c = 0; c < 4; ++c) {
                 float tn = 0.0f;
-                const bool h = kbox(f[c], f[4 + c], f[8 + c], f[12 + c], f[16 + c], f[20 + c], r, kTmin, closest, tn);
+                bool h;
+                KBOX(f[c], f[4 + c], f[8 + c], f[12 + c], f[16 + c], f[20 + c], r, kTmin, closest, tn, h);
                 key[c] = h ? tn : inf;
                 idx[c] = child[c];
             }
