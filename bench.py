@@ -150,13 +150,21 @@ def main():
         flops = FLOP_PER_SPHERE_TEST * work["sphere_tests"] + FLOP_PER_BOX_TEST * work["box_tests"]
         achieved = flops / avg_kernel_s / 1e12
         alg_bytes = BYTES_PER_SPHERE_TEST * work["sphere_tests"] + BYTES_PER_NODE_VISIT * work["node_visits"]
-        traffic = None
+        traffic, traffic_src = None, None
         if os.path.exists(args.traffic_json):
             try:
                 with open(args.traffic_json) as f:
                     tj = json.load(f)
                 if tj.get("config") == args.config and tj.get("width") == W and tj.get("spp") == S:
                     traffic = tj.get("hbm_bytes_per_launch")
+                    import hashlib
+
+                    with open(rrt._lib.LIB_PATH, "rb") as f:
+                        cur = hashlib.sha256(f.read()).hexdigest()
+                    same = cur == tj.get("lib_sha256")
+                    traffic_src = (f"{os.path.relpath(args.traffic_json, ROOT)}: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
+                                   f"passes, {'this' if same else 'an earlier'} librrt_hip.so build "
+                                   f"({tj.get('lib_sha256', '')[:12]})")
             except (OSError, ValueError):
                 traffic = None
         rays_per_frame = work["rays"]
@@ -195,6 +203,7 @@ def main():
                 "unit": "TFLOP/s",
                 "frac": round(achieved / PEAK_F32_VALU_TFLOPS, 4),
                 "traffic": traffic,
+                "traffic_source": traffic_src,
                 "algorithmic_flop_per_launch": flops,
                 "algorithmic_bytes_per_launch": alg_bytes,
                 "effective_fetch_GBps": round(alg_bytes / avg_kernel_s / 1e9, 1),
