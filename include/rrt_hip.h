@@ -124,6 +124,11 @@ int32_t rrt_hip_render(const RrtCamera *cam,
 const char *rrt_hip_last_error(void);
 uint32_t rrt_hip_abi_version(void);
 
+/* Summation order of the accum: a pixel's RGB = sum over consecutive chunks of K samples
+ * (K = rrt_accum_chunk(), counted from the tile's sample_begin) of each chunk's in-order
+ * sample sum, chunks added in order: ((c0 + c1) + c2) + ... Needed to reproduce it bit for bit. */
+uint32_t rrt_accum_chunk(void);
+
 /* ---- device-resident API (bench / multi-rank hosts) --------------------------------- */
 typedef struct RrtScene RrtScene;
 

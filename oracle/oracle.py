@@ -15,6 +15,9 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "build", "librrt_oracle.so")
 TWIN, BOOKS = 0, 1
+# Accum summation chunk of the HIP backend (include/rrt_hip.h rrt_accum_chunk): samples are
+# summed in order within chunks of this many, chunk sums added in order.
+DEFAULT_CHUNK = 64
 
 _LIB = None
 
@@ -35,10 +38,10 @@ def load() -> ctypes.CDLL:
     P = c_void_p
     lib.oracle_render.restype = c_int
     lib.oracle_render.argtypes = [P, P, c_uint32, P, c_uint32, P, c_uint32, c_uint32, c_int, c_uint32, c_uint32,
-                                  c_uint32, c_uint32, c_int, P, P, P]
+                                  c_uint32, c_uint32, c_int, P, P, P, c_uint32]
     lib.oracle_render_kbvh.restype = c_int
     lib.oracle_render_kbvh.argtypes = [P, P, c_uint32, P, c_uint32, P, c_uint32, c_uint32, P, c_uint32, c_uint32, P,
-                                       c_uint32, c_uint32, c_uint32, c_uint32, c_int, P, P, P]
+                                       c_uint32, c_uint32, c_uint32, c_uint32, c_int, P, P, P, c_uint32]
     lib.oracle_rtow_scene.restype = c_int
     lib.oracle_rtow_scene.argtypes = [c_uint64, c_int, P, P, P, P, P, c_uint32, P, P]
     lib.oracle_write_color.restype = None
@@ -74,7 +77,7 @@ class _Tex(ctypes.Structure):
     _fields_ = [("rgb8", POINTER(c_uint8)), ("width", ctypes.c_int32), ("height", ctypes.c_int32)]
 
 
-def render(scene, mode=TWIN, rows=None, samples=None, threads=1):
+def render(scene, mode=TWIN, rows=None, samples=None, threads=1, chunk=DEFAULT_CHUNK):
     """Render `scene` (rustraytrace_amd.SceneData-like: camera/spheres/materials/textures/flags).
 
     rows = (y0, y1) image rows, samples = (s0, s1) sample range. Returns (accum, rays, sphere_tests)
@@ -94,13 +97,13 @@ def render(scene, mode=TWIN, rows=None, samples=None, threads=1):
     rc = lib.oracle_render(_p(scene.camera), _p(scene.spheres), len(scene.spheres), _p(scene.materials),
                            len(scene.materials), ctypes.cast(tex, c_void_p) if keep else None, len(keep),
                            int(scene.flags), int(mode), y0, y1, s0, s1, int(threads), _p(accum),
-                           ctypes.byref(rays), ctypes.byref(tests))
+                           ctypes.byref(rays), ctypes.byref(tests), int(chunk))
     if rc != 0:
         raise RuntimeError(f"oracle_render failed ({rc})")
     return accum, rays.value, tests.value
 
 
-def render_kbvh(scene, nodes, order, width, rows=None, samples=None, threads=1):
+def render_kbvh(scene, nodes, order, width, rows=None, samples=None, threads=1, chunk=DEFAULT_CHUNK):
     """TWIN arithmetic, closest hits by walking the kernel's own BVH in the kernel's order
     (nodes/order from rustraytrace_amd.render.build_bvh). Same return as render()."""
     lib = load()
@@ -121,7 +124,7 @@ def render_kbvh(scene, nodes, order, width, rows=None, samples=None, threads=1):
     rc = lib.oracle_render_kbvh(_p(scene.camera), _p(scene.spheres), len(scene.spheres), _p(scene.materials),
                                 len(scene.materials), ctypes.cast(tex, c_void_p) if keep else None, len(keep),
                                 int(scene.flags), _p(nodes), n_nodes, int(width), _p(order), y0, y1, s0, s1,
-                                int(threads), _p(accum), ctypes.byref(rays), ctypes.byref(tests))
+                                int(threads), _p(accum), ctypes.byref(rays), ctypes.byref(tests), int(chunk))
     if rc != 0:
         raise RuntimeError(f"oracle_render_kbvh failed ({rc})")
     return accum, rays.value, tests.value

@@ -760,7 +760,7 @@ void get_ray(const Cam<T> &cam, PathRng &rng, uint32_t i, uint32_t j, Vec3<T> &o
 template <class T>
 int render(const RrtCamera *c, const RrtSphere *s, uint32_t n, const RrtMaterial *m, uint32_t nm, const RrtTexture *tex,
            uint32_t ntex, uint32_t flags, int mode, uint32_t y0, uint32_t y1, uint32_t s0, uint32_t s1, int threads,
-           double *accum, uint64_t *rays_out, uint64_t *tests_out, const KTree *kt = nullptr) {
+           double *accum, uint64_t *rays_out, uint64_t *tests_out, uint32_t chunk, const KTree *kt = nullptr) {
     World<T> w;
     Cam<T> cam;
     load_world(w, cam, c, s, n, m, nm, tex, ntex, flags);
@@ -776,19 +776,28 @@ int render(const RrtCamera *c, const RrtSphere *s, uint32_t n, const RrtMaterial
             for (uint32_t i = 0; i < cam.width; ++i) {
                 const uint32_t pixel = j * cam.width + i;
                 const uint64_t key = splitmix64(((uint64_t)cam.seed << 32) ^ (uint64_t)pixel);
+                const uint64_t rays_before = tl.rays;
+                // accum order of the kernel (rrt_accum_chunk): in-order sums over chunks of
+                // `chunk` samples from s0, chunk sums added in order
                 Vec3<T> sum = mk(T(0), T(0), T(0));
-                for (uint32_t sidx = s0; sidx < s1; ++sidx) {
-                    PathRng rng{splitmix64(key + sidx)};
-                    Vec3<T> o, d;
-                    get_ray(cam, rng, i, j, o, d);
-                    sum = sum + (mode == 1 ? ray_color_books(w, cam, rng, o, d, (int)cam.max_depth, tl)
-                                           : ray_color_twin(w, cam, rng, o, d, tl, kt));
+                const uint32_t step = chunk ? chunk : (s1 - s0 ? s1 - s0 : 1);
+                for (uint32_t c0 = s0; c0 < s1; c0 += step) {
+                    Vec3<T> csum = mk(T(0), T(0), T(0));
+                    for (uint32_t sidx = c0; sidx < std::min(s1, c0 + step); ++sidx) {
+                        PathRng rng{splitmix64(key + sidx)};
+                        Vec3<T> o, d;
+                        get_ray(cam, rng, i, j, o, d);
+                        csum = csum + ((mode & 0xff) == 1 ? ray_color_books(w, cam, rng, o, d, (int)cam.max_depth, tl)
+                                                          : ray_color_twin(w, cam, rng, o, d, tl, kt));
+                    }
+                    sum = (c0 == s0) ? csum : sum + csum;
                 }
                 double *px = accum + ((size_t)(j - y0) * cam.width + i) * 4;
                 px[0] = (double)sum.x();
                 px[1] = (double)sum.y();
                 px[2] = (double)sum.z();
-                px[3] = (double)(s1 - s0);
+                // diagnostic mode bit 0x100: w = closest-hit queries of this pixel instead of the count
+                px[3] = (mode & 0x100) ? (double)(tl.rays - rays_before) : (double)(s1 - s0);
             }
         }
         rays += tl.rays;
@@ -838,13 +847,17 @@ struct Xoshiro256pp {
 extern "C" {
 
 // mode 0 = TWIN (f32, kernel order), 1 = BOOKS (f64, recursive). Renders rows [y0,y1),
+// chunk = the accum summation chunk (rrt_accum_chunk; 0 = one chunk),
 // samples [s0,s1) into accum[(y1-y0)*W*4] (double; TWIN values are exact f32 sums).
 int oracle_render(const RrtCamera *cam, const RrtSphere *s, uint32_t n, const RrtMaterial *m, uint32_t nm,
                   const RrtTexture *tex, uint32_t ntex, uint32_t flags, int mode, uint32_t y0, uint32_t y1,
-                  uint32_t s0, uint32_t s1, int threads, double *accum, uint64_t *rays, uint64_t *sphere_tests) {
+                  uint32_t s0, uint32_t s1, int threads, double *accum, uint64_t *rays, uint64_t *sphere_tests,
+                  uint32_t chunk) {
     if (!cam || !accum) return -1;
-    if (mode == 1) return render<double>(cam, s, n, m, nm, tex, ntex, flags, 1, y0, y1, s0, s1, threads, accum, rays, sphere_tests);
-    return render<float>(cam, s, n, m, nm, tex, ntex, flags, 0, y0, y1, s0, s1, threads, accum, rays, sphere_tests);
+    if ((mode & 0xff) == 1)
+        return render<double>(cam, s, n, m, nm, tex, ntex, flags, mode, y0, y1, s0, s1, threads, accum, rays, sphere_tests, chunk);
+    return render<float>(cam, s, n, m, nm, tex, ntex, flags, mode & ~0xff, y0, y1, s0, s1, threads, accum, rays,
+                         sphere_tests, chunk);
 }
 
 // mode 2 = KBVH: TWIN arithmetic, but closest hits found by walking the kernel's BVH
@@ -852,14 +865,15 @@ int oracle_render(const RrtCamera *cam, const RrtSphere *s, uint32_t n, const Rr
 int oracle_render_kbvh(const RrtCamera *cam, const RrtSphere *s, uint32_t n, const RrtMaterial *m, uint32_t nm,
                        const RrtTexture *tex, uint32_t ntex, uint32_t flags, const void *nodes, uint32_t n_nodes,
                        uint32_t width, const uint32_t *order, uint32_t y0, uint32_t y1, uint32_t s0, uint32_t s1,
-                       int threads, double *accum, uint64_t *rays, uint64_t *sphere_tests) {
+                       int threads, double *accum, uint64_t *rays, uint64_t *sphere_tests, uint32_t chunk) {
     if (!cam || !accum || !nodes || (width != 2 && width != 4)) return -1;
     KTree kt;
     kt.width = width;
     kt.nodes = static_cast<const uint8_t *>(nodes);
     kt.n_nodes = n_nodes;
     kt.order = order;
-    return render<float>(cam, s, n, m, nm, tex, ntex, flags, 0, y0, y1, s0, s1, threads, accum, rays, sphere_tests, &kt);
+    return render<float>(cam, s, n, m, nm, tex, ntex, flags, 0, y0, y1, s0, s1, threads, accum, rays, sphere_tests, chunk,
+                         &kt);
 }
 
 // gpu::build_in_one_weekend_scene's sphere/material list (no overrides, camera seed out).

@@ -43,6 +43,7 @@ EXPORTED_SYMBOLS = (
     "rrt_hip_render",
     "rrt_hip_last_error",
     "rrt_hip_abi_version",
+    "rrt_accum_chunk",
     "rrt_scene_create",
     "rrt_scene_destroy",
     "rrt_tile_rows",
@@ -156,6 +157,7 @@ def load() -> ctypes.CDLL:
         "rrt_hip_render": (c_int32, [P, P, c_uint32, P, c_uint32, P, c_uint32, c_uint32, c_uint32, c_uint32, P]),
         "rrt_hip_last_error": (c_char_p, []),
         "rrt_hip_abi_version": (c_uint32, []),
+        "rrt_accum_chunk": (c_uint32, []),
         "rrt_scene_create": (c_int32, [P, P, c_uint32, P, c_uint32, P, c_uint32, c_uint32, c_int32, P]),
         "rrt_scene_destroy": (c_int32, [P]),
         "rrt_tile_rows": (c_int32, [c_uint32, P, P]),

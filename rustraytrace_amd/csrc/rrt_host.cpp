@@ -484,6 +484,9 @@ struct RrtScene {
     rrt::GTexture *d_texs = nullptr;
     unsigned long long *d_counters = nullptr;       // 5 x u64, render launches
     unsigned long long *d_work_counters = nullptr;  // 5 x u64, instrumented launches
+    uint32_t *d_unit_counter = nullptr;             // persistent-queue head
+    float4 *d_partial = nullptr;                    // chunk partial sums
+    size_t partial_cap = 0;                         // float4 elements
     rrt::KParams base{};
     RrtBvhInfo info{};
 };
@@ -501,6 +504,8 @@ void free_scene(RrtScene *s) {
     (void)hipFree(s->d_texs);
     (void)hipFree(s->d_counters);
     (void)hipFree(s->d_work_counters);
+    (void)hipFree(s->d_unit_counter);
+    (void)hipFree(s->d_partial);
     delete s;
 }
 
@@ -543,7 +548,31 @@ int fill_params(RrtScene *s, const RrtTile *t, float *d_accum, rrt::KParams &p) 
     p.sample_end = t->sample_end;
     p.tiles_x = (p.width + 7u) / 8u;
     p.n_work_tiles = p.tiles_x * ((p.tile_rows + 7u) / 8u);
+    const uint32_t S = t->sample_end - t->sample_begin;
+    p.n_chunks = (S + p.chunk - 1) / p.chunk;
+    const uint64_t units = (uint64_t)p.n_work_tiles * p.n_chunks * 64u;
+    if (units > 0xFFFFFFFFull) return fail(RRT_E_INVALID, "tile too large: more than 2^32 work units");
+    p.n_units = (uint32_t)units;
+    p.unit_counter = s->d_unit_counter;
+    if (p.n_chunks > 1) {  // partial sums [pixel][chunk]; grow on demand
+        const size_t need = (size_t)p.tile_rows * p.width * p.n_chunks;
+        if (need > s->partial_cap) {
+            HIP_TRY(hipSetDevice(s->device), "hipSetDevice");
+            (void)hipFree(s->d_partial);
+            s->d_partial = nullptr;
+            s->partial_cap = 0;
+            HIP_TRY(hipMalloc((void **)&s->d_partial, need * sizeof(float4)), "hipMalloc chunk partials");
+            s->partial_cap = need;
+        }
+    }
+    p.partial = s->d_partial;
     return RRT_OK;
+}
+
+uint32_t accum_chunk() {
+    uint32_t c = 64;
+    if (const char *e = std::getenv("RRT_CHUNK")) c = (uint32_t)std::max(1, std::atoi(e));
+    return c;
 }
 
 }  // namespace
@@ -551,6 +580,7 @@ int fill_params(RrtScene *s, const RrtTile *t, float *d_accum, rrt::KParams &p) 
 extern "C" {
 
 const char *rrt_hip_last_error(void) { return g_err.c_str(); }
+uint32_t rrt_accum_chunk(void) { return accum_chunk(); }
 uint32_t rrt_hip_abi_version(void) { return RRT_ABI_VERSION; }
 
 int32_t rrt_device_count(int32_t *count) {
@@ -638,7 +668,8 @@ int32_t rrt_scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint32_
         if ((rc = upload(&s->d_tex_pool, tex_pool.data(), tex_pool.size(), "textures"))) break;
         if ((rc = upload(&s->d_texs, texs.data(), texs.size(), "texture table"))) break;
         if (hipMalloc((void **)&s->d_counters, 8 * sizeof(unsigned long long)) != hipSuccess ||
-            hipMalloc((void **)&s->d_work_counters, 8 * sizeof(unsigned long long)) != hipSuccess) {
+            hipMalloc((void **)&s->d_work_counters, 8 * sizeof(unsigned long long)) != hipSuccess ||
+            hipMalloc((void **)&s->d_unit_counter, 64) != hipSuccess) {
             rc = fail(RRT_E_NOMEM, "hipMalloc counters failed");
             break;
         }
@@ -687,6 +718,12 @@ int32_t rrt_scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint32_
     if (const char *e = std::getenv("RRT_SCENE_IN_LDS")) p.scene_in_lds = p.scene_in_lds && std::atoi(e) != 0;
     p.trav_frac = 32;
     p.min_waves = 5;
+    p.chunk = accum_chunk();
+    {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus < 1) cus = 256;
+        p.n_cus = (uint32_t)cus;
+    }
     if (const char *e = std::getenv("RRT_MIN_WAVES")) p.min_waves = (uint32_t)std::atoi(e);
     if (const char *e = std::getenv("RRT_TRAV_FRAC")) p.trav_frac = (uint32_t)std::min(256, std::max(0, std::atoi(e)));
 
@@ -762,9 +799,14 @@ int32_t rrt_tile_row_index(uint32_t height, const RrtTile *tile, uint32_t local_
 int32_t rrt_render_tile_async(RrtScene *scene, const RrtTile *tile, float *d_accum, void *stream) {
     if (int rc = check_tile(scene, tile)) return rc;
     rrt::KParams p;
-    fill_params(scene, tile, d_accum, p);
+    if (int rc = fill_params(scene, tile, d_accum, p)) return rc;
     if (p.tile_rows && !d_accum) return fail(RRT_E_INVALID, "null d_accum");
     HIP_TRY(hipSetDevice(scene->device), "hipSetDevice");
+    if (p.n_chunks == 0) {  // no samples: accum = 0 (sums and count)
+        HIP_TRY(hipMemsetAsync(d_accum, 0, (size_t)p.tile_rows * p.width * sizeof(float4), (hipStream_t)stream),
+                "hipMemsetAsync accum");
+        return RRT_OK;
+    }
     HIP_TRY(rrt::launch_render(p, (hipStream_t)stream), "render kernel launch");
     return RRT_OK;
 }
@@ -791,7 +833,7 @@ int32_t rrt_scene_count_work(RrtScene *scene, const RrtTile *tile, RrtCounters *
     if (int rc = check_tile(scene, tile)) return rc;
     if (!out) return fail(RRT_E_INVALID, "null out");
     rrt::KParams p;
-    fill_params(scene, tile, nullptr, p);
+    if (int rc = fill_params(scene, tile, nullptr, p)) return rc;
     HIP_TRY(hipSetDevice(scene->device), "hipSetDevice");
     float4 *scratch = nullptr;
     HIP_TRY(hipMalloc((void **)&scratch, std::max<size_t>((size_t)p.tile_rows * p.width, 1) * sizeof(float4)),

@@ -91,6 +91,14 @@ struct KParams {
     uint32_t trav_frac;     // leave the traversal loop when <= live*trav_frac/256 lanes still traverse
     uint32_t bvh_width;     // 2 or 4
     uint32_t min_waves;     // launch-bounds occupancy request (waves per SIMD)
+
+    // persistent work queue: units = (pixel, chunk of `chunk` samples), tile-major
+    uint32_t chunk;           // samples per unit
+    uint32_t n_chunks;        // ceil((sample_end - sample_begin) / chunk)
+    uint32_t n_units;         // n_work_tiles * n_chunks * 64
+    uint32_t n_cus;           // compute units of the device (grid sizing)
+    uint32_t *unit_counter;   // device queue head (zeroed per launch)
+    float4 *partial;          // [tile pixel][chunk] partial sums when n_chunks > 1
 };
 
 // Traversal stack entries held in LDS per lane: up to 64 (BVH depth <= 63).

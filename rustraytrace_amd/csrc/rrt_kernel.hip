@@ -23,6 +23,7 @@
 // equal in exact arithmetic (documented in DESIGN.md).
 #include "rrt_internal.h"
 
+#include <algorithm>
 #include <type_traits>
 
 namespace rrt {
@@ -477,80 +478,112 @@ __device__ __forceinline__ void render_body(const KParams &P) {
     LdsStack<StackT> stack;
     stack.init(lds_stack, threadIdx.x);
 
-    const uint32_t wave = threadIdx.x >> 6;
+    // Persistent waves over a global queue of work units. A unit is (pixel, chunk of
+    // P.chunk samples); unit ids run tile-major — 64 consecutive ids are the 8x8 pixels of
+    // one tile and one chunk, the chunks of a tile follow each other — so a wave's lanes
+    // (and every refill) stay spatially coherent. Lanes whose unit is done claim new units
+    // together: one atomic per refill, issued by the lowest idle lane.
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t tile = blockIdx.x * (kBlock / 64) + wave;
     Counters cnt = {0, 0, 0, 0, 0};
-    bool active = tile < P.n_work_tiles;
-    uint32_t x = 0, ly = 0;
-    if (active) {
-        const uint32_t tx = tile % P.tiles_x;
-        const uint32_t ty = tile / P.tiles_x;
-        x = tx * 8u + (lane & 7u);
-        ly = ty * 8u + (lane >> 3);
-        active = x < P.width && ly < P.tile_rows;
-    }
-    if (active) {
-        // tile-local row -> global image row (row bands dealt round-robin over ranks)
-        const uint32_t band = ly / P.band_rows;
-        const uint32_t y = (band * P.n_ranks + P.rank) * P.band_rows + ly % P.band_rows;
-        const uint32_t pixel = y * P.width + x;
-        const uint64_t key = splitmix64(((uint64_t)P.seed << 32) ^ (uint64_t)pixel);
-
-        V3 sum = v3(0.0f, 0.0f, 0.0f);
-        uint32_t s = P.sample_begin;
-        PathState ps;
-        Trav tr;
-        if (s < P.sample_end) {
-            ps.rng = splitmix64(key + s);
-            camera_ray(P, x, y, ps);
+    bool has = false;     // lane owns a unit
+    bool q_open = true;   // wave-uniform: the queue may still hold units
+    uint32_t x = 0, y = 0, ly = 0, chunk = 0, s = 0, s_hi = 0;
+    uint64_t key = 0;
+    V3 sum = v3(0.0f, 0.0f, 0.0f);
+    PathState ps;
+    Trav tr;
+    bool need_ray = false;  // the lane must start the next segment of its path
+    bool tracing = false;
+    uint32_t pool_base = 0, pool_left = 0;  // wave-uniform: claimed, not yet assigned units
+    for (;;) {
+        uint64_t idle = __ballot(!has);
+        if (idle != 0 && pool_left == 0 && q_open) {
+            // one atomic claims a whole tile-chunk (64 units) for this wave
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(P.unit_counter, 64u);
+            base = __shfl(base, 0, 64);
+            if (base >= P.n_units) {
+                q_open = false;
+            } else {
+                pool_base = base;
+                pool_left = min(64u, P.n_units - base);
+            }
         }
-        bool need_ray = true;  // the lane must start the next segment of its path
-        bool tracing = false;
-        while (s < P.sample_end) {
-            if (need_ray) {
-                if (ps.k >= P.max_depth) {  // ray_color: depth <= 0 -> 0 (no query)
-                    sum = add(sum, ps.L);
-                    cnt.paths++;
-                    ++s;
-                    if (s < P.sample_end) {
+        if (idle != 0 && pool_left != 0) {
+            const uint32_t n = min((uint32_t)__popcll(idle), pool_left);
+            const uint32_t r = (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
+            if (!has && r < n) {
+                const uint32_t u = pool_base + r;
+                {
+                    const uint32_t lit = u & 63u;
+                    const uint32_t tc = u >> 6;
+                    const uint32_t t = tc / P.n_chunks;
+                    chunk = tc - t * P.n_chunks;
+                    x = (t % P.tiles_x) * 8u + (lit & 7u);
+                    ly = (t / P.tiles_x) * 8u + (lit >> 3);
+                    if (x < P.width && ly < P.tile_rows) {
+                        // tile-local row -> global image row (row bands dealt round-robin over ranks)
+                        const uint32_t band = ly / P.band_rows;
+                        y = (band * P.n_ranks + P.rank) * P.band_rows + ly % P.band_rows;
+                        key = splitmix64(((uint64_t)P.seed << 32) ^ (uint64_t)(y * P.width + x));
+                        s = P.sample_begin + chunk * P.chunk;
+                        s_hi = min(s + P.chunk, P.sample_end);
+                        sum = v3(0.0f, 0.0f, 0.0f);
                         ps.rng = splitmix64(key + s);
                         camera_ray(P, x, y, ps);
+                        need_ray = true;
+                        has = true;
                     }
-                    continue;
                 }
+            }
+            pool_base += n;
+            pool_left -= n;
+        }
+        if (__ballot(has) == 0) break;
+
+        bool seg_done = false;  // the lane's path ended without a query (depth limit)
+        if (has && need_ray) {
+            if (ps.k >= P.max_depth) {  // ray_color: depth <= 0 -> 0 (no query)
+                seg_done = true;
+            } else {
                 trav_begin(tr, ps.o, ps.d);
                 cnt.rays++;
                 need_ray = false;
                 tracing = true;
             }
-            // Traverse until too few lanes of the wave are still in the tree, then let the
-            // finished lanes shade and fetch their next segment (wave-uniform ballot exit).
-            const uint32_t live = (uint32_t)__popcll(__ballot(1));
-            const uint32_t min_active = (live * P.trav_frac) >> 8;
-            for (;;) {
-                if (tracing) {
-                    bool fin;
-                    if constexpr (kWide) fin = trav_step4<kCount>(nodes, prims, stack, ps.o, ps.d, tr, cnt);
-                    else fin = trav_step<kCount>(nodes, prims, stack, ps.o, ps.d, tr, cnt);
-                    if (fin) tracing = false;
-                }
-                if ((uint32_t)__popcll(__ballot(tracing)) <= min_active) break;
+        }
+        // Traverse until too few lanes of the wave are still in the tree, then let the
+        // finished lanes shade and fetch their next segment (wave-uniform ballot exit).
+        const uint32_t live = (uint32_t)__popcll(__ballot(has));
+        const uint32_t min_active = (live * P.trav_frac) >> 8;
+        for (;;) {
+            if (tracing) {
+                bool fin;
+                if constexpr (kWide) fin = trav_step4<kCount>(nodes, prims, stack, ps.o, ps.d, tr, cnt);
+                else fin = trav_step<kCount>(nodes, prims, stack, ps.o, ps.d, tr, cnt);
+                if (fin) tracing = false;
             }
-            if (!tracing) {
-                need_ray = true;
-                if (shade(P, prims, ps, tr.closest, tr.hit_prim)) {
-                    sum = add(sum, ps.L);  // pixel_color += ray_color(..) (camera.rs:73-76)
-                    cnt.paths++;
-                    ++s;
-                    if (s < P.sample_end) {
-                        ps.rng = splitmix64(key + s);
-                        camera_ray(P, x, y, ps);
-                    }
-                }
+            if ((uint32_t)__popcll(__ballot(tracing)) <= min_active) break;
+        }
+        if (has && !need_ray && !tracing) {
+            need_ray = true;
+            seg_done = shade(P, prims, ps, tr.closest, tr.hit_prim);
+        }
+        if (seg_done) {
+            sum = add(sum, ps.L);  // pixel_color += ray_color(..) (camera.rs:73-76)
+            cnt.paths++;
+            ++s;
+            if (s < s_hi) {
+                ps.rng = splitmix64(key + s);
+                camera_ray(P, x, y, ps);
+            } else {  // unit complete: the chunk's sum, in sample order
+                const size_t px = (size_t)ly * P.width + x;
+                const float4 out = make_float4(sum.x, sum.y, sum.z, (float)(s_hi - (P.sample_begin + chunk * P.chunk)));
+                if (P.n_chunks == 1) P.accum[px] = out;
+                else P.partial[px * P.n_chunks + chunk] = out;
+                has = false;
             }
         }
-        P.accum[(size_t)ly * P.width + x] = make_float4(sum.x, sum.y, sum.z, (float)(P.sample_end - P.sample_begin));
     }
     // one atomic per wave per counter
     const uint32_t r = wave_sum_u32(cnt.rays);
@@ -577,16 +610,44 @@ __global__ __launch_bounds__(kBlock, kWaves) void rrt_render(KParams P) {
     render_body<kLds, kCount, StackT, kWide>(P);
 }
 
+// accum[p] = sum over chunks c = 0..n-1 (in order) of partial[p][c].rgb; w = sample count.
+__global__ __launch_bounds__(256) void rrt_combine_chunks(const float4 *__restrict__ partial, float4 *__restrict__ accum,
+                                                          uint32_t n_pixels, uint32_t n_chunks, float count) {
+    const uint32_t p = blockIdx.x * 256u + threadIdx.x;
+    if (p >= n_pixels) return;
+    const float4 *src = partial + (size_t)p * n_chunks;
+    float4 acc = src[0];
+    for (uint32_t c = 1; c < n_chunks; ++c) {
+        const float4 v = src[c];
+        acc.x = acc.x + v.x;
+        acc.y = acc.y + v.y;
+        acc.z = acc.z + v.z;
+    }
+    accum[p] = make_float4(acc.x, acc.y, acc.z, count);
+}
+
 template <bool kLds, typename StackT, bool kWide, int kWaves = 1>
 hipError_t launch_variant(const KParams &p, bool count, hipStream_t stream) {
-    const uint32_t blocks = (p.n_work_tiles + (kBlock / 64) - 1) / (kBlock / 64);
-    if (blocks == 0) return hipSuccess;
+    if (p.n_units == 0) return hipSuccess;
     size_t lds = ((size_t)p.stack_depth * kBlock * sizeof(StackT) + 15u) / 16u * 16u;
     if (kLds) lds += (size_t)p.n_nodes * (kWide ? sizeof(GNode4) : sizeof(GNode)) + (size_t)p.n_prims * sizeof(float4);
-    if (count)
-        hipLaunchKernelGGL((rrt_render<kLds, true, StackT, kWide, kWaves>), dim3(blocks), dim3(kBlock), lds, stream, p);
-    else
-        hipLaunchKernelGGL((rrt_render<kLds, false, StackT, kWide, kWaves>), dim3(blocks), dim3(kBlock), lds, stream, p);
+    auto kernel = count ? rrt_render<kLds, true, StackT, kWide, kWaves> : rrt_render<kLds, false, StackT, kWide, kWaves>;
+    // Persistent grid: as many blocks as can be resident (occupancy at this LDS size), capped
+    // by the work; the queue counter is zeroed on the stream before the launch.
+    int per_cu = 0;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, lds);
+    if (e != hipSuccess) return e;
+    if (per_cu < 1) per_cu = 1;
+    const uint32_t want = (p.n_units + kBlock - 1) / kBlock;
+    const uint32_t blocks = std::min<uint32_t>(want, (uint32_t)per_cu * p.n_cus);
+    e = hipMemsetAsync(p.unit_counter, 0, sizeof(uint32_t), stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(kernel, dim3(blocks), dim3(kBlock), lds, stream, p);
+    e = hipGetLastError();
+    if (e != hipSuccess || p.n_chunks <= 1) return e;
+    const uint32_t n_pixels = p.tile_rows * p.width;
+    hipLaunchKernelGGL(rrt_combine_chunks, dim3((n_pixels + 255) / 256), dim3(256), 0, stream, p.partial, p.accum,
+                       n_pixels, p.n_chunks, (float)(p.sample_end - p.sample_begin));
     return hipGetLastError();
 }
 

@@ -137,3 +137,9 @@ def test_cli_mirrors_main_rs():
         r = subprocess.run([cli, "--cuda", "in_one_weekend", "--image_width", "16", "--samples_per_pixel", "1"],
                            capture_output=True, text=True)
         assert r.returncode == 1 and "HIP render failed: no HIP device" in r.stderr
+
+
+def test_accum_chunk_matches_oracle_default():
+    from oracle import oracle
+
+    assert _lib.load().rrt_accum_chunk() == oracle.DEFAULT_CHUNK

@@ -134,3 +134,21 @@ def test_multi_gpu_one_shot_equals_single():
         assert np.array_equal(a, b)
     with pytest.raises(rrt.RrtError):
         rrt.render(scene, n_gpus=n + 1)
+
+
+@pytest.mark.parametrize("spp,s0", [(200, 0), (130, 7)])
+def test_chunked_accumulation_matches_oracle(spp, s0):
+    # > rrt_accum_chunk() samples: the persistent queue splits pixels into chunks whose sums are
+    # combined in chunk order; the oracle reproduces that order (rows, partial last chunk, offset).
+    assert rrt._lib.load().rrt_accum_chunk() == oracle.DEFAULT_CHUNK
+    scene = rrt.rtow(image_width=24, samples_per_pixel=spp, max_depth=8)
+    gpu, idx, ctr, _ = gpu_tile(scene, s0=s0, s1=s0 + spp)
+    ref, rays, _ = oracle.render(scene, oracle.TWIN, samples=(s0, s0 + spp))
+    assert_bit_exact(gpu, ref, spp)
+    assert np.all(gpu[..., 3] == spp) and ctr["rays"] == rays
+
+
+def test_zero_samples_tile():
+    scene = rrt.rtow(image_width=16, samples_per_pixel=4, max_depth=4)
+    gpu, idx, ctr, _ = gpu_tile(scene, s0=3, s1=3)
+    assert np.all(gpu == 0) and ctr["rays"] == 0
