@@ -14,7 +14,7 @@ from ctypes import POINTER, c_char_p, c_double, c_float, c_int32, c_size_t, c_ui
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "librrt_hip.so")
+LIB_PATH = os.environ.get("RRT_LIB_PATH") or os.path.join(PKG_DIR, "librrt_hip.so")  # override: experiments only
 
 # ---- #[repr(C)] layouts (gpu/mod.rs:13-42) as numpy dtypes ------------------------------------
 CAMERA_DTYPE = np.dtype(

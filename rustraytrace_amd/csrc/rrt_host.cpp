@@ -717,7 +717,7 @@ int32_t rrt_scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint32_
     p.scene_in_lds = scene_bytes <= rrt::kLdsSceneBudget;
     if (const char *e = std::getenv("RRT_SCENE_IN_LDS")) p.scene_in_lds = p.scene_in_lds && std::atoi(e) != 0;
     p.trav_frac = 32;
-    p.min_waves = 5;
+    p.min_waves = 6;
     p.chunk = accum_chunk();
     {
         int cus = 0;

@@ -103,7 +103,14 @@ struct KParams {
 
 // Traversal stack entries held in LDS per lane: up to 64 (BVH depth <= 63).
 constexpr int kMaxStackDepth = 64;
-constexpr int kBlock = 256;
+#ifndef RRT_BLOCK
+#define RRT_BLOCK 512
+#endif
+#ifndef RRT_WAVES
+#define RRT_WAVES 6
+#endif
+constexpr int kBlock = RRT_BLOCK;          // threads per block (4 or 8 waves)
+constexpr int kWavesPerSimd = RRT_WAVES;   // launch-bounds occupancy target of the main variant
 // Per-block LDS budget for staging the scene (BVH nodes + spheres) next to the stack.
 constexpr size_t kLdsSceneBudget = 40 * 1024;
 

@@ -192,6 +192,31 @@ __device__ __forceinline__ void test_prims(const float4 *__restrict__ prim_cr, i
     }
 }
 
+// Leaf spheres of two ranges [f0, f0+c0) then [f1, f1+c1) in one loop.
+template <bool kCount>
+__device__ __forceinline__ void test_prims2(const float4 *__restrict__ prim_cr, int f0, int c0, int f1, int c1, V3 o,
+                                            V3 d, float a, float &closest, int &hit_prim, Counters &cnt) {
+    const int total = c0 + c1;
+    for (int k = 0; k < total; ++k) {
+        const int i = (k < c0) ? f0 + k : f1 + (k - c0);
+        if (kCount) cnt.spheres++;
+        const float4 cr = prim_cr[i];
+        const V3 oc = v3(cr.x - o.x, cr.y - o.y, cr.z - o.z);
+        const float h = dot(d, oc);
+        const float c = dot(oc, oc) - cr.w * cr.w;
+        const float disc = h * h - a * c;
+        if (disc < 0.0f) continue;
+        const float sq = __builtin_sqrtf(disc);
+        float root = (h - sq) / a;
+        if (!(0.001f < root && root < closest)) {
+            root = (h + sq) / a;
+            if (!(0.001f < root && root < closest)) continue;
+        }
+        closest = root;
+        hit_prim = i;
+    }
+}
+
 // Traversal stack in LDS. 16-bit entries: the dword at (depth, wave, k) holds lanes k and
 // k+32, which the LDS serves in different cycles (2 x 32-lane groups), so no bank conflicts.
 template <typename StackT>
@@ -241,13 +266,13 @@ __device__ __forceinline__ bool trav_step(const GNode *__restrict__ nodes, const
     float tn0 = 0.0f, tn1 = 0.0f;
     bool h0 = box_hit(n.b0.x, n.b0.y, n.b0.z, n.b0.w, n.b1.x, n.b1.y, t.inv, t.oi, 0.001f, t.closest, tn0);
     bool h1 = box_hit(n.b1.z, n.b1.w, n.b2.x, n.b2.y, n.b2.z, n.b2.w, t.inv, t.oi, 0.001f, t.closest, tn1);
-    if (h0 && n.link.z > 0) {
-        test_prims<kCount>(prims, n.link.x, n.link.z, o, d, t.a, t.closest, t.hit_prim, cnt);
-        h0 = false;
-    }
-    if (h1 && n.link.w > 0) {
-        test_prims<kCount>(prims, n.link.y, n.link.w, o, d, t.a, t.closest, t.hit_prim, cnt);
-        h1 = false;
+    // Leaf children: one loop over leaf 0's spheres then leaf 1's (one divergent loop, not two).
+    const int c0 = (h0 && n.link.z > 0) ? n.link.z : 0;
+    const int c1 = (h1 && n.link.w > 0) ? n.link.w : 0;
+    if (c0 + c1 > 0) {
+        test_prims2<kCount>(prims, n.link.x, c0, n.link.y, c1, o, d, t.a, t.closest, t.hit_prim, cnt);
+        if (c0) h0 = false;
+        if (c1) h1 = false;
     }
     if (h0 && h1) {
         const bool first1 = tn1 < tn0;
@@ -403,8 +428,12 @@ __device__ __forceinline__ bool shade(const KParams &P, const float4 *prims, Pat
     if (kind == 4) {  // DiffuseLight: emitted, scatter None
         ps.L = add(ps.L, mul(ps.T, v3(m.a.x, m.a.y, m.a.z)));
         return true;
-    } else if (kind == 0 || kind == 3) {  // Lambertian (material.rs:28-40)
-        const V3 r = random_unit_vector(ps.rng);
+    }
+    // Lambertian and Metal both draw one random_unit_vector and nothing else before RR: one
+    // rejection loop for both kinds (a wave mixing them runs it once, not twice).
+    V3 r = v3(0.0f, 0.0f, 0.0f);
+    if (kind != 2) r = random_unit_vector(ps.rng);
+    if (kind == 0 || kind == 3) {  // Lambertian (material.rs:28-40)
         dir = add(nrm, r);
         if (__builtin_fabsf(dir.x) < 1e-8f && __builtin_fabsf(dir.y) < 1e-8f && __builtin_fabsf(dir.z) < 1e-8f) dir = nrm;
         if (kind == 3) {
@@ -416,7 +445,6 @@ __device__ __forceinline__ bool shade(const KParams &P, const float4 *prims, Pat
         }
     } else if (kind == 1) {  // Metal (material.rs:53-64)
         const V3 refl = unit(reflect(ps.d, nrm));
-        const V3 r = random_unit_vector(ps.rng);
         dir = add(refl, muls(r, m.a.w));
         if (!(dot(dir, nrm) > 0.0f)) return true;  // absorbed
         att = v3(m.a.x, m.a.y, m.a.z);
@@ -426,8 +454,8 @@ __device__ __forceinline__ bool shade(const KParams &P, const float4 *prims, Pat
         const V3 ud = unit(ps.d);
         float c = -dot(ud, nrm);
         c = (c < 1.0f) ? c : 1.0f;
-        const float s = __builtin_sqrtf(1.0f - c * c);
-        const bool cannot = ri * s > 1.0f;
+        const float sn = __builtin_sqrtf(1.0f - c * c);
+        const bool cannot = ri * sn > 1.0f;
         if (cannot || reflectance(c, ri) > rnd(ps.rng)) dir = reflect(ud, nrm);
         else dir = refract(ud, nrm, ri);
         att = v3(1.0f, 1.0f, 1.0f);
@@ -655,7 +683,7 @@ template <bool kWide>
 hipError_t launch_width(const KParams &p, bool count, hipStream_t stream) {
     if (p.stack_depth > (uint32_t)kMaxStackDepth) return hipErrorInvalidValue;
     if (p.n_nodes > 65535u) return launch_variant<false, uint32_t, kWide>(p, count, stream);
-    if (!kWide && p.scene_in_lds && p.min_waves >= 6) return launch_variant<true, uint16_t, kWide, 6>(p, count, stream);
+    if (!kWide && p.scene_in_lds && p.min_waves >= 6) return launch_variant<true, uint16_t, kWide, kWavesPerSimd>(p, count, stream);
     return p.scene_in_lds ? launch_variant<true, uint16_t, kWide>(p, count, stream)
                           : launch_variant<false, uint16_t, kWide>(p, count, stream);
 }
