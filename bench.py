@@ -23,8 +23,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "Mrays/sec + wall-clock for 1920×1080×512spp RTOW final scene"
-PEAK_F32_VALU_TFLOPS = 78.6  # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz, non-packed f32 (MI355X_MICROARCH.md)
-PEAK_F32_PACKED_TFLOPS = 157.3
+# f32 VALU peak: CDNA4 SIMDs are 32 lanes wide, a wave64 v_fma_f32 issues in 2 cycles
+# (MI355X_MICROARCH.md constants table; cdna_hip_programming.md "CU = 4 x SIMD-32"), so
+# 256 CU x 4 SIMD x 32 lanes x 2 FLOP x 2.4 GHz = 157.3 TFLOP/s; v_pk_fma_f32 has the same peak.
+PEAK_F32_VALU_TFLOPS = 157.3
 FLOP_PER_SPHERE_TEST = 23  # sphere.rs:26-31
 FLOP_PER_BOX_TEST = 12  # aabb.rs:56-82 with hoisted reciprocal
 BYTES_PER_SPHERE_TEST = 16
@@ -208,7 +210,8 @@ def main():
                 "algorithmic_bytes_per_launch": alg_bytes,
                 "effective_fetch_GBps": round(alg_bytes / avg_kernel_s / 1e9, 1),
                 "note": "f32 VALU issue bound (SURVEY 8d): 23 FLOP/sphere test + 12 FLOP/box test over the "
-                        "average HIP-event kernel time; packed f32 peak would be 157.3",
+                        "average HIP-event kernel time; peak = wave64 v_fma_f32 at 2 cycles on SIMD-32 "
+                        "(SURVEY 8d's 78.6 assumed 16-lane SIMDs)",
             },
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -478,8 +478,7 @@ struct RrtScene {
     int device = 0;
     uint8_t *d_nodes = nullptr;
     float4 *d_prim_cr = nullptr;
-    uint32_t *d_prim_mat = nullptr;
-    rrt::GMaterial *d_mats = nullptr;
+    rrt::GMaterial *d_prim_mtl = nullptr;
     uint8_t *d_tex_pool = nullptr;
     rrt::GTexture *d_texs = nullptr;
     unsigned long long *d_counters = nullptr;       // 5 x u64, render launches
@@ -498,8 +497,7 @@ void free_scene(RrtScene *s) {
     (void)hipSetDevice(s->device);
     (void)hipFree(s->d_nodes);
     (void)hipFree(s->d_prim_cr);
-    (void)hipFree(s->d_prim_mat);
-    (void)hipFree(s->d_mats);
+    (void)hipFree(s->d_prim_mtl);
     (void)hipFree(s->d_tex_pool);
     (void)hipFree(s->d_texs);
     (void)hipFree(s->d_counters);
@@ -622,15 +620,9 @@ int32_t rrt_scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint32_
     const FlatBvh fb = build_bvh(spheres, n_spheres, width, max_leaf, order);
     if (fb.stack_need > (uint32_t)rrt::kMaxStackDepth)
         return fail(RRT_E_INVALID, "BVH depth " + std::to_string(fb.max_depth) + " exceeds the LDS stack");
+    // postponed leaf tests pack (first primitive, count) as first | count << 28
+    if (fb.max_leaf > 15 || n_spheres >= (1u << 28)) return fail(RRT_E_INVALID, "leaf size > 15 or >= 2^28 spheres");
 
-    std::vector<float4> prim_cr(n_spheres);
-    std::vector<uint32_t> prim_mat(n_spheres);
-    for (uint32_t i = 0; i < n_spheres; ++i) {
-        const RrtSphere &sp = spheres[order[i]];
-        prim_cr[i] = make_float4(sp.center_radius[0], sp.center_radius[1], sp.center_radius[2],
-                                 std::max(sp.center_radius[3], 0.0f));
-        prim_mat[i] = sp.material_index;
-    }
     std::vector<rrt::GMaterial> mats(n_materials);
     for (uint32_t i = 0; i < n_materials; ++i) {
         const RrtMaterial &m = materials[i];
@@ -640,6 +632,16 @@ int32_t rrt_scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint32_
         std::memcpy(&ref_bits, &m.ref_idx, 4);
         mats[i].a = make_float4(m.albedo_fuzz[0], m.albedo_fuzz[1], m.albedo_fuzz[2], fuzz);
         mats[i].b = make_int4((int)m.kind, ref_bits, (int)m._pad[0], 0);
+    }
+    // Spheres in BVH leaf order, each with a copy of its material record: a hit reads one
+    // 32-B record at the primitive's index (no dependent material-index fetch).
+    std::vector<float4> prim_cr(n_spheres);
+    std::vector<rrt::GMaterial> prim_mtl(n_spheres);
+    for (uint32_t i = 0; i < n_spheres; ++i) {
+        const RrtSphere &sp = spheres[order[i]];
+        prim_cr[i] = make_float4(sp.center_radius[0], sp.center_radius[1], sp.center_radius[2],
+                                 std::max(sp.center_radius[3], 0.0f));
+        prim_mtl[i] = mats[sp.material_index];
     }
     std::vector<rrt::GTexture> texs(n_textures);
     size_t pool = 0;
@@ -663,8 +665,7 @@ int32_t rrt_scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint32_
         if (hipSetDevice(device) != hipSuccess) { rc = fail(RRT_E_HIP, "hipSetDevice failed"); break; }
         if ((rc = upload(&s->d_nodes, fb.bytes.data(), fb.bytes.size(), "nodes"))) break;
         if ((rc = upload(&s->d_prim_cr, prim_cr.data(), prim_cr.size(), "spheres"))) break;
-        if ((rc = upload(&s->d_prim_mat, prim_mat.data(), prim_mat.size(), "sphere materials"))) break;
-        if ((rc = upload(&s->d_mats, mats.data(), mats.size(), "materials"))) break;
+        if ((rc = upload(&s->d_prim_mtl, prim_mtl.data(), prim_mtl.size(), "sphere materials"))) break;
         if ((rc = upload(&s->d_tex_pool, tex_pool.data(), tex_pool.size(), "textures"))) break;
         if ((rc = upload(&s->d_texs, texs.data(), texs.size(), "texture table"))) break;
         if (hipMalloc((void **)&s->d_counters, 8 * sizeof(unsigned long long)) != hipSuccess ||
@@ -687,8 +688,7 @@ int32_t rrt_scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint32_
     rrt::KParams &p = s->base;
     p.nodes = s->d_nodes;
     p.prim_cr = s->d_prim_cr;
-    p.prim_mat = s->d_prim_mat;
-    p.mats = s->d_mats;
+    p.prim_mtl = s->d_prim_mtl;
     p.tex_pool = s->d_tex_pool;
     p.texs = s->d_texs;
     p.counters = s->d_counters;
@@ -713,10 +713,11 @@ int32_t rrt_scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint32_
     p.n_prims = n_spheres;
     p.stack_depth = fb.stack_need;
     p.bvh_width = fb.width;
-    const size_t scene_bytes = fb.bytes.size() + (size_t)n_spheres * sizeof(float4);
+    const size_t scene_bytes = fb.bytes.size() + (size_t)n_spheres * rrt::kPrimBytes;
     p.scene_in_lds = scene_bytes <= rrt::kLdsSceneBudget;
     if (const char *e = std::getenv("RRT_SCENE_IN_LDS")) p.scene_in_lds = p.scene_in_lds && std::atoi(e) != 0;
     p.trav_frac = 32;
+    p.leaf_frac = 32;
     p.min_waves = 6;
     p.chunk = accum_chunk();
     {
@@ -726,6 +727,7 @@ int32_t rrt_scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint32_
     }
     if (const char *e = std::getenv("RRT_MIN_WAVES")) p.min_waves = (uint32_t)std::atoi(e);
     if (const char *e = std::getenv("RRT_TRAV_FRAC")) p.trav_frac = (uint32_t)std::min(256, std::max(0, std::atoi(e)));
+    if (const char *e = std::getenv("RRT_LEAF_FRAC")) p.leaf_frac = (uint32_t)std::min(256, std::max(0, std::atoi(e)));
 
     RrtBvhInfo &bi = s->info;
     bi.n_nodes = fb.n_nodes;
@@ -735,7 +737,7 @@ int32_t rrt_scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint32_
     bi.node_bytes = fb.bytes.size();
     bi.width = fb.width;
     bi.max_leaf_param = max_leaf;
-    bi.prim_bytes = (uint64_t)n_spheres * (sizeof(float4) + sizeof(uint32_t));
+    bi.prim_bytes = (uint64_t)n_spheres * rrt::kPrimBytes;
     *out = s;
     return RRT_OK;
 }
@@ -757,7 +759,7 @@ int32_t rrt_build_bvh(const RrtSphere *spheres, uint32_t n_spheres, uint32_t wid
         info->max_depth = fb.max_depth;
         info->max_leaf_size = fb.max_leaf;
         info->node_bytes = fb.bytes.size();
-        info->prim_bytes = (uint64_t)n_spheres * (sizeof(float4) + sizeof(uint32_t));
+        info->prim_bytes = (uint64_t)n_spheres * rrt::kPrimBytes;
         info->width = fb.width;
         info->max_leaf_param = max_leaf;
     }

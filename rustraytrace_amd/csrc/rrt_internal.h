@@ -51,8 +51,7 @@ struct GTexture {
 struct KParams {
     const void *nodes;           // GNode[] (bvh_width 2) or GNode4[] (bvh_width 4)
     const float4 *prim_cr;       // sphere center.xyz, radius — in BVH leaf order
-    const uint32_t *prim_mat;    // material index per primitive (leaf order)
-    const GMaterial *mats;
+    const GMaterial *prim_mtl;   // each primitive's material record, same order (one fetch per hit)
     const uint8_t *tex_pool;
     const GTexture *texs;
     float4 *accum;               // tile-local rows * width
@@ -87,8 +86,9 @@ struct KParams {
     uint32_t n_nodes;
     uint32_t n_prims;
     uint32_t stack_depth;   // entries needed (BVH depth + 1)
-    uint32_t scene_in_lds;  // stage nodes + spheres in LDS per block
+    uint32_t scene_in_lds;  // stage nodes + spheres + their materials in LDS per block
     uint32_t trav_frac;     // leave the traversal loop when <= live*trav_frac/256 lanes still traverse
+    uint32_t leaf_frac;     // run the postponed-leaf loop when > live*leaf_frac/256 lanes wait on leaf tests
     uint32_t bvh_width;     // 2 or 4
     uint32_t min_waves;     // launch-bounds occupancy request (waves per SIMD)
 
@@ -111,8 +111,11 @@ constexpr int kMaxStackDepth = 64;
 #endif
 constexpr int kBlock = RRT_BLOCK;          // threads per block (4 or 8 waves)
 constexpr int kWavesPerSimd = RRT_WAVES;   // launch-bounds occupancy target of the main variant
-// Per-block LDS budget for staging the scene (BVH nodes + spheres) next to the stack.
+// Per-block LDS budget for staging the scene (BVH nodes + spheres + per-sphere materials)
+// next to the stack. RTOW: 13.5 KB nodes + 486 x 48 B = 36.9 KB; + ~11 KB of stack per
+// 512-thread block keeps 3 blocks (6 waves/SIMD) within the CU's 160 KB.
 constexpr size_t kLdsSceneBudget = 40 * 1024;
+constexpr size_t kPrimBytes = sizeof(float4) + sizeof(GMaterial);  // per primitive: sphere + material
 
 // Launch wrappers implemented in rrt_kernel.hip.
 hipError_t launch_render(const KParams &p, hipStream_t stream);

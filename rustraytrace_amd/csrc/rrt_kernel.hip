@@ -29,6 +29,22 @@
 namespace rrt {
 namespace {
 
+// Debug builds only (-DRRT_PHASE_TIMING=1..4, never the shipped library): per-wave phase
+// statistics written into counter slots 2..4 by the non-counting kernel.
+//   1: s_memtime cycles spent in refill+ray start / traversal loop / shading
+//   2: traversal wave-iterations x 64 / sum of tracing lanes per iteration / outer iterations
+//   3: leaf-loop wave-iterations x 64 / active lanes per leaf iteration / lanes taking the root branch
+//   4: shade entries x 64 / shading lanes / rejection-loop wave-iterations x 64
+#ifndef RRT_PHASE_TIMING
+#define RRT_PHASE_TIMING 0
+#endif
+
+// 64 if the calling lane is the wave's first active lane, else 0 (wave-level event count).
+__device__ __forceinline__ uint32_t wave_slot() {
+    return (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x) == threadIdx.x ? 64u : 0u;
+}
+
+
 struct V3 {
     float x, y, z;
 };
@@ -69,8 +85,10 @@ __device__ __forceinline__ float rnd_range(uint64_t &s, float lo, float hi) { re
 
 // vec3.rs:181-189 random_unit_vector: rejection in [-1,1)^3, accept 1e-160 < |p|^2 <= 1
 // (1e-160 underflows to 0 in f32: the one intentional f32 deviation).
-__device__ __forceinline__ V3 random_unit_vector(uint64_t &s) {
+template <typename C>
+__device__ __forceinline__ V3 random_unit_vector(uint64_t &s, C &cnt) {
     for (;;) {
+        if constexpr (RRT_PHASE_TIMING == 4) cnt.d2 += wave_slot();
         const float px = rnd_range(s, -1.0f, 1.0f);
         const float py = rnd_range(s, -1.0f, 1.0f);
         const float pz = rnd_range(s, -1.0f, 1.0f);
@@ -165,8 +183,10 @@ __device__ __forceinline__ bool box_hit(float lx, float hx, float ly, float hy, 
     return nr < fr;
 }
 
+// Per-lane work counts of the instrumented (counting) kernel variant (+ debug statistics).
 struct Counters {
-    uint32_t rays, paths, nodes, boxes, spheres;
+    uint32_t nodes, boxes, spheres;
+    uint32_t d0, d1, d2;
 };
 
 // Sphere::hit (sphere.rs:24-51) root selection; returns true and shrinks `closest`.
@@ -200,12 +220,17 @@ __device__ __forceinline__ void test_prims2(const float4 *__restrict__ prim_cr, 
     for (int k = 0; k < total; ++k) {
         const int i = (k < c0) ? f0 + k : f1 + (k - c0);
         if (kCount) cnt.spheres++;
+        if constexpr (RRT_PHASE_TIMING == 3) {
+            cnt.d0 += wave_slot();
+            cnt.d1 += 1;
+        }
         const float4 cr = prim_cr[i];
         const V3 oc = v3(cr.x - o.x, cr.y - o.y, cr.z - o.z);
         const float h = dot(d, oc);
         const float c = dot(oc, oc) - cr.w * cr.w;
         const float disc = h * h - a * c;
         if (disc < 0.0f) continue;
+        if constexpr (RRT_PHASE_TIMING == 3) cnt.d2 += 1;
         const float sq = __builtin_sqrtf(disc);
         float root = (h - sq) / a;
         if (!(0.001f < root && root < closest)) {
@@ -234,43 +259,107 @@ struct LdsStack {
     __device__ __forceinline__ int load(int sp) const { return (int)base[sp * kBlock]; }
 };
 
-// Resumable BVH2 traversal: one call = one node. The state lives in registers (+ the LDS stack)
-// so a wave can leave the traversal loop while some lanes are still mid-tree.
-struct Trav {
+// Per-ray constants of the box and sphere tests. Recomputed from (o, d) each time a wave
+// enters its traversal loop rather than kept alive across shading (same IEEE ops, so the
+// same values): 7 fewer registers held by lanes parked mid-tree.
+struct RayK {
     V3 inv;
     V3 oi;  // o * inv
     float a;
+};
+
+__device__ __forceinline__ RayK ray_consts(V3 o, V3 d) {
+    RayK r;
+    r.inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);  // aabb.rs:58 adinv, hoisted per ray
+    r.oi = v3(o.x * r.inv.x, o.y * r.inv.y, o.z * r.inv.z);
+    r.a = dot(d, d);                                  // sphere.rs:27, hoisted per ray
+    return r;
+}
+
+// Resumable BVH traversal: one call = one node. The state lives in registers (+ the LDS stack)
+// so a wave can leave the traversal loop while some lanes are still mid-tree.
+struct Trav {
     float closest;
     int hit_prim;
     int node;
     int sp;
 };
 
-__device__ __forceinline__ void trav_begin(Trav &t, V3 o, V3 d) {
-    t.inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);  // aabb.rs:58 adinv, hoisted per ray
-    t.oi = v3(o.x * t.inv.x, o.y * t.inv.y, o.z * t.inv.z);
-    t.a = dot(d, d);                                  // sphere.rs:27, hoisted per ray
-    t.closest = __builtin_inff();                      // camera.rs:187 Interval(0.001, INFINITY)
+__device__ __forceinline__ void trav_begin(Trav &t) {
+    t.closest = __builtin_inff();  // camera.rs:187 Interval(0.001, INFINITY)
     t.hit_prim = -1;
     t.node = 0;
     t.sp = 0;
+}
+
+// A lane's postponed leaf tests: spheres [first0, first0+count0) then [first1, first1+count1),
+// packed first | count << 28 (leaf sizes <= 15, primitive indices < 2^28).
+struct Leaves {
+    uint32_t l0, l1;
+};
+constexpr uint32_t kLeafFirstMask = (1u << 28) - 1u;
+
+// BVH2 node visit with postponed leaf tests: tests both child boxes against the current
+// closest hit, records leaf children in `lv` (tested later, before this lane's next node
+// visit), descends into the nearer internal child and pushes the farther one; t.node = -1
+// when nothing is left to visit. The next node depends only on these box results, so
+// testing the leaves later keeps every ray's sequence of operations unchanged. Returns
+// true when leaf tests are pending.
+template <bool kCount, typename Stack>
+__device__ __forceinline__ bool trav_node(const GNode *__restrict__ nodes, Stack &stack, const RayK &rk, Trav &t,
+                                          Leaves &lv, Counters &cnt) {
+    const GNode n = nodes[t.node];
+    if (kCount) { cnt.nodes++; cnt.boxes += 2; }
+    float tn0 = 0.0f, tn1 = 0.0f;
+    bool h0 = box_hit(n.b0.x, n.b0.y, n.b0.z, n.b0.w, n.b1.x, n.b1.y, rk.inv, rk.oi, 0.001f, t.closest, tn0);
+    bool h1 = box_hit(n.b1.z, n.b1.w, n.b2.x, n.b2.y, n.b2.z, n.b2.w, rk.inv, rk.oi, 0.001f, t.closest, tn1);
+    const uint32_t c0 = (h0 && n.link.z > 0) ? (uint32_t)n.link.z : 0u;
+    const uint32_t c1 = (h1 && n.link.w > 0) ? (uint32_t)n.link.w : 0u;
+    lv.l0 = (uint32_t)n.link.x | (c0 << 28);
+    lv.l1 = (uint32_t)n.link.y | (c1 << 28);
+    if (c0) h0 = false;
+    if (c1) h1 = false;
+    if (h0 && h1) {
+        const bool first1 = tn1 < tn0;
+        stack.store(t.sp, first1 ? n.link.x : n.link.y);
+        ++t.sp;
+        t.node = first1 ? n.link.y : n.link.x;
+    } else if (h0) {
+        t.node = n.link.x;
+    } else if (h1) {
+        t.node = n.link.y;
+    } else if (t.sp == 0) {
+        t.node = -1;
+    } else {
+        --t.sp;
+        t.node = stack.load(t.sp);
+    }
+    return (c0 | c1) != 0;
+}
+
+// The postponed leaf tests of one node visit (leaf 0's spheres, then leaf 1's).
+template <bool kCount>
+__device__ __forceinline__ void trav_leaves(const float4 *__restrict__ prims, const Leaves &lv, V3 o, V3 d,
+                                            const RayK &rk, Trav &t, Counters &cnt) {
+    test_prims2<kCount>(prims, (int)(lv.l0 & kLeafFirstMask), (int)(lv.l0 >> 28), (int)(lv.l1 & kLeafFirstMask),
+                        (int)(lv.l1 >> 28), o, d, rk.a, t.closest, t.hit_prim, cnt);
 }
 
 // Visits node t.node: tests both children, tests leaf spheres in place, descends into the
 // nearer internal child and pushes the farther one. Returns true when the traversal is done.
 template <bool kCount, typename Stack>
 __device__ __forceinline__ bool trav_step(const GNode *__restrict__ nodes, const float4 *__restrict__ prims,
-                                          Stack &stack, V3 o, V3 d, Trav &t, Counters &cnt) {
+                                          Stack &stack, V3 o, V3 d, const RayK &rk, Trav &t, Counters &cnt) {
     const GNode n = nodes[t.node];
     if (kCount) { cnt.nodes++; cnt.boxes += 2; }
     float tn0 = 0.0f, tn1 = 0.0f;
-    bool h0 = box_hit(n.b0.x, n.b0.y, n.b0.z, n.b0.w, n.b1.x, n.b1.y, t.inv, t.oi, 0.001f, t.closest, tn0);
-    bool h1 = box_hit(n.b1.z, n.b1.w, n.b2.x, n.b2.y, n.b2.z, n.b2.w, t.inv, t.oi, 0.001f, t.closest, tn1);
+    bool h0 = box_hit(n.b0.x, n.b0.y, n.b0.z, n.b0.w, n.b1.x, n.b1.y, rk.inv, rk.oi, 0.001f, t.closest, tn0);
+    bool h1 = box_hit(n.b1.z, n.b1.w, n.b2.x, n.b2.y, n.b2.z, n.b2.w, rk.inv, rk.oi, 0.001f, t.closest, tn1);
     // Leaf children: one loop over leaf 0's spheres then leaf 1's (one divergent loop, not two).
     const int c0 = (h0 && n.link.z > 0) ? n.link.z : 0;
     const int c1 = (h1 && n.link.w > 0) ? n.link.w : 0;
     if (c0 + c1 > 0) {
-        test_prims2<kCount>(prims, n.link.x, c0, n.link.y, c1, o, d, t.a, t.closest, t.hit_prim, cnt);
+        test_prims2<kCount>(prims, n.link.x, c0, n.link.y, c1, o, d, rk.a, t.closest, t.hit_prim, cnt);
         if (c0) h0 = false;
         if (c1) h1 = false;
     }
@@ -295,7 +384,7 @@ __device__ __forceinline__ bool trav_step(const GNode *__restrict__ nodes, const
 // into the nearest internal child and push the others farthest-first (5-exchange sort).
 template <bool kCount, typename Stack>
 __device__ __forceinline__ bool trav_step4(const GNode4 *__restrict__ nodes, const float4 *__restrict__ prims,
-                                           Stack &stack, V3 o, V3 d, Trav &t, Counters &cnt) {
+                                           Stack &stack, V3 o, V3 d, const RayK &rk, Trav &t, Counters &cnt) {
     const GNode4 n = nodes[t.node];
     if (kCount) { cnt.nodes++; cnt.boxes += 4; }
     const float lox[4] = {n.lox.x, n.lox.y, n.lox.z, n.lox.w}, hix[4] = {n.hix.x, n.hix.y, n.hix.z, n.hix.w};
@@ -308,14 +397,14 @@ __device__ __forceinline__ bool trav_step4(const GNode4 *__restrict__ nodes, con
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         float tn = 0.0f;
-        const bool h = box_hit(lox[c], hix[c], loy[c], hiy[c], loz[c], hiz[c], t.inv, t.oi, 0.001f, t.closest, tn);
+        const bool h = box_hit(lox[c], hix[c], loy[c], hiy[c], loz[c], hiz[c], rk.inv, rk.oi, 0.001f, t.closest, tn);
         key[c] = h ? tn : __builtin_inff();
         idx[c] = child[c];
     }
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         if (count[c] > 0) {
-            if (key[c] < __builtin_inff()) test_prims<kCount>(prims, child[c], count[c], o, d, t.a, t.closest, t.hit_prim, cnt);
+            if (key[c] < __builtin_inff()) test_prims<kCount>(prims, child[c], count[c], o, d, rk.a, t.closest, t.hit_prim, cnt);
             key[c] = __builtin_inff();
         }
     }
@@ -350,8 +439,12 @@ __device__ __forceinline__ bool trav_step4(const GNode4 *__restrict__ nodes, con
     return false;
 }
 
+// Radiance is only ever added when a path ends (sky/background or an emitter, camera.rs:
+// 182-209), so the path carries no running sum: the terminating contribution T*Le goes
+// straight into the pixel's sample sum. Bit-identical to L = 0 + T*Le; sum += L, since
+// the sum starts at +0 and therefore never becomes -0.
 struct PathState {
-    V3 o, d, T, L;
+    V3 o, d, T;
     uint64_t rng;
     uint32_t k;  // bounce index (camera ray = 0)
 };
@@ -381,8 +474,14 @@ __device__ __forceinline__ void camera_ray(const KParams &P, uint32_t x, uint32_
     ps.o = origin;
     ps.d = sub(sample, origin);
     ps.T = v3(1.0f, 1.0f, 1.0f);
-    ps.L = v3(0.0f, 0.0f, 0.0f);
     ps.k = 0;
+}
+
+// The path's RNG stream for sample s of global pixel (x, y): PCG32 state keyed by
+// splitmix64(splitmix64((seed << 32) ^ pixel) + s). Re-derived per sample (no per-pixel key held).
+__device__ __forceinline__ uint64_t path_rng(const KParams &P, uint32_t x, uint32_t y, uint32_t s) {
+    const uint64_t key = splitmix64(((uint64_t)P.seed << 32) ^ (uint64_t)(y * P.width + x));
+    return splitmix64(key + s);
 }
 
 __device__ __forceinline__ V3 texel(const KParams &P, int tex, float u, float v) {
@@ -400,8 +499,15 @@ __device__ __forceinline__ V3 texel(const KParams &P, int tex, float u, float v)
 }
 
 // After the closest-hit query of the current segment (prim < 0: miss): background, or
-// emission / scatter / RR (camera.rs:182-209). Returns true when the path has ended.
-__device__ __forceinline__ bool shade(const KParams &P, const float4 *prims, PathState &ps, float t, int prim) {
+// emission / scatter / RR (camera.rs:182-209). Returns true when the path has ended; a
+// path ending at the sky or an emitter adds T*Le to `sum`.
+template <typename C>
+__device__ __forceinline__ bool shade(const KParams &P, const float4 *prims, const GMaterial *mtl, PathState &ps,
+                                      float t, int prim, V3 &sum, C &cnt) {
+    if constexpr (RRT_PHASE_TIMING == 4) {
+        cnt.d0 += wave_slot();
+        cnt.d1 += 1;
+    }
     if (prim < 0) {
         V3 bg;
         if (P.bg_mode == 1u) {
@@ -411,7 +517,7 @@ __device__ __forceinline__ bool shade(const KParams &P, const float4 *prims, Pat
             const float a = 0.5f * (ud.y + 1.0f);
             bg = v3((1.0f - a) * 1.0f + a * 0.5f, (1.0f - a) * 1.0f + a * 0.7f, (1.0f - a) * 1.0f + a * 1.0f);
         }
-        ps.L = add(ps.L, mul(ps.T, bg));
+        sum = add(sum, mul(ps.T, bg));
         return true;
     }
     // HitRecord (sphere.rs:47-50, hittable.rs:20-32)
@@ -421,18 +527,18 @@ __device__ __forceinline__ bool shade(const KParams &P, const float4 *prims, Pat
     const V3 outward = v3((p.x - cr.x) * inv_r, (p.y - cr.y) * inv_r, (p.z - cr.z) * inv_r);
     const bool front = dot(ps.d, outward) < 0.0f;
     const V3 nrm = front ? outward : v3(-outward.x, -outward.y, -outward.z);
-    const GMaterial m = P.mats[P.prim_mat[prim]];
+    const GMaterial m = mtl[prim];
     const int kind = m.b.x;
     V3 att;
     V3 dir;
     if (kind == 4) {  // DiffuseLight: emitted, scatter None
-        ps.L = add(ps.L, mul(ps.T, v3(m.a.x, m.a.y, m.a.z)));
+        sum = add(sum, mul(ps.T, v3(m.a.x, m.a.y, m.a.z)));
         return true;
     }
     // Lambertian and Metal both draw one random_unit_vector and nothing else before RR: one
     // rejection loop for both kinds (a wave mixing them runs it once, not twice).
     V3 r = v3(0.0f, 0.0f, 0.0f);
-    if (kind != 2) r = random_unit_vector(ps.rng);
+    if (kind != 2) r = random_unit_vector(ps.rng, cnt);
     if (kind == 0 || kind == 3) {  // Lambertian (material.rs:28-40)
         dir = add(nrm, r);
         if (__builtin_fabsf(dir.x) < 1e-8f && __builtin_fabsf(dir.y) < 1e-8f && __builtin_fabsf(dir.z) < 1e-8f) dir = nrm;
@@ -491,17 +597,22 @@ __device__ __forceinline__ void render_body(const KParams &P) {
     using Node = typename std::conditional<kWide, GNode4, GNode>::type;
     const Node *nodes = reinterpret_cast<const Node *>(P.nodes);
     const float4 *prims = P.prim_cr;
+    const GMaterial *mtl = P.prim_mtl;
     if constexpr (kLds) {
-        // Stage the whole BVH + spheres (KB-sized) in LDS once per block.
+        // Stage the whole BVH + spheres + their materials (KB-sized) in LDS once per block.
         uint4 *dst = lds_dyn + (P.stack_depth * kBlock * sizeof(StackT) + 15u) / 16u;
         const uint4 *src_n = reinterpret_cast<const uint4 *>(P.nodes);
         const uint32_t nn = P.n_nodes * (uint32_t)(sizeof(Node) / 16);
         for (uint32_t i = threadIdx.x; i < nn; i += kBlock) dst[i] = src_n[i];
         const uint4 *src_p = reinterpret_cast<const uint4 *>(P.prim_cr);
         for (uint32_t i = threadIdx.x; i < P.n_prims; i += kBlock) dst[nn + i] = src_p[i];
+        const uint4 *src_m = reinterpret_cast<const uint4 *>(P.prim_mtl);
+        const uint32_t nm = P.n_prims * (uint32_t)(sizeof(GMaterial) / 16);
+        for (uint32_t i = threadIdx.x; i < nm; i += kBlock) dst[nn + P.n_prims + i] = src_m[i];
         __syncthreads();
         nodes = reinterpret_cast<const Node *>(dst);
         prims = reinterpret_cast<const float4 *>(dst + nn);
+        mtl = reinterpret_cast<const GMaterial *>(dst + nn + P.n_prims);
     }
     LdsStack<StackT> stack;
     stack.init(lds_stack, threadIdx.x);
@@ -512,18 +623,22 @@ __device__ __forceinline__ void render_body(const KParams &P) {
     // (and every refill) stay spatially coherent. Lanes whose unit is done claim new units
     // together: one atomic per refill, issued by the lowest idle lane.
     const uint32_t lane = threadIdx.x & 63u;
-    Counters cnt = {0, 0, 0, 0, 0};
+    Counters cnt = {0, 0, 0, 0, 0, 0};
+    uint32_t w_rays = 0, w_paths = 0;  // wave-uniform (scalar) ray / path counts
     bool has = false;     // lane owns a unit
     bool q_open = true;   // wave-uniform: the queue may still hold units
-    uint32_t x = 0, y = 0, ly = 0, chunk = 0, s = 0, s_hi = 0;
-    uint64_t key = 0;
+    // lane's unit: global pixel (x | y << 16), next sample s, end of its sample chunk s_hi
+    uint32_t xy = 0, s = 0, s_hi = 0;
     V3 sum = v3(0.0f, 0.0f, 0.0f);
     PathState ps;
     Trav tr;
     bool need_ray = false;  // the lane must start the next segment of its path
     bool tracing = false;
     uint32_t pool_base = 0, pool_left = 0;  // wave-uniform: claimed, not yet assigned units
+    [[maybe_unused]] uint64_t ph0 = 0, ph1 = 0, ph2 = 0, tp = 0;
     for (;;) {
+        if constexpr (RRT_PHASE_TIMING == 1) tp = __builtin_amdgcn_s_memtime();
+        if constexpr (RRT_PHASE_TIMING == 2) ph2++;
         uint64_t idle = __ballot(!has);
         if (idle != 0 && pool_left == 0 && q_open) {
             // one atomic claims a whole tile-chunk (64 units) for this wave
@@ -546,18 +661,18 @@ __device__ __forceinline__ void render_body(const KParams &P) {
                     const uint32_t lit = u & 63u;
                     const uint32_t tc = u >> 6;
                     const uint32_t t = tc / P.n_chunks;
-                    chunk = tc - t * P.n_chunks;
-                    x = (t % P.tiles_x) * 8u + (lit & 7u);
-                    ly = (t / P.tiles_x) * 8u + (lit >> 3);
+                    const uint32_t chunk = tc - t * P.n_chunks;
+                    const uint32_t x = (t % P.tiles_x) * 8u + (lit & 7u);
+                    const uint32_t ly = (t / P.tiles_x) * 8u + (lit >> 3);
                     if (x < P.width && ly < P.tile_rows) {
                         // tile-local row -> global image row (row bands dealt round-robin over ranks)
                         const uint32_t band = ly / P.band_rows;
-                        y = (band * P.n_ranks + P.rank) * P.band_rows + ly % P.band_rows;
-                        key = splitmix64(((uint64_t)P.seed << 32) ^ (uint64_t)(y * P.width + x));
+                        const uint32_t y = (band * P.n_ranks + P.rank) * P.band_rows + ly % P.band_rows;
+                        xy = x | (y << 16);
                         s = P.sample_begin + chunk * P.chunk;
                         s_hi = min(s + P.chunk, P.sample_end);
                         sum = v3(0.0f, 0.0f, 0.0f);
-                        ps.rng = splitmix64(key + s);
+                        ps.rng = path_rng(P, x, y, s);
                         camera_ray(P, x, y, ps);
                         need_ray = true;
                         has = true;
@@ -570,41 +685,89 @@ __device__ __forceinline__ void render_body(const KParams &P) {
         if (__ballot(has) == 0) break;
 
         bool seg_done = false;  // the lane's path ended without a query (depth limit)
+        bool started = false;   // the lane starts a closest-hit query this iteration
         if (has && need_ray) {
             if (ps.k >= P.max_depth) {  // ray_color: depth <= 0 -> 0 (no query)
                 seg_done = true;
             } else {
-                trav_begin(tr, ps.o, ps.d);
-                cnt.rays++;
+                trav_begin(tr);
                 need_ray = false;
                 tracing = true;
+                started = true;
             }
         }
+        w_rays += (uint32_t)__popcll(__ballot(started));
         // Traverse until too few lanes of the wave are still in the tree, then let the
         // finished lanes shade and fetch their next segment (wave-uniform ballot exit).
         const uint32_t live = (uint32_t)__popcll(__ballot(has));
         const uint32_t min_active = (live * P.trav_frac) >> 8;
-        for (;;) {
-            if (tracing) {
-                bool fin;
-                if constexpr (kWide) fin = trav_step4<kCount>(nodes, prims, stack, ps.o, ps.d, tr, cnt);
-                else fin = trav_step<kCount>(nodes, prims, stack, ps.o, ps.d, tr, cnt);
-                if (fin) tracing = false;
+        if constexpr (RRT_PHASE_TIMING == 1) {
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            ph0 += t - tp;
+            tp = t;
+        }
+        RayK rk;
+        if (tracing) rk = ray_consts(ps.o, ps.d);
+        if constexpr (kWide) {
+            for (;;) {
+                if constexpr (RRT_PHASE_TIMING == 2) {
+                    ph0 += 64;
+                    ph1 += (uint64_t)__popcll(__ballot(tracing));
+                }
+                if (tracing) {
+                    if (trav_step4<kCount>(nodes, prims, stack, ps.o, ps.d, rk, tr, cnt)) tracing = false;
+                }
+                if ((uint32_t)__popcll(__ballot(tracing)) <= min_active) break;
             }
-            if ((uint32_t)__popcll(__ballot(tracing)) <= min_active) break;
+        } else {
+            // BVH2 with postponed leaves: a lane whose visit hit leaf children waits (no further
+            // node visits) until the wave runs its leaf loop, which happens once more than
+            // leaf_min lanes wait, or no lane can take another node step, or before leaving.
+            const uint32_t leaf_min = (live * P.leaf_frac) >> 8;
+            bool pend = false;
+            Leaves lv;
+            for (;;) {
+                if constexpr (RRT_PHASE_TIMING == 2) {
+                    ph0 += 64;
+                    ph1 += (uint64_t)__popcll(__ballot(tracing && !pend));
+                }
+                if (tracing && !pend) {
+                    pend = trav_node<kCount>(nodes, stack, rk, tr, lv, cnt);
+                    if (!pend && tr.node < 0) tracing = false;
+                }
+                const uint64_t pm = __ballot(pend);
+                const bool leave = (uint32_t)__popcll(__ballot(tracing)) <= min_active;
+                if (pm != 0 && (leave || (uint32_t)__popcll(pm) > leaf_min || __ballot(tracing && !pend) == 0)) {
+                    if (pend) {
+                        trav_leaves<kCount>(prims, lv, ps.o, ps.d, rk, tr, cnt);
+                        pend = false;
+                        if (tr.node < 0) tracing = false;
+                    }
+                }
+                if (leave) break;
+            }
+        }
+        if constexpr (RRT_PHASE_TIMING == 1) {
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            ph1 += t - tp;
+            tp = t;
         }
         if (has && !need_ray && !tracing) {
             need_ray = true;
-            seg_done = shade(P, prims, ps, tr.closest, tr.hit_prim);
+            seg_done = shade(P, prims, mtl, ps, tr.closest, tr.hit_prim, sum, cnt);
         }
-        if (seg_done) {
-            sum = add(sum, ps.L);  // pixel_color += ray_color(..) (camera.rs:73-76)
-            cnt.paths++;
+        w_paths += (uint32_t)__popcll(__ballot(seg_done));
+        if (seg_done) {  // pixel_color += ray_color(..) (camera.rs:73-76): already in `sum`
             ++s;
+            const uint32_t x = xy & 0xffffu, y = xy >> 16;
             if (s < s_hi) {
-                ps.rng = splitmix64(key + s);
+                ps.rng = path_rng(P, x, y, s);
                 camera_ray(P, x, y, ps);
             } else {  // unit complete: the chunk's sum, in sample order
+                // chunk index and tile-local row, re-derived from (y, s_hi) once per unit
+                const uint32_t chunk = (s_hi - 1u - P.sample_begin) / P.chunk;
+                const uint32_t gb = y / P.band_rows;
+                const uint32_t ly = ((gb - P.rank) / P.n_ranks) * P.band_rows + (y - gb * P.band_rows);
                 const size_t px = (size_t)ly * P.width + x;
                 const float4 out = make_float4(sum.x, sum.y, sum.z, (float)(s_hi - (P.sample_begin + chunk * P.chunk)));
                 if (P.n_chunks == 1) P.accum[px] = out;
@@ -612,10 +775,23 @@ __device__ __forceinline__ void render_body(const KParams &P) {
                 has = false;
             }
         }
+        if constexpr (RRT_PHASE_TIMING == 1) ph2 += __builtin_amdgcn_s_memtime() - tp;
+    }
+    if constexpr (RRT_PHASE_TIMING >= 3 && !kCount) {
+        ph0 = wave_sum_u32(cnt.d0);
+        ph1 = wave_sum_u32(cnt.d1);
+        ph2 = wave_sum_u32(cnt.d2);
+    }
+    if constexpr (RRT_PHASE_TIMING != 0 && !kCount) {
+        if (lane == 0) {
+            atomicAdd(&P.counters[2], (unsigned long long)ph0);
+            atomicAdd(&P.counters[3], (unsigned long long)ph1);
+            atomicAdd(&P.counters[4], (unsigned long long)ph2);
+        }
     }
     // one atomic per wave per counter
-    const uint32_t r = wave_sum_u32(cnt.rays);
-    const uint32_t pa = wave_sum_u32(cnt.paths);
+    const uint32_t r = w_rays;
+    const uint32_t pa = w_paths;
     uint32_t nv = 0, bt = 0, st = 0;
     if (kCount) {
         nv = wave_sum_u32(cnt.nodes);
@@ -658,7 +834,7 @@ template <bool kLds, typename StackT, bool kWide, int kWaves = 1>
 hipError_t launch_variant(const KParams &p, bool count, hipStream_t stream) {
     if (p.n_units == 0) return hipSuccess;
     size_t lds = ((size_t)p.stack_depth * kBlock * sizeof(StackT) + 15u) / 16u * 16u;
-    if (kLds) lds += (size_t)p.n_nodes * (kWide ? sizeof(GNode4) : sizeof(GNode)) + (size_t)p.n_prims * sizeof(float4);
+    if (kLds) lds += (size_t)p.n_nodes * (kWide ? sizeof(GNode4) : sizeof(GNode)) + (size_t)p.n_prims * kPrimBytes;
     auto kernel = count ? rrt_render<kLds, true, StackT, kWide, kWaves> : rrt_render<kLds, false, StackT, kWide, kWaves>;
     // Persistent grid: as many blocks as can be resident (occupancy at this LDS size), capped
     // by the work; the queue counter is zeroed on the stream before the launch.
@@ -689,10 +865,6 @@ hipError_t launch_width(const KParams &p, bool count, hipStream_t stream) {
 }
 
 }  // namespace
-
-size_t lds_scene_bytes(const KParams &p) {
-    return (size_t)p.n_nodes * sizeof(GNode) + (size_t)p.n_prims * sizeof(float4);
-}
 
 hipError_t launch_render_kernel(const KParams &p, bool count, hipStream_t stream) {
     // Variant choice: BVH width, smallest LDS stack that holds the traversal, and the scene
