@@ -43,6 +43,7 @@ def parse():
     ap.add_argument("--spp", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-breakdown", action="store_true", help="skip the wall-clock split (one extra frame)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_C2.json"),
                     help="per-launch HBM bytes from rocprofv3 PMC passes (written by tools/pmc_traffic.py)")
     return ap.parse_args()
@@ -73,6 +74,42 @@ def cpu_baseline(scene, budget_s):
         "sample": f"{scene.width}x{scene.height} C2 frame at {spp_done} of {scene.spp} spp "
                   f"(f64 books restatement, {threads} threads, {rays} rays in {secs:.2f} s; "
                   f"extrapolated full-frame wall-clock {secs * scene.spp / spp_done:.1f} s)",
+    }
+
+
+def wall_clock_breakdown(scene, accum, kernel_ms):
+    """SURVEY 8(d) split of one C2 frame through the library, measured outside the timed
+    region on rank 0: host BVH build, scene creation (BVH build + H2D upload), kernel (the
+    timed loop's average), D2H of the float accum, P3 formatting (render_io.rs), and the
+    end-to-end drop-in call rrt_hip_render (scene + kernel + D2H) plus the P3 write
+    (render_io::write_ppm_from_accum to /dev/null)."""
+    import torch
+
+    import rustraytrace_amd as rrt
+
+    def timed(fn):
+        t = time.perf_counter()
+        out = fn()
+        return out, (time.perf_counter() - t) * 1e3
+
+    from rustraytrace_amd.render import build_bvh
+
+    _, bvh_ms = timed(lambda: build_bvh(scene))
+    ds, create_ms = timed(lambda: rrt.DeviceScene(scene))
+    ds.close()
+    torch.cuda.synchronize()
+    host, d2h_ms = timed(lambda: accum.cpu())
+    _, fmt_ms = timed(lambda: rrt.write_ppm_from_accum(scene.width, scene.height, host.numpy(), scene.spp, os.devnull))
+    e2e_accum, render_ms = timed(lambda: rrt.render(scene, n_gpus=1))
+    _, fmt2_ms = timed(lambda: rrt.write_ppm_from_accum(scene.width, scene.height, e2e_accum, scene.spp, os.devnull))
+    return {
+        "bvh_build_ms": round(bvh_ms, 3),
+        "scene_create_ms": round(create_ms, 3),
+        "kernel_ms": round(kernel_ms, 3),
+        "d2h_ms": round(d2h_ms, 3),
+        "ppm_write_ms": round(fmt_ms, 3),
+        "end_to_end_ms": round(render_ms + fmt2_ms, 3),
+        "end_to_end_note": "rrt_hip_render (BVH build, H2D, kernel, D2H, 1 GPU) + P3 write of the frame",
     }
 
 
@@ -136,6 +173,14 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kernel_ms = [a.elapsed_time(b) for a, b in zip(k_start, k_end)]
+    gather_ms = None
+    if world > 1:  # the exchange step alone, untimed loop: partial accums -> rank 0
+        dist.barrier()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        gather_sample_ranges(accum, dist, out=total)
+        torch.cuda.synchronize()
+        gather_ms = (time.perf_counter() - t) * 1e3
     ctr = ds.counters()
     rays = ctr["rays"]
     if world > 1:
@@ -214,6 +259,10 @@ def main():
                         "(SURVEY 8d's 78.6 assumed 16-lane SIMDs)",
             },
         }
+        if world == 1 and not args.no_breakdown:
+            out["wall_clock_breakdown"] = wall_clock_breakdown(scene, accum, avg_kernel_s * 1e3)
+        if gather_ms is not None:
+            out["gather_ms"] = round(gather_ms, 3)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(scene, args.cpu_seconds)
         print(json.dumps(out), flush=True)
