@@ -236,6 +236,35 @@ int32_t rrt_format_ppm_from_accum(uint32_t width, uint32_t height, const float *
 int32_t rrt_quantize_accum(uint32_t width, uint32_t height, const float *accum,
                            uint32_t samples_per_pixel, uint8_t *rgb8);
 
+/* ---- output step after the boundary: device quantiser, P6 ---------------
+ * render_io.rs writes P3 ASCII (~25 MB at 1080p) from a float accum copied to the host
+ * (16 B/pixel). These entries quantise on the device (3 B/pixel over PCIe) and format P3 or
+ * binary P6 from the quantised bytes. */
+
+/* rrt_hip_render, then the render_io quantiser on each device: rgb8_out[3*W*H] holds the
+ * bytes render_io::write_ppm_from_accum would print for the float accum (identical to
+ * rrt_quantize_accum of rrt_hip_render's accum_out with samples_per_pixel = total_spp). */
+int32_t rrt_hip_render_rgb8(const RrtCamera *cam,
+                            const RrtSphere *spheres, uint32_t n_spheres,
+                            const RrtMaterial *materials, uint32_t n_materials,
+                            const RrtTexture *textures, uint32_t n_textures,
+                            uint32_t total_spp, uint32_t n_gpus, uint32_t flags,
+                            uint8_t *rgb8_out);
+
+/* Enqueue the render_io quantiser on `stream` (hipStream_t, NULL = default): d_accum =
+ * n_pixels float4 (RGB sums; w ignored), d_rgb8 = n_pixels*3 bytes, scale 1/samples_per_pixel
+ * in f32 as render_io.rs:10 computes it. Asynchronous; byte-identical to rrt_quantize_accum. */
+int32_t rrt_quantize_accum_async(uint32_t n_pixels, const float *d_accum, uint32_t samples_per_pixel,
+                                 uint8_t *d_rgb8, void *stream);
+
+/* PNM from quantised pixels: binary = 0 -> P3 text byte-identical to
+ * rrt_format_ppm_from_accum of the same image; binary = 1 -> P6 ("P6\nW H\n255\n" + rgb8).
+ * *written = bytes needed (call with cap 0 to size). */
+int32_t rrt_format_pnm_from_rgb8(uint32_t width, uint32_t height, const uint8_t *rgb8, int32_t binary,
+                                 char *buf, size_t cap, size_t *written);
+int32_t rrt_write_pnm_from_rgb8(uint32_t width, uint32_t height, const uint8_t *rgb8, int32_t binary,
+                                const char *path);
+
 /* Number of visible HIP devices (0 when no GPU). */
 int32_t rrt_device_count(int32_t *count);
 

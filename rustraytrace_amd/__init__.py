@@ -9,10 +9,14 @@ from ._lib import RrtError, load
 from .render import (
     DeviceScene,
     device_count,
+    format_pnm_from_rgb8,
     format_ppm_from_accum,
     quantize_accum,
+    quantize_accum_async,
     render,
     render_in_one_weekend,
+    render_rgb8,
+    write_pnm_from_rgb8,
     write_ppm_from_accum,
 )
 from .scenes import (
@@ -29,6 +33,7 @@ from .scenes import (
 
 __all__ = [
     "_lib", "RrtError", "load", "DeviceScene", "device_count", "format_ppm_from_accum", "quantize_accum", "render",
-    "render_in_one_weekend", "write_ppm_from_accum", "CONFIGS", "SceneData", "build_in_one_weekend_scene",
+    "render_in_one_weekend", "write_ppm_from_accum", "render_rgb8", "quantize_accum_async", "format_pnm_from_rgb8",
+    "write_pnm_from_rgb8", "CONFIGS", "SceneData", "build_in_one_weekend_scene",
     "config_scene", "earth_light", "earth_texture", "make_camera", "rtow", "three_spheres",
 ]

@@ -32,7 +32,9 @@ static void usage() {
                  "Usage: rrt [--backend hip|cuda|gpu] <book> [scene] [--image_width N] [--samples_per_pixel N]\n"
                  "           [--max_depth N] [--aspect_ratio X] [--vfov X] [--lookfrom x,y,z] [--lookat x,y,z]\n"
                  "           [--vup x,y,z] [--defocus_angle X] [--focus_dist X] [--background r,g,b]\n"
-                 "           [--gpus N] [--seed S] [--grid_half G] [-o out.ppm]\n"
+                 "           [--gpus N] [--seed S] [--grid_half G] [--p6] [--host-quantise] [-o out.ppm]\n"
+                 "  --p6             binary P6 instead of render_io.rs's P3 text\n"
+                 "  --host-quantise  copy the float accum and quantise on the host (same bytes)\n"
                  "books: in_one_weekend\n");
 }
 
@@ -51,6 +53,7 @@ int main(int argc, char **argv) {
     uint64_t seed = 0x5EED1234ull;
     int grid_half = 11;
     std::string out = "-";
+    bool p6 = false, host_quantise = false;
 
     for (int i = 1; i < argc; ++i) {
         std::string a = argv[i];
@@ -80,6 +83,8 @@ int main(int argc, char **argv) {
         else if (a == "--seed") seed = std::strtoull(next("--seed"), nullptr, 0);
         else if (a == "--grid_half") grid_half = std::atoi(next("--grid_half"));
         else if (a == "-o") out = next("-o");
+        else if (a == "--p6") p6 = true;
+        else if (a == "--host-quantise") host_quantise = true;
         else if (a == "-h" || a == "--help") { usage(); return 0; }
         else positional.push_back(a);
     }
@@ -117,15 +122,26 @@ int main(int argc, char **argv) {
     }
     const uint32_t w = (uint32_t)cam.params_f[1], h = (uint32_t)cam.params_f[2];
     const uint32_t spp = (uint32_t)(cam.params_f[3] < 1.0f ? 1.0f : cam.params_f[3]);
-    std::vector<float> accum((size_t)w * h * 4);
     const auto t0 = std::chrono::steady_clock::now();
-    if (rrt_hip_render(&cam, spheres.data(), n, materials.data(), n, nullptr, 0, spp, gpus, 0, accum.data())) {
+    std::vector<float> accum;
+    std::vector<uint8_t> rgb8;
+    int rc;
+    if (host_quantise && !p6) {  // the reference's path: float accum -> render_io P3 on the host
+        accum.resize((size_t)w * h * 4);
+        rc = rrt_hip_render(&cam, spheres.data(), n, materials.data(), n, nullptr, 0, spp, gpus, 0, accum.data());
+    } else {  // render_io quantiser on the device (identical bytes), 3 B/pixel to the host
+        rgb8.resize((size_t)w * h * 3);
+        rc = rrt_hip_render_rgb8(&cam, spheres.data(), n, materials.data(), n, nullptr, 0, spp, gpus, 0, rgb8.data());
+    }
+    if (rc) {
         std::fprintf(stderr, "HIP render failed: %s\n", rrt_hip_last_error());  // main.rs:60-65
         return 1;
     }
     const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     std::fprintf(stderr, "rendered %ux%u @ %u spp, %u spheres, %u GPU(s) in %.3f s\n", w, h, spp, n, gpus, secs);
-    if (rrt_write_ppm_from_accum(w, h, accum.data(), spp, out.c_str())) {
+    rc = accum.empty() ? rrt_write_pnm_from_rgb8(w, h, rgb8.data(), p6 ? 1 : 0, out.c_str())
+                       : rrt_write_ppm_from_accum(w, h, accum.data(), spp, out.c_str());
+    if (rc) {
         std::fprintf(stderr, "HIP render failed: %s\n", rrt_hip_last_error());
         return 1;
     }

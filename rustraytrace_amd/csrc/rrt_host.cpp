@@ -17,6 +17,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -854,11 +855,15 @@ int32_t rrt_scene_count_work(RrtScene *scene, const RrtTile *tile, RrtCounters *
 }
 
 // ---- one-shot drop-in (cuda/mod.rs:342-439) ---------------------------------------------
-int32_t rrt_hip_render(const RrtCamera *cam, const RrtSphere *spheres, uint32_t n_spheres,
-                       const RrtMaterial *materials, uint32_t n_materials, const RrtTexture *textures,
-                       uint32_t n_textures, uint32_t total_spp, uint32_t n_gpus, uint32_t flags,
-                       float *accum_out) {
-    if (!cam || !accum_out) return fail(RRT_E_INVALID, "null camera or accum_out");
+}  // extern "C"
+
+// One-shot frame on n_gpus devices: float accum rows (accum_out) or render_io-quantised rows
+// (rgb8_out, quantised on the device) assembled into the caller's image.
+static int32_t render_frame(const RrtCamera *cam, const RrtSphere *spheres, uint32_t n_spheres,
+                            const RrtMaterial *materials, uint32_t n_materials, const RrtTexture *textures,
+                            uint32_t n_textures, uint32_t total_spp, uint32_t n_gpus, uint32_t flags,
+                            float *accum_out, uint8_t *rgb8_out) {
+    if (!cam || (!accum_out && !rgb8_out)) return fail(RRT_E_INVALID, "null camera or output buffer");
     if (total_spp == 0) total_spp = (uint32_t)std::max(cam->params_f[3], 1.0f);  // cuda/mod.rs:384
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(RRT_E_NODEV, "no HIP device available");
@@ -886,30 +891,47 @@ int32_t rrt_hip_render(const RrtCamera *cam, const RrtSphere *spheres, uint32_t 
         if (rc) return set_err(rc);
         const RrtTile tile{16u, g, n_gpus, 0u, total_spp};
         const uint32_t rows = tile_rows_of(height, tile);
+        const size_t n_px = (size_t)rows * width;
+        const size_t row_bytes = rgb8_out ? (size_t)width * 3 : (size_t)width * 16;
         float *d_accum = nullptr;
-        std::vector<float> host((size_t)rows * width * 4);
-        hipError_t e = hipMalloc((void **)&d_accum, std::max<size_t>(host.size(), 4) * sizeof(float));
+        uint8_t *d_rgb8 = nullptr;
+        std::vector<uint8_t> host(n_px * (rgb8_out ? 3 : 16));
+        hipError_t e = hipMalloc((void **)&d_accum, std::max<size_t>(n_px, 1) * 16);
+        if (e == hipSuccess && rgb8_out) e = hipMalloc((void **)&d_rgb8, std::max<size_t>(n_px, 1) * 3);
         if (e != hipSuccess) {
+            (void)hipFree(d_accum);
             rrt_scene_destroy(scene);
-            g_err = std::string("hipMalloc accum failed: ") + hipGetErrorString(e);
+            g_err = std::string("hipMalloc output failed: ") + hipGetErrorString(e);
             return set_err(RRT_E_NOMEM);
         }
         rc = rrt_render_tile_async(scene, &tile, d_accum, nullptr);
+        if (!rc && rgb8_out) {
+            const float scale = 1.0f / (float)total_spp;  // render_io.rs:10
+            e = rrt::launch_quantize(d_accum, d_rgb8, (uint32_t)n_px, scale, nullptr);
+            if (e != hipSuccess) {
+                g_err = std::string("quantise launch failed: ") + hipGetErrorString(e);
+                rc = RRT_E_HIP;
+            }
+        }
         if (!rc) {
             e = hipDeviceSynchronize();
-            if (e == hipSuccess) e = hipMemcpy(host.data(), d_accum, host.size() * sizeof(float), hipMemcpyDeviceToHost);
+            if (e == hipSuccess)
+                e = hipMemcpy(host.data(), rgb8_out ? (const void *)d_rgb8 : (const void *)d_accum, host.size(),
+                              hipMemcpyDeviceToHost);
             if (e != hipSuccess) {
                 g_err = std::string("render failed: ") + hipGetErrorString(e);
                 rc = RRT_E_HIP;
             }
         }
         (void)hipFree(d_accum);
+        (void)hipFree(d_rgb8);
         rrt_scene_destroy(scene);
         if (rc) return set_err(rc);
+        uint8_t *dst = rgb8_out ? rgb8_out : reinterpret_cast<uint8_t *>(accum_out);
         for (uint32_t lr = 0; lr < rows; ++lr) {
             const uint32_t band = lr / tile.band_rows;
             const uint32_t y = (band * tile.n_ranks + tile.rank) * tile.band_rows + lr % tile.band_rows;
-            std::memcpy(accum_out + (size_t)y * width * 4, host.data() + (size_t)lr * width * 4, (size_t)width * 16);
+            std::memcpy(dst + (size_t)y * row_bytes, host.data() + (size_t)lr * row_bytes, row_bytes);
         }
         const uint32_t d = ++done;
         if (!(flags & RRT_FLAG_QUIET)) {
@@ -926,6 +948,35 @@ int32_t rrt_hip_render(const RrtCamera *cam, const RrtSphere *spheres, uint32_t 
         for (auto &t : th) t.join();
     }
     if (first_rc) return fail(first_rc, first_err);
+    return RRT_OK;
+}
+
+extern "C" {
+
+int32_t rrt_hip_render(const RrtCamera *cam, const RrtSphere *spheres, uint32_t n_spheres,
+                       const RrtMaterial *materials, uint32_t n_materials, const RrtTexture *textures,
+                       uint32_t n_textures, uint32_t total_spp, uint32_t n_gpus, uint32_t flags,
+                       float *accum_out) {
+    if (!accum_out) return fail(RRT_E_INVALID, "null camera or accum_out");
+    return render_frame(cam, spheres, n_spheres, materials, n_materials, textures, n_textures, total_spp, n_gpus,
+                        flags, accum_out, nullptr);
+}
+
+int32_t rrt_hip_render_rgb8(const RrtCamera *cam, const RrtSphere *spheres, uint32_t n_spheres,
+                            const RrtMaterial *materials, uint32_t n_materials, const RrtTexture *textures,
+                            uint32_t n_textures, uint32_t total_spp, uint32_t n_gpus, uint32_t flags,
+                            uint8_t *rgb8_out) {
+    if (!rgb8_out) return fail(RRT_E_INVALID, "null camera or rgb8_out");
+    return render_frame(cam, spheres, n_spheres, materials, n_materials, textures, n_textures, total_spp, n_gpus,
+                        flags, nullptr, rgb8_out);
+}
+
+int32_t rrt_quantize_accum_async(uint32_t n_pixels, const float *d_accum, uint32_t samples_per_pixel, uint8_t *d_rgb8,
+                                 void *stream) {
+    if (n_pixels && (!d_accum || !d_rgb8)) return fail(RRT_E_INVALID, "null d_accum or d_rgb8");
+    const float scale = samples_per_pixel > 0 ? 1.0f / (float)samples_per_pixel : 0.0f;
+    const hipError_t e = rrt::launch_quantize(d_accum, d_rgb8, n_pixels, scale, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(RRT_E_HIP, std::string("quantise launch failed: ") + hipGetErrorString(e));
     return RRT_OK;
 }
 
@@ -1087,12 +1138,119 @@ static inline uint8_t quantize_channel(float x, float scale) {
     return (uint8_t)(int)(r * 256.0f);
 }
 
+}  // extern "C"
+
+// Host threads for the output step: RRT_HOST_THREADS, else OMP_NUM_THREADS, else the
+// hardware count; at most 16 (the GPU box's CPU share per GPU).
+static unsigned host_threads() {
+    const char *e = std::getenv("RRT_HOST_THREADS");
+    if (!e) e = std::getenv("OMP_NUM_THREADS");
+    unsigned n = e ? (unsigned)std::max(1, std::atoi(e)) : std::max(1u, std::thread::hardware_concurrency());
+    return std::min(n, 16u);
+}
+
+// fn(begin, end) over [0, n) in contiguous chunks, one per host thread (inline when small).
+static void parallel_chunks(size_t n, size_t min_chunk, const std::function<void(size_t, size_t, unsigned)> &fn,
+                            unsigned *n_chunks_out = nullptr) {
+    const unsigned t = (unsigned)std::max<size_t>(1, std::min<size_t>(host_threads(), n / std::max<size_t>(min_chunk, 1)));
+    if (n_chunks_out) *n_chunks_out = t;
+    if (t <= 1) {
+        fn(0, n, 0);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (unsigned i = 0; i < t; ++i) th.emplace_back(fn, n * i / t, n * (i + 1) / t, i);
+    for (auto &x : th) x.join();
+}
+
+static void quantize_rgb8(size_t n_px, const float *accum, uint32_t spp, uint8_t *rgb8) {
+    const float scale = spp > 0 ? 1.0f / (float)spp : 0.0f;
+    parallel_chunks(n_px, 1u << 16, [&](size_t b, size_t e, unsigned) {
+        for (size_t i = b; i < e; ++i)
+            for (int c = 0; c < 3; ++c) rgb8[i * 3 + c] = quantize_channel(accum[i * 4 + c], scale);
+    });
+}
+
+// Decimal strings of 0..255 (no leading zeros) for the P3 "r g b\n" lines.
+struct DecTable {
+    char s[256][4];
+    uint8_t n[256];
+    DecTable() {
+        for (int v = 0; v < 256; ++v) n[v] = (uint8_t)std::snprintf(s[v], sizeof(s[v]), "%d", v);
+    }
+};
+static const DecTable &dec_table() {
+    static const DecTable t;
+    return t;
+}
+
+// P3 / P6 bytes of an rgb8 image. P3 lines are "%u %u %u\n" per pixel (render_io.rs:27),
+// formatted in parallel chunks at offsets from a prefix sum of the chunks' lengths.
+static std::vector<char> format_pnm(uint32_t width, uint32_t height, const uint8_t *rgb8, bool binary) {
+    const std::string head =
+        std::string(binary ? "P6\n" : "P3\n") + std::to_string(width) + " " + std::to_string(height) + "\n255\n";
+    const size_t n_px = (size_t)width * height;
+    std::vector<char> out;
+    if (binary) {
+        out.resize(head.size() + n_px * 3);
+        std::memcpy(out.data(), head.data(), head.size());
+        if (n_px) std::memcpy(out.data() + head.size(), rgb8, n_px * 3);
+        return out;
+    }
+    const DecTable &T = dec_table();
+    std::vector<size_t> len(host_threads() + 1, 0);
+    unsigned chunks = 1;
+    parallel_chunks(
+        n_px, 1u << 16,
+        [&](size_t b, size_t e, unsigned i) {
+            size_t l = 0;
+            for (size_t p = b; p < e; ++p) l += (size_t)T.n[rgb8[3 * p]] + T.n[rgb8[3 * p + 1]] + T.n[rgb8[3 * p + 2]] + 3;
+            len[i + 1] = l;
+        },
+        &chunks);
+    for (unsigned i = 0; i < chunks; ++i) len[i + 1] += len[i];
+    out.resize(head.size() + len[chunks]);
+    std::memcpy(out.data(), head.data(), head.size());
+    parallel_chunks(n_px, 1u << 16, [&](size_t b, size_t e, unsigned i) {
+        char *d = out.data() + head.size() + len[i];
+        for (size_t p = b; p < e; ++p) {
+            for (int c = 0; c < 3; ++c) {
+                const uint8_t v = rgb8[3 * p + c];
+                const char *sv = T.s[v];
+                d[0] = sv[0];  // exactly the digits: chunks are written concurrently, no overrun
+                if (T.n[v] > 1) d[1] = sv[1];
+                if (T.n[v] > 2) d[2] = sv[2];
+                d += T.n[v];
+                *d++ = c < 2 ? ' ' : '\n';
+            }
+        }
+    });
+    return out;
+}
+
+static int32_t write_bytes(const std::vector<char> &buf, const char *path) {
+    FILE *f = (!path || std::strcmp(path, "-") == 0) ? stdout : std::fopen(path, "wb");
+    if (!f) return fail(RRT_E_IO, std::string("cannot open ") + path);
+    const size_t w = std::fwrite(buf.data(), 1, buf.size(), f);
+    if (f == stdout) std::fflush(f);
+    else std::fclose(f);
+    if (w != buf.size()) return fail(RRT_E_IO, "short write");
+    return RRT_OK;
+}
+
+static int32_t copy_out(const std::vector<char> &bytes, char *buf, size_t cap, size_t *written) {
+    *written = bytes.size();
+    if (cap == 0) return RRT_OK;
+    if (!buf || cap < bytes.size()) return fail(RRT_E_INVALID, "buffer too small");
+    std::memcpy(buf, bytes.data(), bytes.size());
+    return RRT_OK;
+}
+
+extern "C" {
+
 int32_t rrt_quantize_accum(uint32_t width, uint32_t height, const float *accum, uint32_t spp, uint8_t *rgb8) {
     if ((!accum || !rgb8) && (size_t)width * height) return fail(RRT_E_INVALID, "null accum or rgb8");
-    const float scale = spp > 0 ? 1.0f / (float)spp : 0.0f;
-    const size_t n = (size_t)width * height;
-    for (size_t i = 0; i < n; ++i)
-        for (int c = 0; c < 3; ++c) rgb8[i * 3 + c] = quantize_channel(accum[i * 4 + c], scale);
+    quantize_rgb8((size_t)width * height, accum, spp, rgb8);
     return RRT_OK;
 }
 
@@ -1100,35 +1258,28 @@ int32_t rrt_format_ppm_from_accum(uint32_t width, uint32_t height, const float *
                                   size_t cap, size_t *written) {
     if (!written) return fail(RRT_E_INVALID, "null written");
     if (!accum && (size_t)width * height) return fail(RRT_E_INVALID, "null accum");
-    std::string out;
-    out.reserve((size_t)width * height * 12 + 32);
-    out += "P3\n" + std::to_string(width) + " " + std::to_string(height) + "\n255\n";
-    const float scale = spp > 0 ? 1.0f / (float)spp : 0.0f;
-    char line[16];
-    for (size_t i = 0, n = (size_t)width * height; i < n; ++i) {
-        const int len = std::snprintf(line, sizeof(line), "%u %u %u\n", quantize_channel(accum[i * 4], scale),
-                                      quantize_channel(accum[i * 4 + 1], scale), quantize_channel(accum[i * 4 + 2], scale));
-        out.append(line, (size_t)len);
-    }
-    *written = out.size();
-    if (cap == 0) return RRT_OK;
-    if (!buf || cap < out.size()) return fail(RRT_E_INVALID, "buffer too small");
-    std::memcpy(buf, out.data(), out.size());
-    return RRT_OK;
+    std::vector<uint8_t> rgb8((size_t)width * height * 3);
+    quantize_rgb8((size_t)width * height, accum, spp, rgb8.data());
+    return copy_out(format_pnm(width, height, rgb8.data(), false), buf, cap, written);
 }
 
 int32_t rrt_write_ppm_from_accum(uint32_t width, uint32_t height, const float *accum, uint32_t spp, const char *path) {
-    size_t n = 0;
-    if (int rc = rrt_format_ppm_from_accum(width, height, accum, spp, nullptr, 0, &n)) return rc;
-    std::vector<char> buf(n);
-    if (int rc = rrt_format_ppm_from_accum(width, height, accum, spp, buf.data(), n, &n)) return rc;
-    FILE *f = (!path || std::strcmp(path, "-") == 0) ? stdout : std::fopen(path, "wb");
-    if (!f) return fail(RRT_E_IO, std::string("cannot open ") + path);
-    const size_t w = std::fwrite(buf.data(), 1, n, f);
-    if (f == stdout) std::fflush(f);
-    else std::fclose(f);
-    if (w != n) return fail(RRT_E_IO, "short write");
-    return RRT_OK;
+    if (!accum && (size_t)width * height) return fail(RRT_E_INVALID, "null accum");
+    std::vector<uint8_t> rgb8((size_t)width * height * 3);
+    quantize_rgb8((size_t)width * height, accum, spp, rgb8.data());
+    return write_bytes(format_pnm(width, height, rgb8.data(), false), path);
+}
+
+int32_t rrt_format_pnm_from_rgb8(uint32_t width, uint32_t height, const uint8_t *rgb8, int32_t binary, char *buf,
+                                 size_t cap, size_t *written) {
+    if (!written) return fail(RRT_E_INVALID, "null written");
+    if (!rgb8 && (size_t)width * height) return fail(RRT_E_INVALID, "null rgb8");
+    return copy_out(format_pnm(width, height, rgb8, binary != 0), buf, cap, written);
+}
+
+int32_t rrt_write_pnm_from_rgb8(uint32_t width, uint32_t height, const uint8_t *rgb8, int32_t binary, const char *path) {
+    if (!rgb8 && (size_t)width * height) return fail(RRT_E_INVALID, "null rgb8");
+    return write_bytes(format_pnm(width, height, rgb8, binary != 0), path);
 }
 
 }  // extern "C"

@@ -120,5 +120,7 @@ constexpr size_t kPrimBytes = sizeof(float4) + sizeof(GMaterial);  // per primit
 // Launch wrappers implemented in rrt_kernel.hip.
 hipError_t launch_render(const KParams &p, hipStream_t stream);
 hipError_t launch_render_counting(const KParams &p, hipStream_t stream);
+// render_io quantiser on the device (d_accum: n_pixels x float4; d_rgb8: n_pixels x 3 B).
+hipError_t launch_quantize(const float *d_accum, uint8_t *d_rgb8, uint32_t n_pixels, float scale, hipStream_t stream);
 
 }  // namespace rrt

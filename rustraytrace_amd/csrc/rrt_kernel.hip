@@ -830,6 +830,47 @@ __global__ __launch_bounds__(256) void rrt_combine_chunks(const float4 *__restri
     accum[p] = make_float4(acc.x, acc.y, acc.z, count);
 }
 
+// render_io.rs:3-31 quantiser on the device: x * (1/spp) in f32, non-finite -> 0,
+// sqrt(max(0, x)) (correctly rounded), clamp [0, 0.999], (x * 256) as u8 — the same f32 ops
+// as the host's quantize_channel, so the bytes are identical. One thread per 4 pixels
+// (12 output bytes as 3 dwords when the row of pixels is whole).
+__device__ __forceinline__ uint32_t quantize_channel(float x, float scale) {
+    float r = x * scale;
+    if (!__builtin_isfinite(r)) r = 0.0f;
+    r = __builtin_sqrtf(r < 0.0f ? 0.0f : r);
+    if (r < 0.0f) r = 0.0f;
+    if (r > 0.999f) r = 0.999f;
+    return (uint32_t)(int)(r * 256.0f) & 0xffu;
+}
+
+__global__ __launch_bounds__(256) void rrt_quantize(const float4 *__restrict__ accum, uint8_t *__restrict__ rgb8,
+                                                     uint32_t n_pixels, float scale) {
+    const uint32_t q = blockIdx.x * 256u + threadIdx.x;  // group of 4 pixels
+    const uint32_t p0 = q * 4u;
+    if (p0 >= n_pixels) return;
+    if (p0 + 4u <= n_pixels) {
+        uint32_t b[12];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float4 a = accum[p0 + k];
+            b[3 * k + 0] = quantize_channel(a.x, scale);
+            b[3 * k + 1] = quantize_channel(a.y, scale);
+            b[3 * k + 2] = quantize_channel(a.z, scale);
+        }
+        uint32_t *dst = reinterpret_cast<uint32_t *>(rgb8 + (size_t)p0 * 3u);  // 12-B aligned
+#pragma unroll
+        for (int w = 0; w < 3; ++w)
+            dst[w] = b[4 * w] | (b[4 * w + 1] << 8) | (b[4 * w + 2] << 16) | (b[4 * w + 3] << 24);
+    } else {
+        for (uint32_t p = p0; p < n_pixels; ++p) {
+            const float4 a = accum[p];
+            rgb8[p * 3u + 0] = (uint8_t)quantize_channel(a.x, scale);
+            rgb8[p * 3u + 1] = (uint8_t)quantize_channel(a.y, scale);
+            rgb8[p * 3u + 2] = (uint8_t)quantize_channel(a.z, scale);
+        }
+    }
+}
+
 template <bool kLds, typename StackT, bool kWide, int kWaves = 1>
 hipError_t launch_variant(const KParams &p, bool count, hipStream_t stream) {
     if (p.n_units == 0) return hipSuccess;
@@ -873,6 +914,14 @@ hipError_t launch_render_kernel(const KParams &p, bool count, hipStream_t stream
 }
 
 hipError_t launch_render(const KParams &p, hipStream_t stream) { return launch_render_kernel(p, false, stream); }
+
+hipError_t launch_quantize(const float *d_accum, uint8_t *d_rgb8, uint32_t n_pixels, float scale, hipStream_t stream) {
+    if (n_pixels == 0) return hipSuccess;
+    const uint32_t groups = (n_pixels + 3u) / 4u;
+    hipLaunchKernelGGL(rrt_quantize, dim3((groups + 255u) / 256u), dim3(256), 0, stream,
+                       reinterpret_cast<const float4 *>(d_accum), d_rgb8, n_pixels, scale);
+    return hipGetLastError();
+}
 hipError_t launch_render_counting(const KParams &p, hipStream_t stream) { return launch_render_kernel(p, true, stream); }
 
 }  // namespace rrt

@@ -45,6 +45,47 @@ def render(scene: SceneData, spp: Optional[int] = None, n_gpus: int = 1, quiet: 
     return accum
 
 
+def render_rgb8(scene: SceneData, spp: Optional[int] = None, n_gpus: int = 1, quiet: bool = True) -> np.ndarray:
+    """rrt_hip_render_rgb8: render and quantise on the device (render_io.rs quantiser);
+    returns (H, W, 3) uint8, identical to quantize_accum(render(scene)) at the same spp."""
+    lib = _lib.load()
+    out = np.zeros((scene.height, scene.width, 3), dtype=np.uint8)
+    tex, ntex, keep = _textures(scene)
+    flags = scene.flags | (_lib.FLAG_QUIET if quiet else 0)
+    _lib.check(lib.rrt_hip_render_rgb8(_lib.ptr(scene.camera), _lib.ptr(scene.spheres), len(scene.spheres),
+                                       _lib.ptr(scene.materials), len(scene.materials),
+                                       ctypes.cast(tex, ctypes.c_void_p) if tex is not None else None, ntex,
+                                       int(spp or 0), int(n_gpus), flags, _lib.ptr(out)))
+    del keep
+    return out
+
+
+def quantize_accum_async(n_pixels: int, d_accum_ptr: int, samples_per_pixel: int, d_rgb8_ptr: int,
+                         stream_ptr: int = 0) -> None:
+    """rrt_quantize_accum_async on device pointers (e.g. torch tensors' data_ptr())."""
+    _lib.check(_lib.load().rrt_quantize_accum_async(int(n_pixels), ctypes.c_void_p(d_accum_ptr), int(samples_per_pixel),
+                                                    ctypes.c_void_p(d_rgb8_ptr), ctypes.c_void_p(stream_ptr)))
+
+
+def format_pnm_from_rgb8(width: int, height: int, rgb8: np.ndarray, binary: bool = False) -> bytes:
+    """P3 (byte-identical to format_ppm_from_accum of the same image) or binary P6."""
+    lib = _lib.load()
+    rgb8 = np.ascontiguousarray(rgb8, dtype=np.uint8)
+    assert rgb8.size == width * height * 3
+    n = ctypes.c_size_t(0)
+    _lib.check(lib.rrt_format_pnm_from_rgb8(width, height, _lib.ptr(rgb8), int(binary), None, 0, ctypes.byref(n)))
+    buf = ctypes.create_string_buffer(n.value)
+    _lib.check(lib.rrt_format_pnm_from_rgb8(width, height, _lib.ptr(rgb8), int(binary), buf, n.value,
+                                            ctypes.byref(n)))
+    return buf.raw[: n.value]
+
+
+def write_pnm_from_rgb8(width: int, height: int, rgb8: np.ndarray, binary: bool = False, path: str = "-") -> None:
+    rgb8 = np.ascontiguousarray(rgb8, dtype=np.uint8)
+    assert rgb8.size == width * height * 3
+    _lib.check(_lib.load().rrt_write_pnm_from_rgb8(width, height, _lib.ptr(rgb8), int(binary), path.encode()))
+
+
 def render_in_one_weekend(path: str = "-", n_gpus: int = 1, overrides: Optional[dict] = None) -> None:
     """cuda::render_in_one_weekend: RTOW scene under config::OVERRIDES -> P3 PPM on stdout (or `path`)."""
     scene = build_in_one_weekend_scene(COMMITTED_OVERRIDES if overrides is None else overrides)
