@@ -104,9 +104,12 @@ void put4(float *dst, float a, float b, float c, float d) {
 }
 
 // ------------------------------------------------------------------------------------
-// BVH: binned SAH exactly as bvh.rs:21-156 chooses splits (12 buckets, longest axis of
-// the node bbox, stable-sort+median fallbacks), with leaves of <= max_leaf spheres, then
-// flattened into 64-B GNodes with both child boxes in the parent.
+// BVH over the sphere boxes (aabb.rs padding, sphere.rs:16-21 bounds): by default a full
+// sweep SAH on all three axes (Builder::sweep); RRT_BVH_SPLIT=binned selects the reference's
+// own criterion — binned SAH exactly as bvh.rs:21-156 chooses splits (12 buckets, longest axis
+// of the node bbox, stable-sort+median fallbacks). Leaves hold <= max_leaf spheres; the tree
+// is flattened into 64-B GNodes with both child boxes in the parent. The tree only changes
+// which boxes are tested, never a sphere's result.
 // ------------------------------------------------------------------------------------
 struct Interval {
     double min, max;
@@ -154,6 +157,13 @@ struct Builder {
     const std::vector<Aabb> &boxes;
     std::vector<uint32_t> objs;
     uint32_t max_leaf;
+    // Split criterion: false = bvh.rs's (12 buckets on the longest axis); true (default) = full
+    // sweep SAH over sorted centroids on all three axes, with small nodes kept as leaves unless
+    // splitting is cheaper: leaf cost n (sphere tests) vs node_cost + (A_l n_l + A_r n_r)/A.
+    // node_cost 2 (a node visit ~ two sphere tests in this kernel) measured best: C2 +3.5 %
+    // over the bvh.rs criterion, and the RTOW tree (203 nodes) still fits the LDS budget.
+    bool sweep = true;
+    double node_cost = 2.0;
 
     // Binary SAH tree (bvh.rs:16-156 split choice), leaves of <= max_leaf spheres.
     struct BNode {
@@ -248,6 +258,40 @@ struct Builder {
         return lo + mid;
     }
 
+    // Exact SAH sweep: best (axis, position) over centroid-sorted orders of objs[lo, hi);
+    // reorders objs[lo, hi) into the winning order and returns (split index, A_l n_l + A_r n_r).
+    size_t split_sweep(size_t lo, size_t hi, double &best_cost) {
+        const size_t n = hi - lo;
+        std::vector<uint32_t> order[3];
+        std::vector<double> right_area(n + 1);
+        best_cost = kInf;
+        int best_axis = 0;
+        size_t best_i = n / 2;
+        for (int axis = 0; axis < 3; ++axis) {
+            order[axis].assign(objs.begin() + lo, objs.begin() + hi);
+            std::stable_sort(order[axis].begin(), order[axis].end(), [&](uint32_t a, uint32_t b) {
+                return centroid(a, axis) < centroid(b, axis);
+            });
+            Aabb acc = aabb_empty();
+            for (size_t i = n; i-- > 1;) {
+                acc = aabb_union(acc, boxes[order[axis][i]]);
+                right_area[i] = surface_area(acc);
+            }
+            acc = aabb_empty();
+            for (size_t i = 1; i < n; ++i) {
+                acc = aabb_union(acc, boxes[order[axis][i - 1]]);
+                const double cost = surface_area(acc) * (double)i + right_area[i] * (double)(n - i);
+                if (cost < best_cost) {
+                    best_cost = cost;
+                    best_axis = axis;
+                    best_i = i;
+                }
+            }
+        }
+        std::copy(order[best_axis].begin(), order[best_axis].end(), objs.begin() + lo);
+        return lo + best_i;
+    }
+
     int32_t build(size_t lo, size_t hi) {
         Aabb bbox = aabb_empty();
         for (size_t i = lo; i < hi; ++i) bbox = aabb_union(bbox, boxes[objs[i]]);
@@ -255,13 +299,26 @@ struct Builder {
         bin.push_back(BNode{});
         bin[me].box = bbox;
         const size_t span = hi - lo;
-        if (span <= max_leaf) {
+        size_t mid;
+        if (sweep && span > 1) {
+            double cost = kInf;
+            mid = split_sweep(lo, hi, cost);
+            const double area = surface_area(bbox);
+            const bool keep_leaf = span <= max_leaf && !(area > 0.0 && node_cost + cost / area < (double)span);
+            if (keep_leaf) {
+                bin[me].leaf = true;
+                bin[me].first = (int32_t)lo;
+                bin[me].count = (int32_t)span;
+                return me;
+            }
+        } else if (span <= max_leaf) {
             bin[me].leaf = true;
             bin[me].first = (int32_t)lo;
             bin[me].count = (int32_t)span;
             return me;
+        } else {
+            mid = split(lo, hi, bbox);
         }
-        const size_t mid = split(lo, hi, bbox);
         const int32_t l = build(lo, mid);
         const int32_t r = build(mid, hi);
         bin[me].left = l;
@@ -457,6 +514,8 @@ FlatBvh build_bvh(const RrtSphere *spheres, uint32_t n_spheres, uint32_t width, 
         boxes[i] = pad(b);
     }
     Builder bld(boxes, max_leaf);
+    if (const char *e = std::getenv("RRT_BVH_SPLIT")) bld.sweep = std::strcmp(e, "binned") != 0;
+    if (const char *e = std::getenv("RRT_SAH_CT")) bld.node_cost = std::atof(e);
     FlatBvh fb;
     if (n_spheres == 0) {  // root with never-hit children
         Builder::BNode empty;
