@@ -85,19 +85,21 @@ __device__ __forceinline__ float rnd_range(uint64_t &s, float lo, float hi) { re
 
 // vec3.rs:181-189 random_unit_vector: rejection in [-1,1)^3, accept 1e-160 < |p|^2 <= 1
 // (1e-160 underflows to 0 in f32: the one intentional f32 deviation).
+// The loop only draws and tests; the normalisation runs once after it, with the wave
+// converged (inside the loop it would run in every iteration in which any lane accepts).
 template <typename C>
 __device__ __forceinline__ V3 random_unit_vector(uint64_t &s, C &cnt) {
+    float px, py, pz, lensq;
     for (;;) {
         if constexpr (RRT_PHASE_TIMING == 4) cnt.d2 += wave_slot();
-        const float px = rnd_range(s, -1.0f, 1.0f);
-        const float py = rnd_range(s, -1.0f, 1.0f);
-        const float pz = rnd_range(s, -1.0f, 1.0f);
-        const float lensq = px * px + py * py + pz * pz;
-        if (0.0f < lensq && lensq <= 1.0f) {
-            const float inv = 1.0f / __builtin_sqrtf(lensq);
-            return v3(px * inv, py * inv, pz * inv);
-        }
+        px = rnd_range(s, -1.0f, 1.0f);
+        py = rnd_range(s, -1.0f, 1.0f);
+        pz = rnd_range(s, -1.0f, 1.0f);
+        lensq = px * px + py * py + pz * pz;
+        if (0.0f < lensq && lensq <= 1.0f) break;
     }
+    const float inv = 1.0f / __builtin_sqrtf(lensq);
+    return v3(px * inv, py * inv, pz * inv);
 }
 
 // vec3.rs:201-203 reflect = v - n*(2*dot(v,n))
