@@ -191,6 +191,43 @@ struct Counters {
     uint32_t d0, d1, d2;
 };
 
+// Per-ray constants of the box and sphere tests. Recomputed from (o, d) each time a wave
+// enters its traversal loop rather than kept alive across shading (same IEEE ops, so the
+// same values): 7 fewer registers held by lanes parked mid-tree.
+struct RayK {
+    V3 inv;
+    V3 oi;     // o * inv
+    float a;
+    float ra;  // refined reciprocal of a (0 when a is outside [2^-64, 2^64])
+};
+
+__device__ __forceinline__ RayK ray_consts(V3 o, V3 d) {
+    RayK r;
+    r.inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);  // aabb.rs:58 adinv, hoisted per ray
+    r.oi = v3(o.x * r.inv.x, o.y * r.inv.y, o.z * r.inv.z);
+    r.a = dot(d, d);                                  // sphere.rs:27, hoisted per ray
+    // The reciprocal step of the IEEE f32 division expansion (v_rcp + one Newton step), done
+    // once per ray instead of in every root division (div_by_a).
+    const float r0 = __builtin_amdgcn_rcpf(r.a);
+    const float e = __builtin_fmaf(-r.a, r0, 1.0f);
+    r.ra = (r.a >= 0x1.0p-64f && r.a <= 0x1.0p64f) ? __builtin_fmaf(e, r0, r0) : 0.0f;
+    return r;
+}
+
+// n / a, correctly rounded: the quotient steps of the compiler's IEEE f32 division expansion
+// (q = n*r, two remainder corrections by fma) on the per-ray reciprocal. For a in
+// [2^-64, 2^64] the expansion's v_div_scale / v_div_fmas / v_div_fixup are identities except
+// when |n| < 2^-103, where both results are below the 0.001 acceptance bound, so every
+// accept/reject decision and every accepted root equals the IEEE quotient (the oracle's).
+__device__ __forceinline__ float div_by_a(float n, const RayK &rk) {
+    if (rk.ra == 0.0f) return n / rk.a;
+    const float q0 = n * rk.ra;
+    const float e0 = __builtin_fmaf(-rk.a, q0, n);
+    const float q1 = __builtin_fmaf(e0, rk.ra, q0);
+    const float e1 = __builtin_fmaf(-rk.a, q1, n);
+    return __builtin_fmaf(e1, rk.ra, q1);
+}
+
 // Sphere::hit (sphere.rs:24-51) root selection; returns true and shrinks `closest`.
 template <bool kCount>
 __device__ __forceinline__ void test_prims(const float4 *__restrict__ prim_cr, int first, int count, V3 o, V3 d,
@@ -217,7 +254,8 @@ __device__ __forceinline__ void test_prims(const float4 *__restrict__ prim_cr, i
 // Leaf spheres of two ranges [f0, f0+c0) then [f1, f1+c1) in one loop.
 template <bool kCount>
 __device__ __forceinline__ void test_prims2(const float4 *__restrict__ prim_cr, int f0, int c0, int f1, int c1, V3 o,
-                                            V3 d, float a, float &closest, int &hit_prim, Counters &cnt) {
+                                            V3 d, const RayK &rk, float &closest, int &hit_prim, Counters &cnt) {
+    const float a = rk.a;
     const int total = c0 + c1;
     for (int k = 0; k < total; ++k) {
         const int i = (k < c0) ? f0 + k : f1 + (k - c0);
@@ -234,9 +272,9 @@ __device__ __forceinline__ void test_prims2(const float4 *__restrict__ prim_cr, 
         if (disc < 0.0f) continue;
         if constexpr (RRT_PHASE_TIMING == 3) cnt.d2 += 1;
         const float sq = __builtin_sqrtf(disc);
-        float root = (h - sq) / a;
+        float root = div_by_a(h - sq, rk);
         if (!(0.001f < root && root < closest)) {
-            root = (h + sq) / a;
+            root = div_by_a(h + sq, rk);
             if (!(0.001f < root && root < closest)) continue;
         }
         closest = root;
@@ -260,23 +298,6 @@ struct LdsStack {
     __device__ __forceinline__ void store(int sp, int v) { base[sp * kBlock] = (StackT)v; }
     __device__ __forceinline__ int load(int sp) const { return (int)base[sp * kBlock]; }
 };
-
-// Per-ray constants of the box and sphere tests. Recomputed from (o, d) each time a wave
-// enters its traversal loop rather than kept alive across shading (same IEEE ops, so the
-// same values): 7 fewer registers held by lanes parked mid-tree.
-struct RayK {
-    V3 inv;
-    V3 oi;  // o * inv
-    float a;
-};
-
-__device__ __forceinline__ RayK ray_consts(V3 o, V3 d) {
-    RayK r;
-    r.inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);  // aabb.rs:58 adinv, hoisted per ray
-    r.oi = v3(o.x * r.inv.x, o.y * r.inv.y, o.z * r.inv.z);
-    r.a = dot(d, d);                                  // sphere.rs:27, hoisted per ray
-    return r;
-}
 
 // Resumable BVH traversal: one call = one node. The state lives in registers (+ the LDS stack)
 // so a wave can leave the traversal loop while some lanes are still mid-tree.
@@ -344,7 +365,7 @@ template <bool kCount>
 __device__ __forceinline__ void trav_leaves(const float4 *__restrict__ prims, const Leaves &lv, V3 o, V3 d,
                                             const RayK &rk, Trav &t, Counters &cnt) {
     test_prims2<kCount>(prims, (int)(lv.l0 & kLeafFirstMask), (int)(lv.l0 >> 28), (int)(lv.l1 & kLeafFirstMask),
-                        (int)(lv.l1 >> 28), o, d, rk.a, t.closest, t.hit_prim, cnt);
+                        (int)(lv.l1 >> 28), o, d, rk, t.closest, t.hit_prim, cnt);
 }
 
 // Visits node t.node: tests both children, tests leaf spheres in place, descends into the
@@ -361,7 +382,7 @@ __device__ __forceinline__ bool trav_step(const GNode *__restrict__ nodes, const
     const int c0 = (h0 && n.link.z > 0) ? n.link.z : 0;
     const int c1 = (h1 && n.link.w > 0) ? n.link.w : 0;
     if (c0 + c1 > 0) {
-        test_prims2<kCount>(prims, n.link.x, c0, n.link.y, c1, o, d, rk.a, t.closest, t.hit_prim, cnt);
+        test_prims2<kCount>(prims, n.link.x, c0, n.link.y, c1, o, d, rk, t.closest, t.hit_prim, cnt);
         if (c0) h0 = false;
         if (c1) h1 = false;
     }
