@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define RRT_ABI_VERSION 1u
+#define RRT_ABI_VERSION 2u
 
 /* ---- scene ABI (== src/gpu/mod.rs:13-42) ------------------------------------------ */
 
@@ -52,10 +52,14 @@ typedef struct RrtSphere {
     uint32_t _pad[3];
 } RrtSphere;
 
-/* == MaterialGpu (gpu/mod.rs:37-42), 32 B. kind 0..2 are the reference's; 3 and 4 extend
- * the ABI for the textured-earth config (the_next_week/material.rs:27-53,116-135):
+/* == MaterialGpu (gpu/mod.rs:37-42), 32 B. kind 0..2 are the reference's; 3..6 extend the
+ * ABI for book 2 (the_next_week/material.rs:27-53,116-135, texture.rs:39-77,111-126):
  *   3 = textured Lambertian, _pad[0] = texture index into the RrtTexture array
- *   4 = diffuse light, albedo_fuzz.xyz = emitted radiance */
+ *   4 = diffuse light, albedo_fuzz.xyz = emitted radiance
+ *   5 = Lambertian with a solid-colour CheckerTexture: albedo_fuzz.xyz = even colour,
+ *       albedo_fuzz[3] = inv_scale (1/scale), odd colour = (ref_idx, bits of _pad[0], bits of _pad[1])
+ *   6 = Lambertian with a NoiseTexture: albedo_fuzz[3] = scale, _pad[0] = Perlin table index
+ *       into RrtSceneExt.perlin */
 typedef struct RrtMaterial {
     float albedo_fuzz[4];
     uint32_t kind;
@@ -68,8 +72,32 @@ enum {
     RRT_MAT_METAL = 1,
     RRT_MAT_DIELECTRIC = 2,
     RRT_MAT_TEXTURED_LAMBERTIAN = 3,
-    RRT_MAT_DIFFUSE_LIGHT = 4
+    RRT_MAT_DIFFUSE_LIGHT = 4,
+    RRT_MAT_CHECKER_LAMBERTIAN = 5,
+    RRT_MAT_NOISE_LAMBERTIAN = 6
 };
+
+/* == Perlin (the_next_week/perlin.rs:4-22): 256 unit random vectors and the three
+ * permutations of 0..255. 4 KB. The reference draws them from the thread-local entropy RNG;
+ * rrt_build_next_week_scene draws them from a seeded stream (parity unpinned). */
+typedef struct RrtPerlin {
+    float randvec[256][4]; /* xyz, w unused */
+    uint16_t perm_x[256];
+    uint16_t perm_y[256];
+    uint16_t perm_z[256];
+    uint16_t _pad[256];
+} RrtPerlin;
+
+/* Book-2 scene data beyond the flat sphere/material ABI. NULL = none.
+ * sphere_motion: n_spheres x 4 floats, (center2 - center1).xyz of Sphere::new_moving
+ * (the_next_week/sphere.rs:24-40; the sphere's center at ray time t is center1 + t*motion;
+ * zero = static). Requires RRT_FLAG_RAY_TIME (rays carry the camera's time draw). */
+typedef struct RrtSceneExt {
+    const float *sphere_motion;
+    const RrtPerlin *perlin;
+    uint32_t n_perlin;
+    uint32_t _pad;
+} RrtSceneExt;
 
 /* Image texture, RGB8 row-major (rtw_image.rs:57-67 `to_rgb8().into_raw()`). Borrowed. */
 typedef struct RrtTexture {
@@ -120,6 +148,15 @@ int32_t rrt_hip_render(const RrtCamera *cam,
                        uint32_t total_spp, uint32_t n_gpus, uint32_t flags,
                        float *accum_out);
 
+/* rrt_hip_render with book-2 scene data (moving spheres, Perlin tables); ext may be NULL. */
+int32_t rrt_hip_render_ex(const RrtCamera *cam,
+                          const RrtSphere *spheres, uint32_t n_spheres,
+                          const RrtMaterial *materials, uint32_t n_materials,
+                          const RrtTexture *textures, uint32_t n_textures,
+                          const RrtSceneExt *ext,
+                          uint32_t total_spp, uint32_t n_gpus, uint32_t flags,
+                          float *accum_out);
+
 /* Thread-local message for the last failing call on this thread ("" if none). */
 const char *rrt_hip_last_error(void);
 uint32_t rrt_hip_abi_version(void);
@@ -159,6 +196,13 @@ int32_t rrt_scene_create(const RrtCamera *cam,
                          const RrtMaterial *materials, uint32_t n_materials,
                          const RrtTexture *textures, uint32_t n_textures,
                          uint32_t flags, int32_t device, RrtScene **out);
+/* rrt_scene_create with book-2 scene data; ext may be NULL. */
+int32_t rrt_scene_create_ex(const RrtCamera *cam,
+                            const RrtSphere *spheres, uint32_t n_spheres,
+                            const RrtMaterial *materials, uint32_t n_materials,
+                            const RrtTexture *textures, uint32_t n_textures,
+                            const RrtSceneExt *ext,
+                            uint32_t flags, int32_t device, RrtScene **out);
 int32_t rrt_scene_destroy(RrtScene *scene);
 
 /* Number of image rows `tile` owns in an image of `height` rows (its accum is rows*W float4). */
@@ -197,6 +241,11 @@ int32_t rrt_scene_bvh_info(const RrtScene *scene, RrtBvhInfo *out);
  * (info->node_bytes). Lets a checker walk exactly the tree the kernel walks. */
 int32_t rrt_build_bvh(const RrtSphere *spheres, uint32_t n_spheres, uint32_t width, uint32_t max_leaf,
                       void *nodes_out, size_t nodes_cap, uint32_t *prim_order_out, RrtBvhInfo *info);
+/* The same with moving spheres (motion: n_spheres x 4 floats as RrtSceneExt, or NULL): a moving
+ * sphere's box spans both ends of its motion (Aabb::from_boxes, the_next_week/sphere.rs:31-33). */
+int32_t rrt_build_bvh_ex(const RrtSphere *spheres, uint32_t n_spheres, const float *motion, uint32_t width,
+                         uint32_t max_leaf, void *nodes_out, size_t nodes_cap, uint32_t *prim_order_out,
+                         RrtBvhInfo *info);
 
 /* ---- host-side callers of the boundary ------------------------------------------------ */
 
@@ -208,6 +257,18 @@ int32_t rrt_build_bvh(const RrtSphere *spheres, uint32_t n_spheres, uint32_t wid
 int32_t rrt_build_in_one_weekend_scene(const RrtOverrides *ov, uint64_t seed, int32_t grid_half,
                                        RrtCamera *cam, RrtSphere *spheres, RrtMaterial *materials,
                                        uint32_t sphere_cap, uint32_t *n_spheres);
+
+/* Book-2 scenes (the_next_week/mod.rs:68-255) flattened into the ABI: 1 bouncing_spheres,
+ * 2 checkered_spheres, 3 earth, 4 perlin_spheres. Random draws come from SmallRng(seed)
+ * in the books' order (the reference uses the entropy RNG: parity unpinned). Writes up to
+ * sphere_cap spheres / materials / motion rows (motion may be NULL) and up to perlin_cap
+ * Perlin tables; *n_spheres, *n_perlin = counts needed (call with caps 0 to size). The earth
+ * texture (scene 3) is material texture index 0: the caller supplies the image. The camera
+ * carries book 2's background (bg_mode 1); render with RRT_FLAG_RAY_TIME. */
+int32_t rrt_build_next_week_scene(int32_t scene, const RrtOverrides *ov, uint64_t seed, RrtCamera *cam,
+                                  RrtSphere *spheres, RrtMaterial *materials, float *motion,
+                                  uint32_t sphere_cap, uint32_t *n_spheres,
+                                  RrtPerlin *perlin, uint32_t perlin_cap, uint32_t *n_perlin);
 
 /* Camera::initialize (in_one_weekend/camera.rs:102-150) in f64, cast to the f32 ABI as
  * gpu/mod.rs:278-298 does. lookfrom/lookat/vup are 3-vectors. */

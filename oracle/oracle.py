@@ -37,11 +37,15 @@ def load() -> ctypes.CDLL:
     lib = ctypes.CDLL(LIB_PATH)
     P = c_void_p
     lib.oracle_render.restype = c_int
-    lib.oracle_render.argtypes = [P, P, c_uint32, P, c_uint32, P, c_uint32, c_uint32, c_int, c_uint32, c_uint32,
+    lib.oracle_render.argtypes = [P, P, c_uint32, P, c_uint32, P, c_uint32, P, c_uint32, c_int, c_uint32, c_uint32,
                                   c_uint32, c_uint32, c_int, P, P, P, c_uint32]
     lib.oracle_render_kbvh.restype = c_int
-    lib.oracle_render_kbvh.argtypes = [P, P, c_uint32, P, c_uint32, P, c_uint32, c_uint32, P, c_uint32, c_uint32, P,
+    lib.oracle_render_kbvh.argtypes = [P, P, c_uint32, P, c_uint32, P, c_uint32, P, c_uint32, P, c_uint32, c_uint32, P,
                                        c_uint32, c_uint32, c_uint32, c_uint32, c_int, P, P, P, c_uint32]
+    lib.oracle_sin_f32.restype = None
+    lib.oracle_sin_f32.argtypes = [c_uint32, P, P]
+    lib.oracle_book2_textures.restype = None
+    lib.oracle_book2_textures.argtypes = [c_int, P, c_double, c_double, c_uint32, P, P, P, P]
     lib.oracle_rtow_scene.restype = c_int
     lib.oracle_rtow_scene.argtypes = [c_uint64, c_int, P, P, P, P, P, c_uint32, P, P]
     lib.oracle_write_color.restype = None
@@ -77,6 +81,30 @@ class _Tex(ctypes.Structure):
     _fields_ = [("rgb8", POINTER(c_uint8)), ("width", ctypes.c_int32), ("height", ctypes.c_int32)]
 
 
+class _Ext(ctypes.Structure):  # RrtSceneExt (include/rrt_hip.h)
+    _fields_ = [("sphere_motion", c_void_p), ("perlin", c_void_p), ("n_perlin", c_uint32), ("_pad", c_uint32)]
+
+
+def _ext(scene):
+    """(pointer to RrtSceneExt or None, keep-alive) from the scene's book-2 motion / Perlin data."""
+    motion, perlin = getattr(scene, "motion", None), getattr(scene, "perlin", None)
+    if motion is None and perlin is None:
+        return None, []
+    e, keep = _Ext(), []
+    if motion is not None:
+        m = np.ascontiguousarray(motion, dtype=np.float32)
+        keep.append(m)
+        e.sphere_motion = m.ctypes.data
+    if perlin is not None:
+        t = np.ascontiguousarray(perlin)
+        assert t.dtype.itemsize == 6144, "RrtPerlin tables"
+        keep.append(t)
+        e.perlin = t.ctypes.data
+        e.n_perlin = len(t)
+    keep.append(e)
+    return ctypes.cast(ctypes.byref(e), c_void_p), keep
+
+
 def render(scene, mode=TWIN, rows=None, samples=None, threads=1, chunk=DEFAULT_CHUNK):
     """Render `scene` (rustraytrace_amd.SceneData-like: camera/spheres/materials/textures/flags).
 
@@ -94,10 +122,12 @@ def render(scene, mode=TWIN, rows=None, samples=None, threads=1, chunk=DEFAULT_C
         tex[i].rgb8 = t.ctypes.data_as(POINTER(c_uint8))
         tex[i].height, tex[i].width = t.shape[0], t.shape[1]
     rays, tests = c_uint64(0), c_uint64(0)
+    ext, keep_ext = _ext(scene)
     rc = lib.oracle_render(_p(scene.camera), _p(scene.spheres), len(scene.spheres), _p(scene.materials),
-                           len(scene.materials), ctypes.cast(tex, c_void_p) if keep else None, len(keep),
+                           len(scene.materials), ctypes.cast(tex, c_void_p) if keep else None, len(keep), ext,
                            int(scene.flags), int(mode), y0, y1, s0, s1, int(threads), _p(accum),
                            ctypes.byref(rays), ctypes.byref(tests), int(chunk))
+    del keep_ext
     if rc != 0:
         raise RuntimeError(f"oracle_render failed ({rc})")
     return accum, rays.value, tests.value
@@ -121,10 +151,12 @@ def render_kbvh(scene, nodes, order, width, rows=None, samples=None, threads=1, 
     order = np.ascontiguousarray(order, dtype=np.uint32)
     n_nodes = nodes.size // (64 if width == 2 else 128)
     rays, tests = c_uint64(0), c_uint64(0)
+    ext, keep_ext = _ext(scene)
     rc = lib.oracle_render_kbvh(_p(scene.camera), _p(scene.spheres), len(scene.spheres), _p(scene.materials),
-                                len(scene.materials), ctypes.cast(tex, c_void_p) if keep else None, len(keep),
+                                len(scene.materials), ctypes.cast(tex, c_void_p) if keep else None, len(keep), ext,
                                 int(scene.flags), _p(nodes), n_nodes, int(width), _p(order), y0, y1, s0, s1,
                                 int(threads), _p(accum), ctypes.byref(rays), ctypes.byref(tests), int(chunk))
+    del keep_ext
     if rc != 0:
         raise RuntimeError(f"oracle_render_kbvh failed ({rc})")
     return accum, rays.value, tests.value
@@ -201,3 +233,25 @@ def acos_atan2_f32(x, y):
     a, b = c_float(0), c_float(0)
     lib.oracle_acos_atan2_f32(x, y, ctypes.byref(a), ctypes.byref(b))
     return a.value, b.value
+
+
+def sin_f32(x):
+    """The f32 Cephes sin of the kernel (rrt_sinf) at each element of x."""
+    lib = load()
+    xs = np.ascontiguousarray(x, dtype=np.float32).ravel()
+    out = np.zeros_like(xs)
+    lib.oracle_sin_f32(xs.size, _p(xs), _p(out))
+    return out
+
+
+def book2_textures(perlin_table, points, scale=4.0, inv_scale=1.0 / 0.32, f32=True):
+    """Perlin::noise, NoiseTexture::value and CheckerTexture parity at points (n, 3) for one
+    RrtPerlin table (f32=True: the twin arithmetic, else f64). Returns (noise, value, even)."""
+    lib = load()
+    t = np.ascontiguousarray(perlin_table)
+    pts = np.ascontiguousarray(points, dtype=np.float64).reshape(-1, 3)
+    n = len(pts)
+    noise, value, even = np.zeros(n), np.zeros(n), np.zeros(n, np.int32)
+    lib.oracle_book2_textures(int(f32), _p(t), float(scale), float(inv_scale), n, _p(pts), _p(noise), _p(value),
+                              _p(even))
+    return noise, value, even.astype(bool)

@@ -18,6 +18,9 @@
 //   get_sphere_uv, ImageTexture::value, RtwImage::pixel_data  the_next_week/sphere.rs:46-52, texture.rs:177-196,
 //                                                             rtw_image.rs:46-78
 //   DiffuseLight::emitted                                     the_next_week/material.rs:116-135
+//   Sphere::new_moving / hit at ray time                      the_next_week/sphere.rs:24-45
+//   CheckerTexture / NoiseTexture::value                      the_next_week/texture.rs:39-77, 111-126
+//   Perlin::noise / turb / perlin_interp                      the_next_week/perlin.rs:25-102
 //   write_color (f64 quantiser)                               books/in_one_weekend/color.rs:6-32
 //   write_ppm_from_accum (f32 quantiser)                      render_io.rs:3-31
 //   build_in_one_weekend_scene (seeded SmallRng scene)        gpu/mod.rs:124-301
@@ -33,8 +36,8 @@
 //   * RNG: the reference's thread-local SmallRng::from_entropy (rtweekend.rs:9-11) is not
 //     reproducible; both sides use a PCG32 stream per (seed, pixel, sample) instead, and
 //     random_double() = (u32 >> 8) * 2^-24 (exact in f32 and f64).
-//   * f32 twin: 1e-160 (vec3.rs:185) underflows to 0; transcendentals of sphere UV use the
-//     Cephes f32 polynomials the kernel uses (books mode uses libm acos/atan2).
+//   * f32 twin: 1e-160 (vec3.rs:185) underflows to 0; transcendentals of sphere UV and the
+//     noise texture's sin use the Cephes f32 polynomials the kernel uses (books mode: libm).
 #include "../include/rrt_hip.h"
 
 #include <algorithm>
@@ -228,17 +231,25 @@ template <class T> bool aabb_hit(const Aabb<T> &box, Vec3<T> o, Vec3<T> d, Inter
 
 // ---- scene in T ---------------------------------------------------------------------------------
 template <class T> struct Sphere {
-    Vec3<T> center;
+    Vec3<T> center;  // center1 (Ray origin of the_next_week/sphere.rs:38)
     T radius;
     uint32_t mat;
     Aabb<T> bbox;
+    Vec3<T> motion;  // center2 - center1 (zero: static)
+    Vec3<T> at(T time) const { return center + time * motion; }  // Ray::at (ray.rs: orig + t*dir)
 };
 template <class T> struct Material {
     uint32_t kind;
     Vec3<T> albedo;
-    T fuzz;
+    T fuzz;   // metal fuzz (clamped <= 1)
+    T w;      // albedo_fuzz[3] raw: checker inv_scale, noise scale
     T ref_idx;
     uint32_t tex;
+    Vec3<T> odd;  // checker odd colour
+};
+template <class T> struct PerlinT {  // perlin.rs:4-9
+    Vec3<T> randvec[256];
+    uint32_t perm_x[256], perm_y[256], perm_z[256];
 };
 struct Texture {
     const uint8_t *data;
@@ -264,6 +275,8 @@ template <class T> struct World {
     std::vector<Sphere<T>> spheres;
     std::vector<Material<T>> mats;
     std::vector<Texture> texs;
+    std::vector<PerlinT<T>> perlin;
+    bool book2 = false;  // moving spheres or checker / noise materials (kernel: kBook2)
     std::vector<BvhNode<T>> nodes;
     ChildRef root{false, -1};
 
@@ -356,10 +369,10 @@ template <class T> struct World {
     }
 
     // Sphere::hit (sphere.rs:24-51): Some(t) iff a root lies in the open interval.
-    bool hit_sphere(int32_t i, Vec3<T> o, Vec3<T> d, Interval<T> ray_t, T &t_out, uint64_t *tests) const {
+    bool hit_sphere(int32_t i, Vec3<T> o, Vec3<T> d, T time, Interval<T> ray_t, T &t_out, uint64_t *tests) const {
         if (tests) ++*tests;
         const Sphere<T> &s = spheres[i];
-        const Vec3<T> oc = s.center - o;
+        const Vec3<T> oc = (book2 ? s.at(time) : s.center) - o;  // current_center (the_next_week/sphere.rs:44)
         const T a = length_squared(d);
         const T h = dot(d, oc);
         const T c = length_squared(oc) - s.radius * s.radius;
@@ -377,18 +390,18 @@ template <class T> struct World {
 
     // HittableObject::hit dispatch + BvhNode::hit (bvh.rs:159-172), left first, right with
     // max = left.t, result = right.or(left).
-    bool hit(ChildRef ref, Vec3<T> o, Vec3<T> d, Interval<T> ray_t, Hit<T> &rec, uint64_t *tests) const {
+    bool hit(ChildRef ref, Vec3<T> o, Vec3<T> d, T time, Interval<T> ray_t, Hit<T> &rec, uint64_t *tests) const {
         if (ref.is_sphere) {
             T t;
-            if (!hit_sphere(ref.index, o, d, ray_t, t, tests)) return false;
+            if (!hit_sphere(ref.index, o, d, time, ray_t, t, tests)) return false;
             rec = Hit<T>{t, ref.index};
             return true;
         }
         const BvhNode<T> &n = nodes[ref.index];
         if (!aabb_hit(n.bbox, o, d, ray_t)) return false;
         Hit<T> hl, hr;
-        const bool l = hit(n.left, o, d, ray_t, hl, tests);
-        const bool r = hit(n.right, o, d, Interval<T>{ray_t.min, l ? hl.t : ray_t.max}, hr, tests);
+        const bool l = hit(n.left, o, d, time, ray_t, hl, tests);
+        const bool r = hit(n.right, o, d, time, Interval<T>{ray_t.min, l ? hl.t : ray_t.max}, hr, tests);
         if (r) { rec = hr; return true; }
         if (l) { rec = hl; return true; }
         return false;
@@ -435,7 +448,8 @@ static inline float max_num(float a, float b) { return (b != b) ? a : ((a != a) 
 // std::fmaf is a slow libm call without -mfma: clone the traversal for FMA-capable hosts
 // (results are identical either way: fmaf is correctly rounded in both).
 __attribute__((target_clones("fma", "default")))
-bool kbvh_hit(const World<float> &w, const KTree &kt, Vec3<float> o, Vec3<float> d, Hit<float> &rec, uint64_t *tests) {
+bool kbvh_hit(const World<float> &w, const KTree &kt, Vec3<float> o, Vec3<float> d, float time, Hit<float> &rec,
+              uint64_t *tests) {
     KRay r;
     r.ix = 1.0f / d[0];
     r.iy = 1.0f / d[1];
@@ -449,7 +463,7 @@ bool kbvh_hit(const World<float> &w, const KTree &kt, Vec3<float> o, Vec3<float>
     auto leaf = [&](int32_t first, int32_t count) {
         for (int32_t i = first; i < first + count; ++i) {
             float t;
-            if (w.hit_sphere((int32_t)kt.order[i], o, d, Interval<float>{kTmin, closest}, t, tests)) {
+            if (w.hit_sphere((int32_t)kt.order[i], o, d, time, Interval<float>{kTmin, closest}, t, tests)) {
                 closest = t;
                 hit = i;
             }
@@ -526,7 +540,7 @@ template <class T> struct Cam {
 
 template <class T>
 void load_world(World<T> &w, Cam<T> &cam, const RrtCamera *c, const RrtSphere *s, uint32_t n, const RrtMaterial *m,
-                uint32_t nm, const RrtTexture *tex, uint32_t ntex, uint32_t flags) {
+                uint32_t nm, const RrtTexture *tex, uint32_t ntex, uint32_t flags, const RrtSceneExt *ext) {
     auto v3 = [](const float *f) { return mk<T>((T)f[0], (T)f[1], (T)f[2]); };
     cam.center = v3(c->origin);
     cam.p00 = v3(c->pixel00);
@@ -542,12 +556,21 @@ void load_world(World<T> &w, Cam<T> &cam, const RrtCamera *c, const RrtSphere *s
     cam.flags = flags;
     cam.width = (uint32_t)c->params_f[1];
     cam.height = (uint32_t)c->params_f[2];
+    const float *motion = ext ? ext->sphere_motion : nullptr;
     w.spheres.resize(n);
-    for (uint32_t i = 0; i < n; ++i) {  // Sphere::new (sphere.rs:16-21)
+    for (uint32_t i = 0; i < n; ++i) {  // Sphere::new / new_moving (sphere.rs:16-21; the_next_week/sphere.rs:14-40)
         const Vec3<T> center = v3(s[i].center_radius);
         const T r = std::max((T)s[i].center_radius[3], T(0));
         const Vec3<T> rvec = mk(r, r, r);
-        w.spheres[i] = Sphere<T>{center, r, s[i].material_index, from_points(center - rvec, center + rvec)};
+        Sphere<T> sp{center, r, s[i].material_index, from_points(center - rvec, center + rvec), mk(T(0), T(0), T(0))};
+        if (motion) {
+            sp.motion = v3(motion + 4 * (size_t)i);
+            w.book2 = w.book2 || motion[4 * i] != 0.0f || motion[4 * i + 1] != 0.0f || motion[4 * i + 2] != 0.0f;
+            const Vec3<T> c2 = mk((T)(s[i].center_radius[0] + motion[4 * i]), (T)(s[i].center_radius[1] + motion[4 * i + 1]),
+                                  (T)(s[i].center_radius[2] + motion[4 * i + 2]));
+            sp.bbox = from_boxes(sp.bbox, from_points(c2 - rvec, c2 + rvec));
+        }
+        w.spheres[i] = sp;
     }
     w.mats.resize(nm);
     for (uint32_t i = 0; i < nm; ++i) {
@@ -555,11 +578,28 @@ void load_world(World<T> &w, Cam<T> &cam, const RrtCamera *c, const RrtSphere *s
         mm.kind = m[i].kind;
         mm.albedo = v3(m[i].albedo_fuzz);
         const T fuzz = (T)m[i].albedo_fuzz[3];
-        mm.fuzz = fuzz < T(1) ? fuzz : T(1);  // Metal::new (material.rs:48-50)
+        mm.w = fuzz;
+        mm.fuzz = (mm.kind == RRT_MAT_METAL && !(fuzz < T(1))) ? T(1) : fuzz;  // Metal::new (material.rs:48-50)
         mm.ref_idx = (T)m[i].ref_idx;
         mm.tex = m[i]._pad[0];
+        float g, b;
+        std::memcpy(&g, &m[i]._pad[0], 4);
+        std::memcpy(&b, &m[i]._pad[1], 4);
+        mm.odd = mk((T)m[i].ref_idx, (T)g, (T)b);
+        if (mm.kind == RRT_MAT_CHECKER_LAMBERTIAN || mm.kind == RRT_MAT_NOISE_LAMBERTIAN) w.book2 = true;
     }
     for (uint32_t i = 0; i < ntex; ++i) w.texs.push_back(Texture{tex[i].rgb8, tex[i].width, tex[i].height});
+    if (ext && ext->perlin)
+        for (uint32_t t = 0; t < ext->n_perlin; ++t) {
+            PerlinT<T> pt;
+            for (int i = 0; i < 256; ++i) {
+                pt.randvec[i] = v3(ext->perlin[t].randvec[i]);
+                pt.perm_x[i] = ext->perlin[t].perm_x[i] & 255u;
+                pt.perm_y[i] = ext->perlin[t].perm_y[i] & 255u;
+                pt.perm_z[i] = ext->perlin[t].perm_z[i] & 255u;
+            }
+            w.perlin.push_back(pt);
+        }
     if (n) {
         std::vector<int32_t> objs(n);
         for (uint32_t i = 0; i < n; ++i) objs[i] = (int32_t)i;
@@ -574,23 +614,25 @@ template <class T> struct Record {
 };
 
 template <class T>
-bool world_hit(const World<T> &w, Vec3<T> o, Vec3<T> d, Record<T> &rec, uint64_t *tests,
+bool world_hit(const World<T> &w, Vec3<T> o, Vec3<T> d, T time, Record<T> &rec, uint64_t *tests,
                const KTree *kt = nullptr) {  // camera.rs:187
     Hit<T> h;
     if constexpr (std::is_same_v<T, float>) {
         if (kt) {
-            if (!kbvh_hit(w, *kt, o, d, h, tests)) return false;
+            if (!kbvh_hit(w, *kt, o, d, time, h, tests)) return false;
         } else {
             if (w.root.index < 0) return false;
-            if (!w.hit(w.root, o, d, Interval<T>{L(0.001), std::numeric_limits<T>::infinity()}, h, tests)) return false;
+            if (!w.hit(w.root, o, d, time, Interval<T>{L(0.001), std::numeric_limits<T>::infinity()}, h, tests))
+                return false;
         }
     } else {
         if (w.root.index < 0) return false;
-        if (!w.hit(w.root, o, d, Interval<T>{L(0.001), std::numeric_limits<T>::infinity()}, h, tests)) return false;
+        if (!w.hit(w.root, o, d, time, Interval<T>{L(0.001), std::numeric_limits<T>::infinity()}, h, tests)) return false;
     }
     const Sphere<T> &s = w.spheres[h.sphere];
-    rec.p = o + h.t * d;                         // Ray::at
-    rec.outward = (rec.p - s.center) / s.radius;  // sphere.rs:48
+    const Vec3<T> center = w.book2 ? s.at(time) : s.center;
+    rec.p = o + h.t * d;                      // Ray::at
+    rec.outward = (rec.p - center) / s.radius;  // sphere.rs:48 (current_center: the_next_week/sphere.rs:64)
     rec.front = dot(d, rec.outward) < T(0);       // hittable.rs:28-29
     rec.normal = rec.front ? rec.outward : -rec.outward;
     rec.mat = s.mat;
@@ -626,17 +668,102 @@ Vec3<T> texture_value(const World<T> &w, uint32_t tex, Vec3<T> outward) {
     return mk(cs * (T)px[0], cs * (T)px[1], cs * (T)px[2]);
 }
 
+// ---- book-2 procedural textures (the_next_week/texture.rs:39-77, 111-126; perlin.rs) -------
+// f32 twin: Cephes sinf, the kernel's rrt_sinf op for op; f64 books: libm sin.
+float cephes_sinf(float xx) {
+    float x = xx;
+    float sign = 1.0f;
+    if (x < 0.0f) { sign = -1.0f; x = -x; }
+    if (x > 16777215.0f) return 0.0f;
+    if (!(x == x)) return xx;
+    int j = (int)(1.27323954473516f * x);
+    float y = (float)j;
+    if (j & 1) { j += 1; y += 1.0f; }
+    j &= 7;
+    if (j > 3) { sign = -sign; j -= 4; }
+    if (x > 8192.0f) x = x - y * 0.7853981633974483096f;
+    else x = ((x - y * 0.78515625f) - y * 2.4187564849853515625e-4f) - y * 3.77489497744594108e-8f;
+    const float z = x * x;
+    if (j == 1 || j == 2) {
+        y = ((2.443315711809948e-5f * z - 1.388731625493765e-3f) * z + 4.166664568298827e-2f) * z * z;
+        y = y - 0.5f * z;
+        y = y + 1.0f;
+    } else {
+        y = ((-1.9515295891e-4f * z + 8.3321608736e-3f) * z - 1.6666654611e-1f) * z * x;
+        y = y + x;
+    }
+    return sign < 0.0f ? -y : y;
+}
+template <class T> T t_sin(T x) { if constexpr (std::is_same_v<T, float>) return cephes_sinf(x); else return std::sin(x); }
+
+template <class T> int32_t floor_as_i32(T x) {  // `x.floor() as i32`: saturating, NaN -> 0
+    const T f = std::floor(x);
+    if (!(f == f)) return 0;
+    if (f <= (T)-2147483648.0) return INT32_MIN;
+    if (f >= (T)2147483647.0) return INT32_MAX;
+    return (int32_t)f;
+}
+
+template <class T> T perlin_noise(const PerlinT<T> &pt, Vec3<T> p) {  // perlin.rs:25-48, 84-102
+    const T u = p.x() - std::floor(p.x());
+    const T v = p.y() - std::floor(p.y());
+    const T w = p.z() - std::floor(p.z());
+    const int32_t i = floor_as_i32(p.x()), j = floor_as_i32(p.y()), k = floor_as_i32(p.z());
+    const T uu = u * u * (T(3) - T(2) * u);
+    const T vv = v * v * (T(3) - T(2) * v);
+    const T ww = w * w * (T(3) - T(2) * w);
+    T accum = T(0);
+    for (int di = 0; di < 2; ++di)
+        for (int dj = 0; dj < 2; ++dj)
+            for (int dk = 0; dk < 2; ++dk) {
+                const uint32_t idx = pt.perm_x[(uint32_t)(i + di) & 255u] ^ pt.perm_y[(uint32_t)(j + dj) & 255u] ^
+                                     pt.perm_z[(uint32_t)(k + dk) & 255u];
+                const Vec3<T> c = pt.randvec[idx];
+                const Vec3<T> wv = mk(u - (T)di, v - (T)dj, w - (T)dk);
+                const T fi = (T)di * uu + (T(1) - (T)di) * (T(1) - uu);
+                const T fj = (T)dj * vv + (T(1) - (T)dj) * (T(1) - vv);
+                const T fk = (T)dk * ww + (T(1) - (T)dk) * (T(1) - ww);
+                accum += fi * fj * fk * dot(c, wv);
+            }
+    return accum;
+}
+
+template <class T> T noise_value(const PerlinT<T> &pt, T scale, Vec3<T> p) {  // texture.rs:119-123, perlin.rs:50-62
+    T accum = T(0), weight = T(1);
+    Vec3<T> tp = p;
+    for (int o = 0; o < 7; ++o) {
+        accum += weight * perlin_noise(pt, tp);
+        weight *= L(0.5);
+        tp = tp * T(2);
+    }
+    const T turb = std::fabs(accum);
+    return L(0.5) * (T(1) + t_sin<T>(scale * p.z() + T(10) * turb));
+}
+
+template <class T> bool checker_even(T inv_scale, Vec3<T> p) {  // texture.rs:66-77
+    const int32_t x = floor_as_i32(inv_scale * p.x()), y = floor_as_i32(inv_scale * p.y()), z = floor_as_i32(inv_scale * p.z());
+    const int32_t sum = (int32_t)((uint32_t)x + (uint32_t)y + (uint32_t)z);
+    return sum % 2 == 0;
+}
+
 // Material::scatter (material.rs:28-102; book 2 material.rs:41-53). Returns false for None.
 template <class T>
 bool scatter(const World<T> &w, PathRng &rng, Vec3<T> d_in, const Record<T> &rec, Vec3<T> &att, Vec3<T> &dir) {
     const Material<T> &m = w.mats[rec.mat];
     switch (m.kind) {
         case RRT_MAT_LAMBERTIAN:
-        case RRT_MAT_TEXTURED_LAMBERTIAN: {
+        case RRT_MAT_TEXTURED_LAMBERTIAN:
+        case RRT_MAT_CHECKER_LAMBERTIAN:
+        case RRT_MAT_NOISE_LAMBERTIAN: {
             Vec3<T> sd = rec.normal + random_unit_vector<T>(rng);
             if (near_zero(sd)) sd = rec.normal;
             dir = sd;
-            att = m.kind == RRT_MAT_LAMBERTIAN ? m.albedo : texture_value(w, m.tex, rec.outward);
+            if (m.kind == RRT_MAT_TEXTURED_LAMBERTIAN) att = texture_value(w, m.tex, rec.outward);
+            else if (m.kind == RRT_MAT_CHECKER_LAMBERTIAN) att = checker_even(m.w, rec.p) ? m.albedo : m.odd;
+            else if (m.kind == RRT_MAT_NOISE_LAMBERTIAN) {
+                const T g = noise_value(w.perlin[m.tex], m.w, rec.p);
+                att = mk(g, g, g);
+            } else att = m.albedo;
             return true;
         }
         case RRT_MAT_METAL: {
@@ -698,11 +825,12 @@ struct Tally {
 
 // BOOKS: Camera::ray_color (camera.rs:182-209 / the_next_week/camera.rs:174-201), recursive.
 template <class T>
-Vec3<T> ray_color_books(const World<T> &w, const Cam<T> &cam, PathRng &rng, Vec3<T> o, Vec3<T> d, int depth, Tally &tl) {
+Vec3<T> ray_color_books(const World<T> &w, const Cam<T> &cam, PathRng &rng, Vec3<T> o, Vec3<T> d, T time, int depth,
+                        Tally &tl) {
     if (depth <= 0) return mk(T(0), T(0), T(0));
     tl.rays++;
     Record<T> rec;
-    if (!world_hit(w, o, d, rec, &tl.tests)) return miss_color(cam, d);
+    if (!world_hit(w, o, d, time, rec, &tl.tests)) return miss_color(cam, d);
     const Vec3<T> em = emitted(w, rec);
     Vec3<T> att, dir;
     if (!scatter(w, rng, d, rec, att, dir)) return em;
@@ -710,20 +838,20 @@ Vec3<T> ray_color_books(const World<T> &w, const Cam<T> &cam, PathRng &rng, Vec3
     if (bounces >= 5) {
         const T p = rr_probability(att);
         if (rng.random_double<T>() > p) return em;
-        return em + att * ray_color_books(w, cam, rng, rec.p, dir, depth - 1, tl) / p;
+        return em + att * ray_color_books(w, cam, rng, rec.p, dir, time, depth - 1, tl) / p;
     }
-    return em + att * ray_color_books(w, cam, rng, rec.p, dir, depth - 1, tl);
+    return em + att * ray_color_books(w, cam, rng, rec.p, dir, time, depth - 1, tl);
 }
 
 // TWIN: the same path, throughput front-to-back (the HIP kernel's order, rrt_kernel.hip).
 template <class T>
-Vec3<T> ray_color_twin(const World<T> &w, const Cam<T> &cam, PathRng &rng, Vec3<T> o, Vec3<T> d, Tally &tl,
+Vec3<T> ray_color_twin(const World<T> &w, const Cam<T> &cam, PathRng &rng, Vec3<T> o, Vec3<T> d, T time, Tally &tl,
                        const KTree *kt = nullptr) {
     Vec3<T> Tp = mk(T(1), T(1), T(1)), Lp = mk(T(0), T(0), T(0));
     for (uint32_t k = 0; k < cam.max_depth; ++k) {
         tl.rays++;
         Record<T> rec;
-        if (!world_hit(w, o, d, rec, &tl.tests, kt)) return Lp + Tp * miss_color(cam, d);
+        if (!world_hit(w, o, d, time, rec, &tl.tests, kt)) return Lp + Tp * miss_color(cam, d);
         const Material<T> &m = w.mats[rec.mat];
         if (m.kind == RRT_MAT_DIFFUSE_LIGHT) return Lp + Tp * m.albedo;
         Vec3<T> att, dir;
@@ -743,7 +871,7 @@ Vec3<T> ray_color_twin(const World<T> &w, const Cam<T> &cam, PathRng &rng, Vec3<
 
 // Camera::get_ray (camera.rs:152-169, the_next_week/camera.rs:148-163)
 template <class T>
-void get_ray(const Cam<T> &cam, PathRng &rng, uint32_t i, uint32_t j, Vec3<T> &o, Vec3<T> &d) {
+void get_ray(const Cam<T> &cam, PathRng &rng, uint32_t i, uint32_t j, Vec3<T> &o, Vec3<T> &d, T &time) {
     const T ox = rng.random_double<T>() - L(0.5);
     const T oy = rng.random_double<T>() - L(0.5);
     const Vec3<T> pixel_sample = cam.p00 + ((T)i + ox) * cam.du + ((T)j + oy) * cam.dv;
@@ -754,16 +882,18 @@ void get_ray(const Cam<T> &cam, PathRng &rng, uint32_t i, uint32_t j, Vec3<T> &o
         o = cam.center + (p[0] * cam.disk_u) + (p[1] * cam.disk_v);
     }
     d = pixel_sample - o;
-    if (cam.flags & RRT_FLAG_RAY_TIME) (void)rng.random_double<T>();
+    time = T(0);
+    if (cam.flags & RRT_FLAG_RAY_TIME) time = rng.random_double<T>();  // the_next_week/camera.rs:160
 }
 
 template <class T>
 int render(const RrtCamera *c, const RrtSphere *s, uint32_t n, const RrtMaterial *m, uint32_t nm, const RrtTexture *tex,
-           uint32_t ntex, uint32_t flags, int mode, uint32_t y0, uint32_t y1, uint32_t s0, uint32_t s1, int threads,
-           double *accum, uint64_t *rays_out, uint64_t *tests_out, uint32_t chunk, const KTree *kt = nullptr) {
+           uint32_t ntex, const RrtSceneExt *ext, uint32_t flags, int mode, uint32_t y0, uint32_t y1, uint32_t s0,
+           uint32_t s1, int threads, double *accum, uint64_t *rays_out, uint64_t *tests_out, uint32_t chunk,
+           const KTree *kt = nullptr) {
     World<T> w;
     Cam<T> cam;
-    load_world(w, cam, c, s, n, m, nm, tex, ntex, flags);
+    load_world(w, cam, c, s, n, m, nm, tex, ntex, flags, ext);
     if (y1 > cam.height) y1 = cam.height;
     if (y0 > y1) return -1;
     std::atomic<uint32_t> next_row{y0};
@@ -786,9 +916,10 @@ int render(const RrtCamera *c, const RrtSphere *s, uint32_t n, const RrtMaterial
                     for (uint32_t sidx = c0; sidx < std::min(s1, c0 + step); ++sidx) {
                         PathRng rng{splitmix64(key + sidx)};
                         Vec3<T> o, d;
-                        get_ray(cam, rng, i, j, o, d);
-                        csum = csum + ((mode & 0xff) == 1 ? ray_color_books(w, cam, rng, o, d, (int)cam.max_depth, tl)
-                                                          : ray_color_twin(w, cam, rng, o, d, tl, kt));
+                        T time;
+                        get_ray(cam, rng, i, j, o, d, time);
+                        csum = csum + ((mode & 0xff) == 1 ? ray_color_books(w, cam, rng, o, d, time, (int)cam.max_depth, tl)
+                                                          : ray_color_twin(w, cam, rng, o, d, time, tl, kt));
                     }
                     sum = (c0 == s0) ? csum : sum + csum;
                 }
@@ -850,20 +981,22 @@ extern "C" {
 // chunk = the accum summation chunk (rrt_accum_chunk; 0 = one chunk),
 // samples [s0,s1) into accum[(y1-y0)*W*4] (double; TWIN values are exact f32 sums).
 int oracle_render(const RrtCamera *cam, const RrtSphere *s, uint32_t n, const RrtMaterial *m, uint32_t nm,
-                  const RrtTexture *tex, uint32_t ntex, uint32_t flags, int mode, uint32_t y0, uint32_t y1,
-                  uint32_t s0, uint32_t s1, int threads, double *accum, uint64_t *rays, uint64_t *sphere_tests,
-                  uint32_t chunk) {
+                  const RrtTexture *tex, uint32_t ntex, const RrtSceneExt *ext, uint32_t flags, int mode, uint32_t y0,
+                  uint32_t y1, uint32_t s0, uint32_t s1, int threads, double *accum, uint64_t *rays,
+                  uint64_t *sphere_tests, uint32_t chunk) {
     if (!cam || !accum) return -1;
     if ((mode & 0xff) == 1)
-        return render<double>(cam, s, n, m, nm, tex, ntex, flags, mode, y0, y1, s0, s1, threads, accum, rays, sphere_tests, chunk);
-    return render<float>(cam, s, n, m, nm, tex, ntex, flags, mode & ~0xff, y0, y1, s0, s1, threads, accum, rays,
+        return render<double>(cam, s, n, m, nm, tex, ntex, ext, flags, mode, y0, y1, s0, s1, threads, accum, rays,
+                              sphere_tests, chunk);
+    return render<float>(cam, s, n, m, nm, tex, ntex, ext, flags, mode & ~0xff, y0, y1, s0, s1, threads, accum, rays,
                          sphere_tests, chunk);
 }
 
 // mode 2 = KBVH: TWIN arithmetic, but closest hits found by walking the kernel's BVH
 // (rrt_build_bvh output: `nodes` of n_nodes x 64 B (width 2) or 128 B (width 4), `order`).
 int oracle_render_kbvh(const RrtCamera *cam, const RrtSphere *s, uint32_t n, const RrtMaterial *m, uint32_t nm,
-                       const RrtTexture *tex, uint32_t ntex, uint32_t flags, const void *nodes, uint32_t n_nodes,
+                       const RrtTexture *tex, uint32_t ntex, const RrtSceneExt *ext, uint32_t flags, const void *nodes,
+                       uint32_t n_nodes,
                        uint32_t width, const uint32_t *order, uint32_t y0, uint32_t y1, uint32_t s0, uint32_t s1,
                        int threads, double *accum, uint64_t *rays, uint64_t *sphere_tests, uint32_t chunk) {
     if (!cam || !accum || !nodes || (width != 2 && width != 4)) return -1;
@@ -872,8 +1005,8 @@ int oracle_render_kbvh(const RrtCamera *cam, const RrtSphere *s, uint32_t n, con
     kt.nodes = static_cast<const uint8_t *>(nodes);
     kt.n_nodes = n_nodes;
     kt.order = order;
-    return render<float>(cam, s, n, m, nm, tex, ntex, flags, 0, y0, y1, s0, s1, threads, accum, rays, sphere_tests, chunk,
-                         &kt);
+    return render<float>(cam, s, n, m, nm, tex, ntex, ext, flags, 0, y0, y1, s0, s1, threads, accum, rays, sphere_tests,
+                         chunk, &kt);
 }
 
 // gpu::build_in_one_weekend_scene's sphere/material list (no overrides, camera seed out).
@@ -973,7 +1106,7 @@ int oracle_sphere_hit(int f32, const double *center, double radius, const double
         w.spheres.push_back(Sphere<T>{c, r, 0, from_points(c - mk(r, r, r), c + mk(r, r, r))});
         const Vec3<T> O = mk((T)o[0], (T)o[1], (T)o[2]), D = mk((T)d[0], (T)d[1], (T)d[2]);
         T t;
-        if (!w.hit_sphere(0, O, D, Interval<T>{(T)tmin, (T)tmax}, t, nullptr)) return 0;
+        if (!w.hit_sphere(0, O, D, T(0), Interval<T>{(T)tmin, (T)tmax}, t, nullptr)) return 0;
         const Vec3<T> p = O + t * D;
         const Vec3<T> out = (p - c) / r;
         const bool front = dot(D, out) < T(0);
@@ -1021,6 +1154,33 @@ void oracle_path_stream(uint32_t seed, uint32_t pixel, uint32_t sample, uint32_t
 void oracle_acos_atan2_f32(float x, float y, float *acos_out, float *atan2_out) {
     *acos_out = cephes_acosf(x);
     *atan2_out = cephes_atan2f(y, x);
+}
+
+// Known-answer hooks for book-2 textures: f32 Cephes sin, and the Perlin noise / NoiseTexture
+// value / checker parity at points p[n][3] with table `pt` (f32 != 0: twin arithmetic).
+void oracle_sin_f32(uint32_t n, const float *x, float *out) {
+    for (uint32_t i = 0; i < n; ++i) out[i] = cephes_sinf(x[i]);
+}
+
+void oracle_book2_textures(int f32, const RrtPerlin *pt, double scale, double inv_scale, uint32_t n, const double *p,
+                           double *noise_out, double *value_out, int32_t *even_out) {
+    auto run = [&](auto tag) {
+        using T = decltype(tag);
+        PerlinT<T> t;
+        for (int i = 0; i < 256; ++i) {
+            t.randvec[i] = mk((T)pt->randvec[i][0], (T)pt->randvec[i][1], (T)pt->randvec[i][2]);
+            t.perm_x[i] = pt->perm_x[i] & 255u;
+            t.perm_y[i] = pt->perm_y[i] & 255u;
+            t.perm_z[i] = pt->perm_z[i] & 255u;
+        }
+        for (uint32_t k = 0; k < n; ++k) {
+            const Vec3<T> q = mk((T)p[3 * k], (T)p[3 * k + 1], (T)p[3 * k + 2]);
+            noise_out[k] = (double)perlin_noise(t, q);
+            value_out[k] = (double)noise_value(t, (T)scale, q);
+            even_out[k] = checker_even((T)inv_scale, q) ? 1 : 0;
+        }
+    };
+    if (f32) run(0.0f); else run(0.0);
 }
 
 }  // extern "C"

@@ -64,12 +64,25 @@ EXPORTED_SYMBOLS = (
     "rrt_quantize_accum_async",
     "rrt_format_pnm_from_rgb8",
     "rrt_write_pnm_from_rgb8",
+    "rrt_hip_render_ex",
+    "rrt_scene_create_ex",
+    "rrt_build_bvh_ex",
+    "rrt_build_next_week_scene",
     "rrt_device_count",
 )
 
 
 class RrtTexture(ctypes.Structure):
     _fields_ = [("rgb8", POINTER(c_uint8)), ("width", c_int32), ("height", c_int32)]
+
+
+# == RrtPerlin (include/rrt_hip.h): 256 x float4 random vectors + 3 x 256 u16 permutations (+pad)
+PERLIN_DTYPE = np.dtype([("randvec", "<f4", (256, 4)), ("perm_x", "<u2", 256), ("perm_y", "<u2", 256),
+                         ("perm_z", "<u2", 256), ("_pad", "<u2", 256)])
+
+
+class RrtSceneExt(ctypes.Structure):
+    _fields_ = [("sphere_motion", c_void_p), ("perlin", c_void_p), ("n_perlin", c_uint32), ("_pad", c_uint32)]
 
 
 class RrtOverrides(ctypes.Structure):
@@ -185,9 +198,16 @@ def load() -> ctypes.CDLL:
         "rrt_quantize_accum_async": (c_int32, [c_uint32, P, c_uint32, P, P]),
         "rrt_format_pnm_from_rgb8": (c_int32, [c_uint32, c_uint32, P, c_int32, P, c_size_t, P]),
         "rrt_write_pnm_from_rgb8": (c_int32, [c_uint32, c_uint32, P, c_int32, c_char_p]),
+        "rrt_hip_render_ex": (c_int32, [P, P, c_uint32, P, c_uint32, P, c_uint32, P, c_uint32, c_uint32, c_uint32, P]),
+        "rrt_scene_create_ex": (c_int32, [P, P, c_uint32, P, c_uint32, P, c_uint32, P, c_uint32, c_int32, P]),
+        "rrt_build_bvh_ex": (c_int32, [P, c_uint32, P, c_uint32, c_uint32, P, c_size_t, P, P]),
+        "rrt_build_next_week_scene": (c_int32, [c_int32, P, c_uint64, P, P, P, P, c_uint32, P, P, c_uint32, P]),
         "rrt_device_count": (c_int32, [P]),
     }
+    experiment = "RRT_LIB_PATH" in os.environ  # A/B of older builds: tolerate symbols they lack
     for name, (res, args) in sig.items():
+        if experiment and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -71,6 +71,16 @@ struct SmallRng {
     uint32_t next_u32() { return (uint32_t)(next_u64() >> 32); }
     float gen_f32() { return (float)(next_u32() >> 8) * (1.0f / 16777216.0f); }          // Standard f32
     double gen_f64() { return (double)(next_u64() >> 11) * (1.0 / 9007199254740992.0); }  // Standard f64
+    double gen_range_f64(double lo, double hi) {  // UniformFloat<f64>::sample_single
+        const double scale = hi - lo;
+        for (;;) {
+            const uint64_t bits = (next_u64() >> 12) | (1023ull << 52);
+            double v12;
+            std::memcpy(&v12, &bits, 8);
+            const double res = (v12 - 1.0) * scale + lo;
+            if (res < hi) return res;
+        }
+    }
     float gen_range_f32(float lo, float hi) {  // UniformFloat<f32>::sample_single
         const float scale = hi - lo;
         for (;;) {
@@ -499,10 +509,11 @@ void bvh_defaults(uint32_t &width, uint32_t &max_leaf) {
     if (const char *e = std::getenv("RRT_BVH_WIDTH")) width = std::atoi(e) == 4 ? 4 : 2;
 }
 
-// Sphere boxes (sphere.rs:16-21, aabb.rs:29-34: r = max(radius, 0), padded), SAH build,
-// flatten. order[i] = original index of the i-th primitive in leaf order.
-FlatBvh build_bvh(const RrtSphere *spheres, uint32_t n_spheres, uint32_t width, uint32_t max_leaf,
-                  std::vector<uint32_t> &order) {
+// Sphere boxes (sphere.rs:16-21, aabb.rs:29-34: r = max(radius, 0), padded; a moving sphere's
+// box spans both ends, the_next_week/sphere.rs:31-33), SAH build, flatten. order[i] = original
+// index of the i-th primitive in leaf order.
+FlatBvh build_bvh(const RrtSphere *spheres, uint32_t n_spheres, const float *motion, uint32_t width,
+                  uint32_t max_leaf, std::vector<uint32_t> &order) {
     std::vector<Aabb> boxes(n_spheres);
     for (uint32_t i = 0; i < n_spheres; ++i) {
         const double r = std::max((double)spheres[i].center_radius[3], 0.0);
@@ -510,6 +521,10 @@ FlatBvh build_bvh(const RrtSphere *spheres, uint32_t n_spheres, uint32_t width, 
         for (int a = 0; a < 3; ++a) {
             const double c = spheres[i].center_radius[a];
             b.ax[a] = Interval{c - r, c + r};
+            if (motion) {  // center2 = center1 + motion (f32 sum, as the kernel's t = 1 end)
+                const double c2 = (double)(spheres[i].center_radius[a] + motion[4 * (size_t)i + a]);
+                b.ax[a] = iv_union(b.ax[a], Interval{c2 - r, c2 + r});
+            }
         }
         boxes[i] = pad(b);
     }
@@ -539,6 +554,8 @@ struct RrtScene {
     uint8_t *d_nodes = nullptr;
     float4 *d_prim_cr = nullptr;
     rrt::GMaterial *d_prim_mtl = nullptr;
+    float4 *d_prim_motion = nullptr;
+    rrt::GPerlin *d_perlin = nullptr;
     uint8_t *d_tex_pool = nullptr;
     rrt::GTexture *d_texs = nullptr;
     unsigned long long *d_counters = nullptr;       // 5 x u64, render launches
@@ -558,6 +575,8 @@ void free_scene(RrtScene *s) {
     (void)hipFree(s->d_nodes);
     (void)hipFree(s->d_prim_cr);
     (void)hipFree(s->d_prim_mtl);
+    (void)hipFree(s->d_prim_motion);
+    (void)hipFree(s->d_perlin);
     (void)hipFree(s->d_tex_pool);
     (void)hipFree(s->d_texs);
     (void)hipFree(s->d_counters);
@@ -649,10 +668,27 @@ int32_t rrt_device_count(int32_t *count) {
     return RRT_OK;
 }
 
-int32_t rrt_scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint32_t n_spheres,
-                         const RrtMaterial *materials, uint32_t n_materials, const RrtTexture *textures,
-                         uint32_t n_textures, uint32_t flags, int32_t device, RrtScene **out) {
+}  // extern "C"
+
+static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint32_t n_spheres,
+                            const RrtMaterial *materials, uint32_t n_materials, const RrtTexture *textures,
+                            uint32_t n_textures, const RrtSceneExt *ext, uint32_t flags, int32_t device,
+                            RrtScene **out) {
     if (!cam || !out) return fail(RRT_E_INVALID, "null camera or out pointer");
+    const float *motion = ext ? ext->sphere_motion : nullptr;
+    const uint32_t n_perlin = ext && ext->perlin ? ext->n_perlin : 0u;
+    bool has_motion = false;
+    if (motion)
+        for (size_t i = 0; i < (size_t)n_spheres * 4 && !has_motion; ++i)
+            has_motion = (i % 4 != 3) && motion[i] != 0.0f;
+    if (has_motion && !(flags & RRT_FLAG_RAY_TIME))
+        return fail(RRT_E_INVALID, "moving spheres need RRT_FLAG_RAY_TIME (rays carry the camera's time draw)");
+    // Book-2 scenes (moving spheres or checker / noise materials) take the kernel variant that
+    // supports them; it reads a motion row per sphere (zero for static spheres).
+    bool book2 = has_motion;
+    for (uint32_t i = 0; i < n_materials && materials; ++i)
+        book2 = book2 || materials[i].kind == RRT_MAT_CHECKER_LAMBERTIAN || materials[i].kind == RRT_MAT_NOISE_LAMBERTIAN;
+    if (!has_motion) motion = nullptr;
     if (n_spheres && !spheres) return fail(RRT_E_INVALID, "null spheres");
     if (n_materials && !materials) return fail(RRT_E_INVALID, "null materials");
     if (n_textures && !textures) return fail(RRT_E_INVALID, "null textures");
@@ -664,10 +700,12 @@ int32_t rrt_scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint32_
         if (spheres[i].material_index >= n_materials)
             return fail(RRT_E_INVALID, "sphere " + std::to_string(i) + " material_index out of range");
     for (uint32_t i = 0; i < n_materials; ++i) {
-        if (materials[i].kind > RRT_MAT_DIFFUSE_LIGHT)
+        if (materials[i].kind > RRT_MAT_NOISE_LAMBERTIAN)
             return fail(RRT_E_INVALID, "material " + std::to_string(i) + " has unknown kind");
         if (materials[i].kind == RRT_MAT_TEXTURED_LAMBERTIAN && materials[i]._pad[0] >= n_textures)
             return fail(RRT_E_INVALID, "material " + std::to_string(i) + " texture index out of range");
+        if (materials[i].kind == RRT_MAT_NOISE_LAMBERTIAN && materials[i]._pad[0] >= n_perlin)
+            return fail(RRT_E_INVALID, "material " + std::to_string(i) + " Perlin table index out of range");
     }
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(RRT_E_NODEV, "no HIP device available");
@@ -676,8 +714,9 @@ int32_t rrt_scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint32_
     // ---- BVH over the sphere bounding boxes ----
     uint32_t width, max_leaf;
     bvh_defaults(width, max_leaf);
+    if (book2) width = 2;  // the book-2 kernel variants are BVH2 only
     std::vector<uint32_t> order;
-    const FlatBvh fb = build_bvh(spheres, n_spheres, width, max_leaf, order);
+    const FlatBvh fb = build_bvh(spheres, n_spheres, motion, width, max_leaf, order);
     if (fb.stack_need > (uint32_t)rrt::kMaxStackDepth)
         return fail(RRT_E_INVALID, "BVH depth " + std::to_string(fb.max_depth) + " exceeds the LDS stack");
     // postponed leaf tests pack (first primitive, count) as first | count << 28
@@ -691,17 +730,32 @@ int32_t rrt_scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint32_
         int ref_bits;
         std::memcpy(&ref_bits, &m.ref_idx, 4);
         mats[i].a = make_float4(m.albedo_fuzz[0], m.albedo_fuzz[1], m.albedo_fuzz[2], fuzz);
-        mats[i].b = make_int4((int)m.kind, ref_bits, (int)m._pad[0], 0);
+        mats[i].b = make_int4((int)m.kind, ref_bits, (int)m._pad[0], (int)m._pad[1]);
     }
     // Spheres in BVH leaf order, each with a copy of its material record: a hit reads one
     // 32-B record at the primitive's index (no dependent material-index fetch).
     std::vector<float4> prim_cr(n_spheres);
     std::vector<rrt::GMaterial> prim_mtl(n_spheres);
+    std::vector<float4> prim_motion(book2 ? n_spheres : 0, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
     for (uint32_t i = 0; i < n_spheres; ++i) {
         const RrtSphere &sp = spheres[order[i]];
         prim_cr[i] = make_float4(sp.center_radius[0], sp.center_radius[1], sp.center_radius[2],
                                  std::max(sp.center_radius[3], 0.0f));
         prim_mtl[i] = mats[sp.material_index];
+        if (motion) {
+            const float *m = motion + 4 * (size_t)order[i];
+            prim_motion[i] = make_float4(m[0], m[1], m[2], 0.0f);
+        }
+    }
+    std::vector<rrt::GPerlin> perlin(n_perlin);
+    for (uint32_t t = 0; t < n_perlin; ++t) {
+        const RrtPerlin &src = ext->perlin[t];
+        for (int i = 0; i < 256; ++i) {
+            if (src.perm_x[i] > 255 || src.perm_y[i] > 255 || src.perm_z[i] > 255)
+                return fail(RRT_E_INVALID, "Perlin permutation entry > 255");
+            perlin[t].randvec[i] = make_float4(src.randvec[i][0], src.randvec[i][1], src.randvec[i][2], 0.0f);
+            perlin[t].perm[i] = (uint32_t)src.perm_x[i] | ((uint32_t)src.perm_y[i] << 8) | ((uint32_t)src.perm_z[i] << 16);
+        }
     }
     std::vector<rrt::GTexture> texs(n_textures);
     size_t pool = 0;
@@ -726,6 +780,8 @@ int32_t rrt_scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint32_
         if ((rc = upload(&s->d_nodes, fb.bytes.data(), fb.bytes.size(), "nodes"))) break;
         if ((rc = upload(&s->d_prim_cr, prim_cr.data(), prim_cr.size(), "spheres"))) break;
         if ((rc = upload(&s->d_prim_mtl, prim_mtl.data(), prim_mtl.size(), "sphere materials"))) break;
+        if (book2 && (rc = upload(&s->d_prim_motion, prim_motion.data(), prim_motion.size(), "sphere motion"))) break;
+        if (n_perlin && (rc = upload(&s->d_perlin, perlin.data(), perlin.size(), "Perlin tables"))) break;
         if ((rc = upload(&s->d_tex_pool, tex_pool.data(), tex_pool.size(), "textures"))) break;
         if ((rc = upload(&s->d_texs, texs.data(), texs.size(), "texture table"))) break;
         if (hipMalloc((void **)&s->d_counters, 8 * sizeof(unsigned long long)) != hipSuccess ||
@@ -749,6 +805,9 @@ int32_t rrt_scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint32_
     p.nodes = s->d_nodes;
     p.prim_cr = s->d_prim_cr;
     p.prim_mtl = s->d_prim_mtl;
+    p.prim_motion = s->d_prim_motion;
+    p.perlin = s->d_perlin;
+    p.n_perlin = n_perlin;
     p.tex_pool = s->d_tex_pool;
     p.texs = s->d_texs;
     p.counters = s->d_counters;
@@ -773,7 +832,8 @@ int32_t rrt_scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint32_
     p.n_prims = n_spheres;
     p.stack_depth = fb.stack_need;
     p.bvh_width = fb.width;
-    const size_t scene_bytes = fb.bytes.size() + (size_t)n_spheres * rrt::kPrimBytes;
+    const size_t scene_bytes =
+        fb.bytes.size() + (size_t)n_spheres * (rrt::kPrimBytes + (book2 ? rrt::kMotionBytes : 0));
     p.scene_in_lds = scene_bytes <= rrt::kLdsSceneBudget;
     if (const char *e = std::getenv("RRT_SCENE_IN_LDS")) p.scene_in_lds = p.scene_in_lds && std::atoi(e) != 0;
     p.trav_frac = 32;
@@ -797,21 +857,49 @@ int32_t rrt_scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint32_
     bi.node_bytes = fb.bytes.size();
     bi.width = fb.width;
     bi.max_leaf_param = max_leaf;
-    bi.prim_bytes = (uint64_t)n_spheres * rrt::kPrimBytes;
+    bi.prim_bytes = (uint64_t)n_spheres * (rrt::kPrimBytes + (book2 ? rrt::kMotionBytes : 0));
     *out = s;
     return RRT_OK;
 }
 
+extern "C" {
+
+int32_t rrt_scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint32_t n_spheres,
+                         const RrtMaterial *materials, uint32_t n_materials, const RrtTexture *textures,
+                         uint32_t n_textures, uint32_t flags, int32_t device, RrtScene **out) {
+    return scene_create(cam, spheres, n_spheres, materials, n_materials, textures, n_textures, nullptr, flags, device,
+                        out);
+}
+
+int32_t rrt_scene_create_ex(const RrtCamera *cam, const RrtSphere *spheres, uint32_t n_spheres,
+                            const RrtMaterial *materials, uint32_t n_materials, const RrtTexture *textures,
+                            uint32_t n_textures, const RrtSceneExt *ext, uint32_t flags, int32_t device,
+                            RrtScene **out) {
+    return scene_create(cam, spheres, n_spheres, materials, n_materials, textures, n_textures, ext, flags, device,
+                        out);
+}
+
 int32_t rrt_build_bvh(const RrtSphere *spheres, uint32_t n_spheres, uint32_t width, uint32_t max_leaf,
                       void *nodes_out, size_t nodes_cap, uint32_t *prim_order_out, RrtBvhInfo *info) {
+    return rrt_build_bvh_ex(spheres, n_spheres, nullptr, width, max_leaf, nodes_out, nodes_cap, prim_order_out, info);
+}
+
+int32_t rrt_build_bvh_ex(const RrtSphere *spheres, uint32_t n_spheres, const float *motion, uint32_t width,
+                         uint32_t max_leaf, void *nodes_out, size_t nodes_cap, uint32_t *prim_order_out,
+                         RrtBvhInfo *info) {
     if (n_spheres && !spheres) return fail(RRT_E_INVALID, "null spheres");
+    if (motion) {  // same rule as scene creation: an all-zero motion array is a static scene
+        bool any = false;
+        for (size_t i = 0; i < (size_t)n_spheres * 4 && !any; ++i) any = (i % 4 != 3) && motion[i] != 0.0f;
+        if (!any) motion = nullptr;
+    }
     uint32_t dw, dl;
     bvh_defaults(dw, dl);
     if (width == 0) width = dw;
     if (max_leaf == 0) max_leaf = dl;
     if ((width != 2 && width != 4) || max_leaf > 15) return fail(RRT_E_INVALID, "width must be 2 or 4, max_leaf <= 15");
     std::vector<uint32_t> order;
-    const FlatBvh fb = build_bvh(spheres, n_spheres, width, max_leaf, order);
+    const FlatBvh fb = build_bvh(spheres, n_spheres, motion, width, max_leaf, order);
     if (info) {
         *info = RrtBvhInfo{};
         info->n_nodes = fb.n_nodes;
@@ -819,7 +907,7 @@ int32_t rrt_build_bvh(const RrtSphere *spheres, uint32_t n_spheres, uint32_t wid
         info->max_depth = fb.max_depth;
         info->max_leaf_size = fb.max_leaf;
         info->node_bytes = fb.bytes.size();
-        info->prim_bytes = (uint64_t)n_spheres * rrt::kPrimBytes;
+        info->prim_bytes = (uint64_t)n_spheres * (rrt::kPrimBytes + (motion ? rrt::kMotionBytes : 0));
         info->width = fb.width;
         info->max_leaf_param = max_leaf;
     }
@@ -920,8 +1008,8 @@ int32_t rrt_scene_count_work(RrtScene *scene, const RrtTile *tile, RrtCounters *
 // (rgb8_out, quantised on the device) assembled into the caller's image.
 static int32_t render_frame(const RrtCamera *cam, const RrtSphere *spheres, uint32_t n_spheres,
                             const RrtMaterial *materials, uint32_t n_materials, const RrtTexture *textures,
-                            uint32_t n_textures, uint32_t total_spp, uint32_t n_gpus, uint32_t flags,
-                            float *accum_out, uint8_t *rgb8_out) {
+                            uint32_t n_textures, const RrtSceneExt *ext, uint32_t total_spp, uint32_t n_gpus,
+                            uint32_t flags, float *accum_out, uint8_t *rgb8_out) {
     if (!cam || (!accum_out && !rgb8_out)) return fail(RRT_E_INVALID, "null camera or output buffer");
     if (total_spp == 0) total_spp = (uint32_t)std::max(cam->params_f[3], 1.0f);  // cuda/mod.rs:384
     int ndev = 0;
@@ -945,8 +1033,8 @@ static int32_t render_frame(const RrtCamera *cam, const RrtSphere *spheres, uint
             }
         };
         RrtScene *scene = nullptr;
-        int rc = rrt_scene_create(cam, spheres, n_spheres, materials, n_materials, textures, n_textures, flags,
-                                  (int32_t)g, &scene);
+        int rc = scene_create(cam, spheres, n_spheres, materials, n_materials, textures, n_textures, ext, flags,
+                              (int32_t)g, &scene);
         if (rc) return set_err(rc);
         const RrtTile tile{16u, g, n_gpus, 0u, total_spp};
         const uint32_t rows = tile_rows_of(height, tile);
@@ -1017,8 +1105,17 @@ int32_t rrt_hip_render(const RrtCamera *cam, const RrtSphere *spheres, uint32_t 
                        uint32_t n_textures, uint32_t total_spp, uint32_t n_gpus, uint32_t flags,
                        float *accum_out) {
     if (!accum_out) return fail(RRT_E_INVALID, "null camera or accum_out");
-    return render_frame(cam, spheres, n_spheres, materials, n_materials, textures, n_textures, total_spp, n_gpus,
-                        flags, accum_out, nullptr);
+    return render_frame(cam, spheres, n_spheres, materials, n_materials, textures, n_textures, nullptr, total_spp,
+                        n_gpus, flags, accum_out, nullptr);
+}
+
+int32_t rrt_hip_render_ex(const RrtCamera *cam, const RrtSphere *spheres, uint32_t n_spheres,
+                          const RrtMaterial *materials, uint32_t n_materials, const RrtTexture *textures,
+                          uint32_t n_textures, const RrtSceneExt *ext, uint32_t total_spp, uint32_t n_gpus,
+                          uint32_t flags, float *accum_out) {
+    if (!accum_out) return fail(RRT_E_INVALID, "null camera or accum_out");
+    return render_frame(cam, spheres, n_spheres, materials, n_materials, textures, n_textures, ext, total_spp,
+                        n_gpus, flags, accum_out, nullptr);
 }
 
 int32_t rrt_hip_render_rgb8(const RrtCamera *cam, const RrtSphere *spheres, uint32_t n_spheres,
@@ -1026,8 +1123,8 @@ int32_t rrt_hip_render_rgb8(const RrtCamera *cam, const RrtSphere *spheres, uint
                             uint32_t n_textures, uint32_t total_spp, uint32_t n_gpus, uint32_t flags,
                             uint8_t *rgb8_out) {
     if (!rgb8_out) return fail(RRT_E_INVALID, "null camera or rgb8_out");
-    return render_frame(cam, spheres, n_spheres, materials, n_materials, textures, n_textures, total_spp, n_gpus,
-                        flags, nullptr, rgb8_out);
+    return render_frame(cam, spheres, n_spheres, materials, n_materials, textures, n_textures, nullptr, total_spp,
+                        n_gpus, flags, nullptr, rgb8_out);
 }
 
 int32_t rrt_quantize_accum_async(uint32_t n_pixels, const float *d_accum, uint32_t samples_per_pixel, uint8_t *d_rgb8,
@@ -1184,6 +1281,145 @@ int32_t rrt_build_in_one_weekend_scene(const RrtOverrides *ov, uint64_t seed, in
         return fail(RRT_E_INVALID, "sphere_cap too small (need " + std::to_string(sph.size()) + ")");
     std::memcpy(spheres, sph.data(), sph.size() * sizeof(RrtSphere));
     std::memcpy(materials, mat.data(), mat.size() * sizeof(RrtMaterial));
+    return RRT_OK;
+}
+
+// ---- book-2 scenes (the_next_week/mod.rs:83-255) -----------------------------------------
+// The reference draws from the thread-local entropy RNG (rtweekend.rs:9-30); here the same
+// draws, in the same order, come from SmallRng(seed): random_double() = gen_range(0.0..1.0),
+// random_double_range = gen_range(min..max), random_int(min,max) = random_double_range(min,
+// max+1) as i32 (rtweekend.rs:17-30). Parity unpinned (entropy RNG).
+int32_t rrt_build_next_week_scene(int32_t scene, const RrtOverrides *ov, uint64_t seed, RrtCamera *cam,
+                                  RrtSphere *spheres, RrtMaterial *materials, float *motion, uint32_t sphere_cap,
+                                  uint32_t *n_spheres, RrtPerlin *perlin, uint32_t perlin_cap, uint32_t *n_perlin) {
+    if (!n_spheres || !n_perlin) return fail(RRT_E_INVALID, "null n_spheres or n_perlin");
+    if (scene < 1 || scene > 4)
+        return fail(RRT_E_INVALID, "book-2 scene must be 1 bouncing_spheres, 2 checkered_spheres, 3 earth, 4 perlin_spheres");
+    // Camera (the_next_week/mod.rs:137-150, 177-190, 203-216, 237-250)
+    double aspect_ratio = 16.0 / 9.0;
+    int32_t image_width = 400, samples_per_pixel = 100, max_depth = 50;
+    double vfov = 20.0;
+    double lookfrom[3] = {13.0, 2.0, 3.0}, lookat[3] = {0.0, 0.0, 0.0}, vup[3] = {0.0, 1.0, 0.0};
+    double defocus_angle = 0.0, focus_dist = 10.0;
+    double background[3] = {0.70, 0.80, 1.00};
+    int32_t has_bg = 1;
+    if (scene == 1) defocus_angle = 0.6;
+    if (scene == 3) lookfrom[0] = 0.0, lookfrom[1] = 0.0, lookfrom[2] = 12.0;
+    rrt_apply_overrides(ov, 2, &aspect_ratio, &image_width, &samples_per_pixel, &max_depth, &vfov, lookfrom, lookat,
+                        vup, &defocus_angle, &focus_dist, background, &has_bg);
+
+    SmallRng rng(seed);
+    auto random_double = [&]() { return rng.gen_range_f64(0.0, 1.0); };
+    auto random_range = [&](double lo, double hi) { return rng.gen_range_f64(lo, hi); };
+    std::vector<RrtSphere> sph;
+    std::vector<RrtMaterial> mat;
+    std::vector<float> mot;
+    std::vector<RrtPerlin> tables;
+    auto bits = [](float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; };
+    auto add_material = [&](uint32_t kind, float r, float g, float b, float w, float ref_idx, uint32_t p0, uint32_t p1) {
+        RrtMaterial m{};
+        put4(m.albedo_fuzz, r, g, b, w);
+        m.kind = kind;
+        m.ref_idx = ref_idx;
+        m._pad[0] = p0;
+        m._pad[1] = p1;
+        mat.push_back(m);
+        return (uint32_t)(mat.size() - 1);
+    };
+    // CheckerTexture::from_colors(0.32, (.2,.3,.1), (.9,.9,.9)) (mod.rs:86-90): inv_scale = 1/scale
+    auto checker = [&]() {
+        return add_material(RRT_MAT_CHECKER_LAMBERTIAN, 0.2f, 0.3f, 0.1f, (float)(1.0 / 0.32), 0.9f, bits(0.9f),
+                            bits(0.9f));
+    };
+    auto add_sphere = [&](D3 c, double r, uint32_t m, D3 move) {
+        RrtSphere s{};
+        put4(s.center_radius, (float)c.x, (float)c.y, (float)c.z, (float)r);
+        s.material_index = m;
+        sph.push_back(s);
+        mot.insert(mot.end(), {(float)move.x, (float)move.y, (float)move.z, 0.0f});
+    };
+    const D3 still = d3(0.0, 0.0, 0.0);
+    if (scene == 1) {  // bouncing_spheres (mod.rs:83-135)
+        add_sphere(d3(0.0, -1000.0, 0.0), 1000.0, checker(), still);
+        for (int a = -11; a < 11; ++a) {
+            for (int b = -11; b < 11; ++b) {
+                const double choose_mat = random_double();
+                const double cx = (double)a + 0.9 * random_double();
+                const double cz = (double)b + 0.9 * random_double();
+                const D3 center = d3(cx, 0.2, cz);
+                if (length(center - d3(4.0, 0.2, 0.0)) > 0.9) {
+                    if (choose_mat < 0.8) {
+                        double c1[3], c2[3];  // Color::random() * Color::random()
+                        for (double &v : c1) v = random_double();
+                        for (double &v : c2) v = random_double();
+                        const uint32_t m = add_material(RRT_MAT_LAMBERTIAN, (float)(c1[0] * c2[0]), (float)(c1[1] * c2[1]),
+                                                        (float)(c1[2] * c2[2]), 0.0f, 1.0f, 0, 0);
+                        const D3 center2 = center + d3(0.0, random_double() * 0.5, 0.0);
+                        add_sphere(center, 0.2, m, center2 - center);  // Sphere::new_moving
+                    } else if (choose_mat < 0.95) {
+                        double al[3];
+                        for (double &v : al) v = random_range(0.5, 1.0);
+                        const double fuzz = random_double() * 0.5;
+                        add_sphere(center, 0.2,
+                                   add_material(RRT_MAT_METAL, (float)al[0], (float)al[1], (float)al[2], (float)fuzz,
+                                                1.0f, 0, 0),
+                                   still);
+                    } else {
+                        add_sphere(center, 0.2, add_material(RRT_MAT_DIELECTRIC, 1, 1, 1, 0, 1.5f, 0, 0), still);
+                    }
+                }
+            }
+        }
+        add_sphere(d3(0.0, 1.0, 0.0), 1.0, add_material(RRT_MAT_DIELECTRIC, 1, 1, 1, 0, 1.5f, 0, 0), still);
+        add_sphere(d3(-4.0, 1.0, 0.0), 1.0, add_material(RRT_MAT_LAMBERTIAN, 0.4f, 0.2f, 0.1f, 0, 1.0f, 0, 0), still);
+        add_sphere(d3(4.0, 1.0, 0.0), 1.0, add_material(RRT_MAT_METAL, 0.7f, 0.6f, 0.5f, 0.0f, 1.0f, 0, 0), still);
+    } else if (scene == 2) {  // checkered_spheres (mod.rs:157-175)
+        add_sphere(d3(0.0, -10.0, 0.0), 10.0, checker(), still);
+        add_sphere(d3(0.0, 10.0, 0.0), 10.0, checker(), still);
+    } else if (scene == 3) {  // earth (mod.rs:196-201): the image is texture 0
+        add_sphere(d3(0.0, 0.0, 0.0), 2.0, add_material(RRT_MAT_TEXTURED_LAMBERTIAN, 0, 0, 0, 0, 1.0f, 0, 0), still);
+    } else {  // perlin_spheres (mod.rs:222-235): one NoiseTexture(4) shared by both spheres
+        RrtPerlin t{};
+        for (int i = 0; i < 256; ++i) {  // Perlin::new (perlin.rs:12-22)
+            double v[3];
+            for (double &x : v) x = random_range(-1.0, 1.0);
+            const D3 u = unit_vector(d3(v[0], v[1], v[2]));
+            t.randvec[i][0] = (float)u.x;
+            t.randvec[i][1] = (float)u.y;
+            t.randvec[i][2] = (float)u.z;
+        }
+        for (uint16_t *perm : {t.perm_x, t.perm_y, t.perm_z}) {  // perlin_generate_perm / permute (perlin.rs:70-82)
+            for (int i = 0; i < 256; ++i) perm[i] = (uint16_t)i;
+            for (int i = 255; i > 0; --i) {
+                const int target = (int)random_range(0.0, (double)(i + 1));
+                std::swap(perm[i], perm[target]);
+            }
+        }
+        tables.push_back(t);
+        add_sphere(d3(0.0, -1000.0, 0.0), 1000.0, add_material(RRT_MAT_NOISE_LAMBERTIAN, 0.5f, 0.5f, 0.5f, 4.0f, 1.0f, 0, 0),
+                   still);
+        add_sphere(d3(0.0, 2.0, 0.0), 2.0, add_material(RRT_MAT_NOISE_LAMBERTIAN, 0.5f, 0.5f, 0.5f, 4.0f, 1.0f, 0, 0),
+                   still);
+    }
+    const uint32_t sample_seed = rng.next_u32();
+    *n_spheres = (uint32_t)sph.size();
+    *n_perlin = (uint32_t)tables.size();
+    if (cam) {
+        int rc = rrt_make_camera(aspect_ratio, image_width, samples_per_pixel, max_depth, vfov, lookfrom, lookat, vup,
+                                 defocus_angle, focus_dist, has_bg ? background : nullptr, sample_seed,
+                                 (uint32_t)sph.size(), cam);
+        if (rc) return rc;
+    }
+    if (perlin_cap) {
+        if (perlin_cap < tables.size() || !perlin) return fail(RRT_E_INVALID, "perlin_cap too small");
+        if (!tables.empty()) std::memcpy(perlin, tables.data(), tables.size() * sizeof(RrtPerlin));
+    }
+    if (sphere_cap == 0) return RRT_OK;
+    if (sphere_cap < sph.size() || !spheres || !materials)
+        return fail(RRT_E_INVALID, "sphere_cap too small (need " + std::to_string(sph.size()) + ")");
+    std::memcpy(spheres, sph.data(), sph.size() * sizeof(RrtSphere));
+    std::memcpy(materials, mat.data(), mat.size() * sizeof(RrtMaterial));
+    if (motion) std::memcpy(motion, mot.data(), mot.size() * sizeof(float));
     return RRT_OK;
 }
 

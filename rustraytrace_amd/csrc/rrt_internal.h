@@ -40,6 +40,13 @@ struct alignas(16) GMaterial {
     int4 b;
 };
 
+// Perlin tables on the device (the_next_week/perlin.rs:4-22): the 256 random unit vectors
+// and the three permutations packed per index: perm_x | perm_y << 8 | perm_z << 16.
+struct alignas(16) GPerlin {
+    float4 randvec[256];
+    uint32_t perm[256];
+};
+
 struct GTexture {
     int32_t offset;  // byte offset into the texture pool
     int32_t width;
@@ -52,6 +59,8 @@ struct KParams {
     const void *nodes;           // GNode[] (bvh_width 2) or GNode4[] (bvh_width 4)
     const float4 *prim_cr;       // sphere center.xyz, radius — in BVH leaf order
     const GMaterial *prim_mtl;   // each primitive's material record, same order (one fetch per hit)
+    const float4 *prim_motion;   // (center2 - center1).xyz per primitive, same order; null = static scene
+    const GPerlin *perlin;       // Perlin tables (noise textures)
     const uint8_t *tex_pool;
     const GTexture *texs;
     float4 *accum;               // tile-local rows * width
@@ -85,6 +94,7 @@ struct KParams {
 
     uint32_t n_nodes;
     uint32_t n_prims;
+    uint32_t n_perlin;
     uint32_t stack_depth;   // entries needed (BVH depth + 1)
     uint32_t scene_in_lds;  // stage nodes + spheres + their materials in LDS per block
     uint32_t trav_frac;     // leave the traversal loop when <= live*trav_frac/256 lanes still traverse
@@ -116,6 +126,7 @@ constexpr int kWavesPerSimd = RRT_WAVES;   // launch-bounds occupancy target of 
 // 512-thread block keeps 3 blocks (6 waves/SIMD) within the CU's 160 KB.
 constexpr size_t kLdsSceneBudget = 40 * 1024;
 constexpr size_t kPrimBytes = sizeof(float4) + sizeof(GMaterial);  // per primitive: sphere + material
+constexpr size_t kMotionBytes = sizeof(float4);                     // + motion, scenes with moving spheres
 
 // Launch wrappers implemented in rrt_kernel.hip.
 hipError_t launch_render(const KParams &p, hipStream_t stream);

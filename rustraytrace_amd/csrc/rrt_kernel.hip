@@ -228,13 +228,33 @@ __device__ __forceinline__ float div_by_a(float n, const RayK &rk) {
     return __builtin_fmaf(e1, rk.ra, q1);
 }
 
+// Sphere centers as the sphere test sees them: static, or (book-2 scenes) a moving sphere's
+// center at the ray's time, center1 + time * (center2 - center1) (the_next_week/sphere.rs:44:
+// Ray::at; static book-2 spheres carry a zero motion).
+template <bool kBook2>
+struct Prims {
+    const float4 *cr;
+    const float4 *mo;
+    float time;
+    __device__ __forceinline__ float4 at(int i) const {
+        float4 c = cr[i];
+        if constexpr (kBook2) {
+            const float4 m = mo[i];
+            c.x = c.x + time * m.x;
+            c.y = c.y + time * m.y;
+            c.z = c.z + time * m.z;
+        }
+        return c;
+    }
+};
+
 // Sphere::hit (sphere.rs:24-51) root selection; returns true and shrinks `closest`.
-template <bool kCount>
-__device__ __forceinline__ void test_prims(const float4 *__restrict__ prim_cr, int first, int count, V3 o, V3 d,
+template <bool kCount, class PR>
+__device__ __forceinline__ void test_prims(const PR &prim_cr, int first, int count, V3 o, V3 d,
                                            float a, float &closest, int &hit_prim, Counters &cnt) {
     for (int i = first; i < first + count; ++i) {
         if (kCount) cnt.spheres++;
-        const float4 cr = prim_cr[i];
+        const float4 cr = prim_cr.at(i);
         const V3 oc = v3(cr.x - o.x, cr.y - o.y, cr.z - o.z);
         const float h = dot(d, oc);
         const float c = dot(oc, oc) - cr.w * cr.w;
@@ -252,8 +272,8 @@ __device__ __forceinline__ void test_prims(const float4 *__restrict__ prim_cr, i
 }
 
 // Leaf spheres of two ranges [f0, f0+c0) then [f1, f1+c1) in one loop.
-template <bool kCount>
-__device__ __forceinline__ void test_prims2(const float4 *__restrict__ prim_cr, int f0, int c0, int f1, int c1, V3 o,
+template <bool kCount, class PR>
+__device__ __forceinline__ void test_prims2(const PR &prim_cr, int f0, int c0, int f1, int c1, V3 o,
                                             V3 d, const RayK &rk, float &closest, int &hit_prim, Counters &cnt) {
     const float a = rk.a;
     const int total = c0 + c1;
@@ -264,7 +284,7 @@ __device__ __forceinline__ void test_prims2(const float4 *__restrict__ prim_cr, 
             cnt.d0 += wave_slot();
             cnt.d1 += 1;
         }
-        const float4 cr = prim_cr[i];
+        const float4 cr = prim_cr.at(i);
         const V3 oc = v3(cr.x - o.x, cr.y - o.y, cr.z - o.z);
         const float h = dot(d, oc);
         const float c = dot(oc, oc) - cr.w * cr.w;
@@ -361,8 +381,8 @@ __device__ __forceinline__ bool trav_node(const GNode *__restrict__ nodes, Stack
 }
 
 // The postponed leaf tests of one node visit (leaf 0's spheres, then leaf 1's).
-template <bool kCount>
-__device__ __forceinline__ void trav_leaves(const float4 *__restrict__ prims, const Leaves &lv, V3 o, V3 d,
+template <bool kCount, class PR>
+__device__ __forceinline__ void trav_leaves(const PR &prims, const Leaves &lv, V3 o, V3 d,
                                             const RayK &rk, Trav &t, Counters &cnt) {
     test_prims2<kCount>(prims, (int)(lv.l0 & kLeafFirstMask), (int)(lv.l0 >> 28), (int)(lv.l1 & kLeafFirstMask),
                         (int)(lv.l1 >> 28), o, d, rk, t.closest, t.hit_prim, cnt);
@@ -370,8 +390,8 @@ __device__ __forceinline__ void trav_leaves(const float4 *__restrict__ prims, co
 
 // Visits node t.node: tests both children, tests leaf spheres in place, descends into the
 // nearer internal child and pushes the farther one. Returns true when the traversal is done.
-template <bool kCount, typename Stack>
-__device__ __forceinline__ bool trav_step(const GNode *__restrict__ nodes, const float4 *__restrict__ prims,
+template <bool kCount, typename Stack, class PR>
+__device__ __forceinline__ bool trav_step(const GNode *__restrict__ nodes, const PR &prims,
                                           Stack &stack, V3 o, V3 d, const RayK &rk, Trav &t, Counters &cnt) {
     const GNode n = nodes[t.node];
     if (kCount) { cnt.nodes++; cnt.boxes += 2; }
@@ -405,8 +425,8 @@ __device__ __forceinline__ bool trav_step(const GNode *__restrict__ nodes, const
 
 // BVH4 step: test the 4 child boxes, test leaf children's spheres in place, then descend
 // into the nearest internal child and push the others farthest-first (5-exchange sort).
-template <bool kCount, typename Stack>
-__device__ __forceinline__ bool trav_step4(const GNode4 *__restrict__ nodes, const float4 *__restrict__ prims,
+template <bool kCount, typename Stack, class PR>
+__device__ __forceinline__ bool trav_step4(const GNode4 *__restrict__ nodes, const PR &prims,
                                            Stack &stack, V3 o, V3 d, const RayK &rk, Trav &t, Counters &cnt) {
     const GNode4 n = nodes[t.node];
     if (kCount) { cnt.nodes++; cnt.boxes += 4; }
@@ -470,6 +490,7 @@ struct PathState {
     V3 o, d, T;
     uint64_t rng;
     uint32_t k;  // bounce index (camera ray = 0)
+    float time;  // the camera ray's time draw, kept by every bounce (book 2, moving spheres)
 };
 
 // Camera::get_ray (camera.rs:152-180) for global pixel (x, y) and the path's RNG.
@@ -493,7 +514,8 @@ __device__ __forceinline__ void camera_ray(const KParams &P, uint32_t x, uint32_
                     P.center[1] + P.disk_u[1] * px + P.disk_v[1] * py,
                     P.center[2] + P.disk_u[2] * px + P.disk_v[2] * py);
     }
-    if (P.flags & 0x1u) (void)rnd(ps.rng);  // RRT_FLAG_RAY_TIME
+    ps.time = 0.0f;
+    if (P.flags & 0x1u) ps.time = rnd(ps.rng);  // RRT_FLAG_RAY_TIME (the_next_week/camera.rs:160)
     ps.o = origin;
     ps.d = sub(sample, origin);
     ps.T = v3(1.0f, 1.0f, 1.0f);
@@ -505,6 +527,97 @@ __device__ __forceinline__ void camera_ray(const KParams &P, uint32_t x, uint32_
 __device__ __forceinline__ uint64_t path_rng(const KParams &P, uint32_t x, uint32_t y, uint32_t s) {
     const uint64_t key = splitmix64(((uint64_t)P.seed << 32) ^ (uint64_t)(y * P.width + x));
     return splitmix64(key + s);
+}
+
+// ---- book-2 procedural textures (the_next_week/texture.rs:39-77, 111-126; perlin.rs) --------
+// f32 sin with only + - * and truncation, bit-reproducible by the oracle: Cephes sinf (octant
+// reduction by 4/pi with the three-part pi/4 of DP1..DP3, minimax polynomials on [0, pi/4]).
+// Arguments >= 2^24 - 1 return 0 (Cephes' total-loss bound); NaN propagates.
+__device__ __forceinline__ float rrt_sinf(float xx) {
+    float x = xx;
+    float sign = 1.0f;
+    if (x < 0.0f) { sign = -1.0f; x = -x; }
+    if (x > 16777215.0f) return 0.0f;
+    if (!(x == x)) return xx;
+    int j = (int)(1.27323954473516f * x);
+    float y = (float)j;
+    if (j & 1) { j += 1; y += 1.0f; }
+    j &= 7;
+    if (j > 3) { sign = -sign; j -= 4; }
+    if (x > 8192.0f) x = x - y * 0.7853981633974483096f;
+    else x = ((x - y * 0.78515625f) - y * 2.4187564849853515625e-4f) - y * 3.77489497744594108e-8f;
+    const float z = x * x;
+    if (j == 1 || j == 2) {
+        y = ((2.443315711809948e-5f * z - 1.388731625493765e-3f) * z + 4.166664568298827e-2f) * z * z;
+        y = y - 0.5f * z;
+        y = y + 1.0f;
+    } else {
+        y = ((-1.9515295891e-4f * z + 8.3321608736e-3f) * z - 1.6666654611e-1f) * z * x;
+        y = y + x;
+    }
+    return sign < 0.0f ? -y : y;
+}
+
+// Rust `f32 as i32` of a floored value: saturating, NaN -> 0.
+__device__ __forceinline__ int floor_i32(float x) {
+    const float f = __builtin_floorf(x);
+    if (!(f == f)) return 0;
+    if (f <= -2147483648.0f) return (int)0x80000000;
+    if (f >= 2147483647.0f) return 0x7fffffff;
+    return (int)f;
+}
+
+// Perlin::noise (perlin.rs:25-48) + perlin_interp (perlin.rs:84-102), operation order kept:
+// the (i*uu + (1-i)*(1-uu)) factors are exactly uu or 1-uu for i in {0,1}.
+__device__ __forceinline__ float perlin_noise(const GPerlin *__restrict__ pt, V3 p) {
+    const float fx = __builtin_floorf(p.x), fy = __builtin_floorf(p.y), fz = __builtin_floorf(p.z);
+    const float u = p.x - fx, v = p.y - fy, w = p.z - fz;
+    const int i = floor_i32(p.x), j = floor_i32(p.y), k = floor_i32(p.z);
+    const float uu = u * u * (3.0f - 2.0f * u);
+    const float vv = v * v * (3.0f - 2.0f * v);
+    const float ww = w * w * (3.0f - 2.0f * w);
+    float accum = 0.0f;
+#pragma unroll 1
+    for (int di = 0; di < 2; ++di)
+#pragma unroll 1
+        for (int dj = 0; dj < 2; ++dj)
+#pragma unroll 1
+            for (int dk = 0; dk < 2; ++dk) {
+                const uint32_t px = pt->perm[(uint32_t)(i + di) & 255u] & 0xffu;
+                const uint32_t py = (pt->perm[(uint32_t)(j + dj) & 255u] >> 8) & 0xffu;
+                const uint32_t pz = (pt->perm[(uint32_t)(k + dk) & 255u] >> 16) & 0xffu;
+                const float4 c = pt->randvec[px ^ py ^ pz];
+                const float wx = u - (float)di, wy = v - (float)dj, wz = w - (float)dk;
+                const float fi = di ? uu : 1.0f - uu;
+                const float fj = dj ? vv : 1.0f - vv;
+                const float fk = dk ? ww : 1.0f - ww;
+                accum = accum + fi * fj * fk * (c.x * wx + c.y * wy + c.z * wz);
+            }
+    return accum;
+}
+
+// NoiseTexture::value (texture.rs:119-123): 0.5 * (1 + sin(scale * p.z + 10 * turb(p, 7))),
+// turb (perlin.rs:50-62): |sum of weight * noise(p * 2^i)|, weight halving. The octave and
+// corner loops stay rolled: unrolled (56 corner evaluations) they swamp the megakernel's
+// register allocation.
+__device__ __forceinline__ float noise_value(const GPerlin *__restrict__ pt, float scale, V3 p) {
+    float accum = 0.0f, weight = 1.0f;
+    V3 tp = p;
+#pragma unroll 1
+    for (int o = 0; o < 7; ++o) {
+        accum = accum + weight * perlin_noise(pt, tp);
+        weight = weight * 0.5f;
+        tp = muls(tp, 2.0f);
+    }
+    const float turb = __builtin_fabsf(accum);
+    return 0.5f * (1.0f + rrt_sinf(scale * p.z + 10.0f * turb));
+}
+
+// CheckerTexture::value (texture.rs:66-77) with solid even/odd colours.
+__device__ __forceinline__ bool checker_even(float inv_scale, V3 p) {
+    const int xi = floor_i32(inv_scale * p.x), yi = floor_i32(inv_scale * p.y), zi = floor_i32(inv_scale * p.z);
+    const int sum = (int)((uint32_t)xi + (uint32_t)yi + (uint32_t)zi);  // i32 wrapping add
+    return sum % 2 == 0;
 }
 
 __device__ __forceinline__ V3 texel(const KParams &P, int tex, float u, float v) {
@@ -524,8 +637,8 @@ __device__ __forceinline__ V3 texel(const KParams &P, int tex, float u, float v)
 // After the closest-hit query of the current segment (prim < 0: miss): background, or
 // emission / scatter / RR (camera.rs:182-209). Returns true when the path has ended; a
 // path ending at the sky or an emitter adds T*Le to `sum`.
-template <typename C>
-__device__ __forceinline__ bool shade(const KParams &P, const float4 *prims, const GMaterial *mtl, PathState &ps,
+template <bool kBook2, typename C, class PR>
+__device__ __forceinline__ bool shade(const KParams &P, const PR &prims, const GMaterial *mtl, PathState &ps,
                                       float t, int prim, V3 &sum, C &cnt) {
     if constexpr (RRT_PHASE_TIMING == 4) {
         cnt.d0 += wave_slot();
@@ -544,7 +657,7 @@ __device__ __forceinline__ bool shade(const KParams &P, const float4 *prims, con
         return true;
     }
     // HitRecord (sphere.rs:47-50, hittable.rs:20-32)
-    const float4 cr = prims[prim];
+    const float4 cr = prims.at(prim);  // the sphere's center at the ray's time (sphere.rs:48)
     const V3 p = v3(ps.o.x + ps.d.x * t, ps.o.y + ps.d.y * t, ps.o.z + ps.d.z * t);
     const float inv_r = 1.0f / cr.w;
     const V3 outward = v3((p.x - cr.x) * inv_r, (p.y - cr.y) * inv_r, (p.z - cr.z) * inv_r);
@@ -562,13 +675,19 @@ __device__ __forceinline__ bool shade(const KParams &P, const float4 *prims, con
     // rejection loop for both kinds (a wave mixing them runs it once, not twice).
     V3 r = v3(0.0f, 0.0f, 0.0f);
     if (kind != 2) r = random_unit_vector(ps.rng, cnt);
-    if (kind == 0 || kind == 3) {  // Lambertian (material.rs:28-40)
+    if (kind != 1 && kind != 2) {  // Lambertian, plain or textured (material.rs:28-40; book 2 :41-53)
         dir = add(nrm, r);
         if (__builtin_fabsf(dir.x) < 1e-8f && __builtin_fabsf(dir.y) < 1e-8f && __builtin_fabsf(dir.z) < 1e-8f) dir = nrm;
-        if (kind == 3) {
+        if (kind == 3) {  // ImageTexture at the sphere's (u, v) (sphere.rs:46-52)
             const float theta = rrt_acosf(-outward.y);
             const float phi = rrt_atan2f(-outward.z, outward.x) + kPi;
             att = texel(P, m.b.z, phi / (2.0f * kPi), theta / kPi);
+        } else if (kBook2 && kind == 5) {  // CheckerTexture at p
+            att = checker_even(m.a.w, p) ? v3(m.a.x, m.a.y, m.a.z)
+                                         : v3(__int_as_float(m.b.y), __int_as_float(m.b.z), __int_as_float(m.b.w));
+        } else if (kBook2 && kind == 6) {  // NoiseTexture at p
+            const float g = noise_value(P.perlin + m.b.z, m.a.w, p);
+            att = v3(g, g, g);
         } else {
             att = v3(m.a.x, m.a.y, m.a.z);
         }
@@ -612,7 +731,7 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
     return v;
 }
 
-template <bool kLds, bool kCount, typename StackT, bool kWide>
+template <bool kLds, bool kCount, typename StackT, bool kWide, bool kBook2>
 __device__ __forceinline__ void render_body(const KParams &P) {
     extern __shared__ uint4 lds_dyn[];
     // LDS layout: [traversal stack: stack_depth x kBlock x StackT, 16-B aligned][nodes][primitives]
@@ -621,6 +740,7 @@ __device__ __forceinline__ void render_body(const KParams &P) {
     const Node *nodes = reinterpret_cast<const Node *>(P.nodes);
     const float4 *prims = P.prim_cr;
     const GMaterial *mtl = P.prim_mtl;
+    const float4 *motion = P.prim_motion;
     if constexpr (kLds) {
         // Stage the whole BVH + spheres + their materials (KB-sized) in LDS once per block.
         uint4 *dst = lds_dyn + (P.stack_depth * kBlock * sizeof(StackT) + 15u) / 16u;
@@ -632,10 +752,15 @@ __device__ __forceinline__ void render_body(const KParams &P) {
         const uint4 *src_m = reinterpret_cast<const uint4 *>(P.prim_mtl);
         const uint32_t nm = P.n_prims * (uint32_t)(sizeof(GMaterial) / 16);
         for (uint32_t i = threadIdx.x; i < nm; i += kBlock) dst[nn + P.n_prims + i] = src_m[i];
+        if constexpr (kBook2) {
+            const uint4 *src_v = reinterpret_cast<const uint4 *>(P.prim_motion);
+            for (uint32_t i = threadIdx.x; i < P.n_prims; i += kBlock) dst[nn + P.n_prims + nm + i] = src_v[i];
+        }
         __syncthreads();
         nodes = reinterpret_cast<const Node *>(dst);
         prims = reinterpret_cast<const float4 *>(dst + nn);
         mtl = reinterpret_cast<const GMaterial *>(dst + nn + P.n_prims);
+        if constexpr (kBook2) motion = reinterpret_cast<const float4 *>(dst + nn + P.n_prims + nm);
     }
     LdsStack<StackT> stack;
     stack.init(lds_stack, threadIdx.x);
@@ -731,6 +856,7 @@ __device__ __forceinline__ void render_body(const KParams &P) {
         }
         RayK rk;
         if (tracing) rk = ray_consts(ps.o, ps.d);
+        const Prims<kBook2> pr{prims, motion, ps.time};
         if constexpr (kWide) {
             for (;;) {
                 if constexpr (RRT_PHASE_TIMING == 2) {
@@ -738,7 +864,7 @@ __device__ __forceinline__ void render_body(const KParams &P) {
                     ph1 += (uint64_t)__popcll(__ballot(tracing));
                 }
                 if (tracing) {
-                    if (trav_step4<kCount>(nodes, prims, stack, ps.o, ps.d, rk, tr, cnt)) tracing = false;
+                    if (trav_step4<kCount>(nodes, pr, stack, ps.o, ps.d, rk, tr, cnt)) tracing = false;
                 }
                 if ((uint32_t)__popcll(__ballot(tracing)) <= min_active) break;
             }
@@ -762,7 +888,7 @@ __device__ __forceinline__ void render_body(const KParams &P) {
                 const bool leave = (uint32_t)__popcll(__ballot(tracing)) <= min_active;
                 if (pm != 0 && (leave || (uint32_t)__popcll(pm) > leaf_min || __ballot(tracing && !pend) == 0)) {
                     if (pend) {
-                        trav_leaves<kCount>(prims, lv, ps.o, ps.d, rk, tr, cnt);
+                        trav_leaves<kCount>(pr, lv, ps.o, ps.d, rk, tr, cnt);
                         pend = false;
                         if (tr.node < 0) tracing = false;
                     }
@@ -777,7 +903,7 @@ __device__ __forceinline__ void render_body(const KParams &P) {
         }
         if (has && !need_ray && !tracing) {
             need_ray = true;
-            seg_done = shade(P, prims, mtl, ps, tr.closest, tr.hit_prim, sum, cnt);
+            seg_done = shade<kBook2>(P, Prims<kBook2>{prims, motion, ps.time}, mtl, ps, tr.closest, tr.hit_prim, sum, cnt);
         }
         w_paths += (uint32_t)__popcll(__ballot(seg_done));
         if (seg_done) {  // pixel_color += ray_color(..) (camera.rs:73-76): already in `sum`
@@ -832,9 +958,9 @@ __device__ __forceinline__ void render_body(const KParams &P) {
     }
 }
 
-template <bool kLds, bool kCount, typename StackT, bool kWide, int kWaves>
+template <bool kLds, bool kCount, typename StackT, bool kWide, int kWaves, bool kBook2>
 __global__ __launch_bounds__(kBlock, kWaves) void rrt_render(KParams P) {
-    render_body<kLds, kCount, StackT, kWide>(P);
+    render_body<kLds, kCount, StackT, kWide, kBook2>(P);
 }
 
 // accum[p] = sum over chunks c = 0..n-1 (in order) of partial[p][c].rgb; w = sample count.
@@ -894,12 +1020,15 @@ __global__ __launch_bounds__(256) void rrt_quantize(const float4 *__restrict__ a
     }
 }
 
-template <bool kLds, typename StackT, bool kWide, int kWaves = 1>
+template <bool kLds, typename StackT, bool kWide, bool kBook2, int kWaves = 1>
 hipError_t launch_variant(const KParams &p, bool count, hipStream_t stream) {
     if (p.n_units == 0) return hipSuccess;
     size_t lds = ((size_t)p.stack_depth * kBlock * sizeof(StackT) + 15u) / 16u * 16u;
-    if (kLds) lds += (size_t)p.n_nodes * (kWide ? sizeof(GNode4) : sizeof(GNode)) + (size_t)p.n_prims * kPrimBytes;
-    auto kernel = count ? rrt_render<kLds, true, StackT, kWide, kWaves> : rrt_render<kLds, false, StackT, kWide, kWaves>;
+    if (kLds)
+        lds += (size_t)p.n_nodes * (kWide ? sizeof(GNode4) : sizeof(GNode)) +
+               (size_t)p.n_prims * (kPrimBytes + (kBook2 ? kMotionBytes : 0));
+    auto kernel = count ? rrt_render<kLds, true, StackT, kWide, kWaves, kBook2>
+                        : rrt_render<kLds, false, StackT, kWide, kWaves, kBook2>;
     // Persistent grid: as many blocks as can be resident (occupancy at this LDS size), capped
     // by the work; the queue counter is zeroed on the stream before the launch.
     int per_cu = 0;
@@ -919,13 +1048,14 @@ hipError_t launch_variant(const KParams &p, bool count, hipStream_t stream) {
     return hipGetLastError();
 }
 
-template <bool kWide>
+template <bool kWide, bool kBook2>
 hipError_t launch_width(const KParams &p, bool count, hipStream_t stream) {
     if (p.stack_depth > (uint32_t)kMaxStackDepth) return hipErrorInvalidValue;
-    if (p.n_nodes > 65535u) return launch_variant<false, uint32_t, kWide>(p, count, stream);
-    if (!kWide && p.scene_in_lds && p.min_waves >= 6) return launch_variant<true, uint16_t, kWide, kWavesPerSimd>(p, count, stream);
-    return p.scene_in_lds ? launch_variant<true, uint16_t, kWide>(p, count, stream)
-                          : launch_variant<false, uint16_t, kWide>(p, count, stream);
+    if (p.n_nodes > 65535u) return launch_variant<false, uint32_t, kWide, kBook2>(p, count, stream);
+    if (!kWide && p.scene_in_lds && p.min_waves >= 6)
+        return launch_variant<true, uint16_t, kWide, kBook2, kWavesPerSimd>(p, count, stream);
+    return p.scene_in_lds ? launch_variant<true, uint16_t, kWide, kBook2>(p, count, stream)
+                          : launch_variant<false, uint16_t, kWide, kBook2>(p, count, stream);
 }
 
 }  // namespace
@@ -933,7 +1063,10 @@ hipError_t launch_width(const KParams &p, bool count, hipStream_t stream) {
 hipError_t launch_render_kernel(const KParams &p, bool count, hipStream_t stream) {
     // Variant choice: BVH width, smallest LDS stack that holds the traversal, and the scene
     // staged in LDS when the BVH + spheres fit the per-block budget (RTOW: ~20-26 KB).
-    return p.bvh_width == 4 ? launch_width<true>(p, count, stream) : launch_width<false>(p, count, stream);
+    // Book-2 scenes (moving spheres, checker / noise textures): BVH2 only (the host builds a
+    // binary tree for them); motion is always present (zero for static spheres).
+    if (p.prim_motion) return p.bvh_width == 2 ? launch_width<false, true>(p, count, stream) : hipErrorInvalidValue;
+    return p.bvh_width == 4 ? launch_width<true, false>(p, count, stream) : launch_width<false, false>(p, count, stream);
 }
 
 hipError_t launch_render(const KParams &p, hipStream_t stream) { return launch_render_kernel(p, false, stream); }

@@ -31,17 +31,38 @@ def _textures(scene: SceneData):
     return arr, len(scene.textures), keep
 
 
+def scene_ext(scene: SceneData):
+    """(RrtSceneExt or None, keep-alive list) for the book-2 data of `scene` (motion, Perlin)."""
+    if scene.motion is None and scene.perlin is None:
+        return None, []
+    ext = _lib.RrtSceneExt()
+    keep = []
+    if scene.motion is not None:
+        m = np.ascontiguousarray(scene.motion, dtype=np.float32)
+        assert m.shape == (len(scene.spheres), 4), "motion is (n_spheres, 4) float32"
+        keep.append(m)
+        ext.sphere_motion = m.ctypes.data
+    if scene.perlin is not None:
+        t = np.ascontiguousarray(scene.perlin, dtype=_lib.PERLIN_DTYPE)
+        keep.append(t)
+        ext.perlin = t.ctypes.data
+        ext.n_perlin = len(t)
+    return ext, keep
+
+
 def render(scene: SceneData, spp: Optional[int] = None, n_gpus: int = 1, quiet: bool = True) -> np.ndarray:
     """Render `scene` on `n_gpus` GPUs; returns the RGBA float32 accum (H, W, 4), w = sample count."""
     lib = _lib.load()
     accum = np.zeros((scene.height, scene.width, 4), dtype=np.float32)
     tex, ntex, keep = _textures(scene)
+    ext, keep_ext = scene_ext(scene)
     flags = scene.flags | (_lib.FLAG_QUIET if quiet else 0)
-    _lib.check(lib.rrt_hip_render(_lib.ptr(scene.camera), _lib.ptr(scene.spheres), len(scene.spheres),
-                                  _lib.ptr(scene.materials), len(scene.materials),
-                                  ctypes.cast(tex, ctypes.c_void_p) if tex is not None else None, ntex,
-                                  int(spp or 0), int(n_gpus), flags, _lib.ptr(accum)))
-    del keep
+    _lib.check(lib.rrt_hip_render_ex(_lib.ptr(scene.camera), _lib.ptr(scene.spheres), len(scene.spheres),
+                                     _lib.ptr(scene.materials), len(scene.materials),
+                                     ctypes.cast(tex, ctypes.c_void_p) if tex is not None else None, ntex,
+                                     ctypes.byref(ext) if ext is not None else None,
+                                     int(spp or 0), int(n_gpus), flags, _lib.ptr(accum)))
+    del keep, keep_ext
     return accum
 
 
@@ -149,11 +170,20 @@ def build_bvh(scene: SceneData, width: int = 0, max_leaf: int = 0):
     lib = _lib.load()
     info = _lib.RrtBvhInfo()
     n = len(scene.spheres)
-    _lib.check(lib.rrt_build_bvh(_lib.ptr(scene.spheres), n, width, max_leaf, None, 0, None, ctypes.byref(info)))
+    motion = None if scene.motion is None else np.ascontiguousarray(scene.motion, dtype=np.float32)
+    if scene.motion is not None or scene.perlin is not None or np.isin(scene.materials["kind"], (5, 6)).any():
+        width = 2  # book-2 scenes render with the BVH2 kernel variant (rrt_scene_create_ex)
+    def build(nodes_p, cap, order_p):
+        if motion is None:
+            return lib.rrt_build_bvh(_lib.ptr(scene.spheres), n, width, max_leaf, nodes_p, cap, order_p,
+                                     ctypes.byref(info))
+        return lib.rrt_build_bvh_ex(_lib.ptr(scene.spheres), n, _lib.ptr(motion), width, max_leaf, nodes_p, cap,
+                                    order_p, ctypes.byref(info))
+
+    _lib.check(build(None, 0, None))
     nodes = np.zeros(info.node_bytes, dtype=np.uint8)
     order = np.zeros(max(n, 1), dtype=np.uint32)
-    _lib.check(lib.rrt_build_bvh(_lib.ptr(scene.spheres), n, width, max_leaf, _lib.ptr(nodes), nodes.size,
-                                 _lib.ptr(order), ctypes.byref(info)))
+    _lib.check(build(_lib.ptr(nodes), nodes.size, _lib.ptr(order)))
     return nodes, order[:n], info.as_dict()
 
 
@@ -172,11 +202,17 @@ class DeviceScene:
         self._lib = lib
         self._h = ctypes.c_void_p()
         tex, ntex, keep = _textures(scene)
-        _lib.check(lib.rrt_scene_create(_lib.ptr(scene.camera), _lib.ptr(scene.spheres), len(scene.spheres),
-                                        _lib.ptr(scene.materials), len(scene.materials),
-                                        ctypes.cast(tex, ctypes.c_void_p) if tex is not None else None, ntex,
-                                        scene.flags, int(device), ctypes.byref(self._h)))
-        del keep
+        ext, keep_ext = scene_ext(scene)
+        texp = ctypes.cast(tex, ctypes.c_void_p) if tex is not None else None
+        if ext is None:
+            _lib.check(lib.rrt_scene_create(_lib.ptr(scene.camera), _lib.ptr(scene.spheres), len(scene.spheres),
+                                            _lib.ptr(scene.materials), len(scene.materials), texp, ntex,
+                                            scene.flags, int(device), ctypes.byref(self._h)))
+        else:
+            _lib.check(lib.rrt_scene_create_ex(_lib.ptr(scene.camera), _lib.ptr(scene.spheres), len(scene.spheres),
+                                               _lib.ptr(scene.materials), len(scene.materials), texp, ntex,
+                                               ctypes.byref(ext), scene.flags, int(device), ctypes.byref(self._h)))
+        del keep, keep_ext
 
     def close(self):
         if self._h:

@@ -8,6 +8,9 @@
     C3 rtow_4k         same scene, 3840x2160, 2048 spp (8-GPU tile split)
     C4 earth_light     textured earth + emissive sphere, 1920x1080, 1024 spp
     C5 stress10k       RTOW generator on a 100x100 grid (<=10,004 spheres), 1920x1080, 256 spp
+* `next_week_scene` — book-2 scenes 1-4 (the_next_week/mod.rs:83-255: bouncing_spheres with
+  moving spheres and a checker ground, checkered_spheres, earth, perlin_spheres), flattened by
+  rrt_build_next_week_scene.
 """
 from __future__ import annotations
 
@@ -23,6 +26,8 @@ from . import _lib
 RTOW_SEED = 0x5EED_1234
 C1_SEED = 0xC0FFEE
 C4_SEED = 0xE4A7_0001
+NEXT_WEEK_SEED = 0xB00C_0002
+NEXT_WEEK_SCENES = {1: "bouncing_spheres", 2: "checkered_spheres", 3: "earth", 4: "perlin_spheres"}
 
 # config.rs:50-62 committed OVERRIDES (width 2160, spp 5000, depth 100)
 COMMITTED_OVERRIDES = dict(image_width=2160, samples_per_pixel=5000, max_depth=100)
@@ -38,6 +43,8 @@ class SceneData:
     textures: list = dataclasses.field(default_factory=list)  # uint8 (H, W, 3) arrays
     flags: int = 0
     name: str = ""
+    motion: Optional[np.ndarray] = None  # (n_spheres, 4) float32: center2 - center1 (book 2), or None
+    perlin: Optional[np.ndarray] = None  # PERLIN_DTYPE tables for noise materials, or None
 
     @property
     def width(self) -> int:
@@ -142,6 +149,28 @@ def earth_light(image_width=1920, samples_per_pixel=1024, max_depth=100, seed=C4
                       max_depth=max_depth, vfov=20.0, lookfrom=(0.0, 0.0, 12.0), lookat=(0.0, 0.0, 0.0),
                       background=(0.0, 0.0, 0.0), seed=seed, n_spheres=len(sph))
     return SceneData(cam, sph, mats, textures=[earth_texture()], flags=_lib.FLAG_RAY_TIME, name="earth_light")
+
+
+def next_week_scene(scene: int, overrides: Optional[dict] = None, seed: int = NEXT_WEEK_SEED) -> SceneData:
+    """The book-2 scene `scene` (1 bouncing_spheres, 2 checkered_spheres, 3 earth, 4 perlin_spheres;
+    the_next_week/mod.rs:83-255) under RenderOverrides `overrides`, with its motion rows and Perlin
+    tables. Book-2 camera: background colour, a time draw per camera ray."""
+    lib = _lib.load()
+    ov = _lib.make_overrides(**(overrides or {}))
+    n, nt = ctypes.c_uint32(0), ctypes.c_uint32(0)
+    cam = _empty(_lib.CAMERA_DTYPE, 1)
+    _lib.check(lib.rrt_build_next_week_scene(int(scene), _lib.ptr(ov), seed, _lib.ptr(cam), None, None, None, 0,
+                                             _lib.ptr(n), None, 0, _lib.ptr(nt)))
+    spheres = _empty(_lib.SPHERE_DTYPE, n.value)
+    mats = _empty(_lib.MATERIAL_DTYPE, n.value)
+    motion = np.zeros((n.value, 4), dtype=np.float32)
+    perlin = np.zeros(nt.value, dtype=_lib.PERLIN_DTYPE)
+    _lib.check(lib.rrt_build_next_week_scene(int(scene), _lib.ptr(ov), seed, _lib.ptr(cam), _lib.ptr(spheres),
+                                             _lib.ptr(mats), _lib.ptr(motion), n.value, _lib.ptr(n), _lib.ptr(perlin),
+                                             nt.value, _lib.ptr(nt)))
+    textures = [earth_texture()] if scene == 3 else []
+    return SceneData(cam, spheres, mats, textures=textures, flags=_lib.FLAG_RAY_TIME, name=NEXT_WEEK_SCENES[scene],
+                     motion=motion if np.any(motion[:, :3]) else None, perlin=perlin if nt.value else None)
 
 
 def rtow(image_width=1920, samples_per_pixel=512, max_depth=100, grid_half=11, seed=RTOW_SEED) -> SceneData:

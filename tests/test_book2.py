@@ -1,0 +1,172 @@
+"""Book-2 breadth on the CPU: moving spheres, checker and Perlin-noise
+textures, the book-2 scene builders — the oracle's restatement of the_next_week/{sphere,texture,
+perlin,mod}.rs checked against independent numpy restatements and known answers, and its f32
+twin against its f64 books mode. The GPU side is tests/test_gpu_book2.py.
+
+Parity note: the reference draws scene layouts and Perlin tables from the entropy RNG
+(rtweekend.rs:9-30); rrt_build_next_week_scene draws them from SmallRng(seed) in the same order,
+so these are restatement checks, not reference vectors (parity unpinned, as for book 1)."""
+import math
+
+import numpy as np
+import pytest
+
+import rustraytrace_amd as rrt
+from oracle import oracle
+from rustraytrace_amd.render import build_bvh
+
+
+# ---- f32 sin (Cephes sinf, the kernel's rrt_sinf) ---------------------------------------------
+def test_sin_f32_accuracy():
+    rng = np.random.default_rng(1)
+    x = np.concatenate([np.linspace(-20, 20, 4001), rng.uniform(-8000, 8000, 4000), [0.0, -0.0, 1e-30, math.pi / 2]])
+    x = x.astype(np.float32)
+    got = oracle.sin_f32(x).astype(np.float64)
+    want = np.sin(x.astype(np.float64))
+    small = np.abs(x) < 100
+    assert np.max(np.abs(got - want)[small]) < 2e-7
+    assert np.max(np.abs(got - want)) < 2e-4  # reduction error grows with |x| (|x| up to 8000 here)
+    assert oracle.sin_f32([0.0])[0] == 0.0 and math.isnan(oracle.sin_f32([float("nan")])[0])
+
+
+# ---- Perlin noise / NoiseTexture / CheckerTexture vs an independent numpy restatement --------------
+def numpy_noise(table, p):
+    """perlin.rs:25-48 + 84-102 in float64 numpy."""
+    rv = table["randvec"][:, :3].astype(np.float64)
+    px, py, pz = (table[k].astype(np.int64) for k in ("perm_x", "perm_y", "perm_z"))
+    fl = np.floor(p)
+    u, v, w = p - fl
+    i, j, k = fl.astype(np.int64)
+    uu, vv, ww = u * u * (3 - 2 * u), v * v * (3 - 2 * v), w * w * (3 - 2 * w)
+    acc = 0.0
+    for di in range(2):
+        for dj in range(2):
+            for dk in range(2):
+                c = rv[px[(i + di) & 255] ^ py[(j + dj) & 255] ^ pz[(k + dk) & 255]]
+                wv = np.array([u - di, v - dj, w - dk])
+                acc += ((di * uu + (1 - di) * (1 - uu)) * (dj * vv + (1 - dj) * (1 - vv))
+                        * (dk * ww + (1 - dk) * (1 - ww)) * float(c @ wv))
+    return acc
+
+
+def numpy_value(table, scale, p):
+    acc, weight, tp = 0.0, 1.0, np.array(p, dtype=np.float64)
+    for _ in range(7):
+        acc += weight * numpy_noise(table, tp)
+        weight *= 0.5
+        tp = tp * 2.0
+    return 0.5 * (1.0 + math.sin(scale * p[2] + 10.0 * abs(acc)))
+
+
+def test_perlin_noise_matches_numpy_restatement():
+    sc = rrt.next_week_scene(4)
+    table = sc.perlin[0]
+    rng = np.random.default_rng(7)
+    pts = np.concatenate([rng.uniform(-20, 20, (200, 3)), [[0.0, 0.0, 0.0], [1.5, -2.25, 3.0], [255.5, 256.5, -0.5]]])
+    noise64, value64, _ = oracle.book2_textures(table, pts, f32=False)
+    for k in range(len(pts)):
+        assert noise64[k] == pytest.approx(numpy_noise(table, pts[k]), abs=1e-12)
+        assert value64[k] == pytest.approx(numpy_value(table, 4.0, pts[k]), abs=1e-12)
+    noise32, value32, _ = oracle.book2_textures(table, pts, f32=True)
+    assert np.max(np.abs(noise32 - noise64)) < 1e-5
+    assert np.max(np.abs(value32 - value64)) < 2e-5
+    assert np.all((value64 >= 0) & (value64 <= 1))
+
+
+def test_checker_parity_matches_numpy():
+    sc = rrt.next_week_scene(4)
+    rng = np.random.default_rng(3)
+    pts = np.concatenate([rng.uniform(-5, 5, (500, 3)), [[0.0, 0.0, 0.0], [-0.01, 0.0, 0.0], [0.32, 0.0, 0.0],
+                                                         [0.319, 0.64, -0.33]]])
+    inv = float(np.float32(1.0 / 0.32))
+    _, _, even64 = oracle.book2_textures(sc.perlin[0], pts, inv_scale=inv, f32=False)
+    want = (np.floor(inv * pts).astype(np.int64).sum(axis=1) % 2) == 0  # Rust %: sign of dividend; == 0 alike
+    assert np.array_equal(even64, want)
+    _, _, even32 = oracle.book2_textures(sc.perlin[0], pts, inv_scale=inv, f32=True)
+    assert (even32 == even64).mean() > 0.99  # f32 vs f64 products flip only at cell boundaries
+
+
+# ---- book-2 scene builders (the_next_week/mod.rs:83-255) ------------------------------------------
+def test_next_week_scene_structure():
+    s1 = rrt.next_week_scene(1)
+    assert 484 <= len(s1.spheres) <= 488 and s1.name == "bouncing_spheres"
+    kinds = s1.materials["kind"][s1.spheres["material_index"]]
+    assert kinds[0] == 5  # checker ground
+    mot = s1.motion
+    moving = np.any(mot[:, :3] != 0, axis=1)
+    assert np.all(kinds[moving] == 0)  # only the Lambertian grid spheres move (mod.rs:111-112)
+    assert np.all(mot[moving, 0] == 0) and np.all(mot[moving, 2] == 0)
+    assert np.all((mot[moving, 1] >= 0) & (mot[moving, 1] < 0.5))
+    assert moving.sum() > 300
+    cam = s1.camera
+    assert (s1.width, s1.height, s1.spp, s1.max_depth) == (400, 225, 100, 50)
+    assert int(cam["params_u"][0, 3]) == 1 and np.allclose(cam["background"][0, :3], [0.7, 0.8, 1.0])
+    assert cam["params_f"][0, 0] > 0  # defocus 0.6 at 10
+    assert s1.flags & rrt._lib.FLAG_RAY_TIME
+    for k, n in ((2, 2), (3, 1), (4, 2)):
+        s = rrt.next_week_scene(k)
+        assert len(s.spheres) == n and s.motion is None and s.camera["params_f"][0, 0] == 0.0
+    assert rrt.next_week_scene(3).textures[0].shape == (512, 1024, 3)
+    p = rrt.next_week_scene(4).perlin
+    assert len(p) == 1 and all(sorted(p[0][k].tolist()) == list(range(256)) for k in ("perm_x", "perm_y", "perm_z"))
+    # deterministic per seed; a different seed redraws the layout
+    assert np.array_equal(rrt.next_week_scene(1).spheres, s1.spheres)
+    assert not np.array_equal(rrt.next_week_scene(1, seed=5).spheres["center_radius"], s1.spheres["center_radius"])
+    o = rrt.next_week_scene(2, dict(image_width=64, samples_per_pixel=3, background=(0.1, 0.2, 0.3)))
+    assert (o.width, o.spp) == (64, 3) and np.allclose(o.camera["background"][0, :3], [0.1, 0.2, 0.3])
+    with pytest.raises(rrt.RrtError):
+        rrt.next_week_scene(5)
+
+
+def test_moving_sphere_boxes_span_both_ends():
+    sc = rrt.next_week_scene(1)
+    nodes, order, info = build_bvh(sc)
+    assert info["width"] == 2
+    f = nodes.view(np.float32).reshape(-1, 16)
+    links = nodes.view(np.int32).reshape(-1, 16)[:, 12:16]
+    cr = sc.spheres["center_radius"][order]
+    mo = sc.motion[order]
+    checked = 0
+    for n in range(len(f)):
+        for child, (lo, hi) in enumerate([((0, 2, 4), (1, 3, 5)), ((6, 8, 10), (7, 9, 11))]):
+            cnt = links[n, 2 + child]
+            if cnt <= 0:
+                continue
+            first = links[n, child]
+            blo, bhi = f[n, list(lo)], f[n, list(hi)]
+            for i in range(first, first + cnt):
+                for t in (0.0, 0.5, 0.999):
+                    c = cr[i, :3] + np.float32(t) * mo[i, :3]
+                    assert np.all(blo <= c - cr[i, 3]) and np.all(c + cr[i, 3] <= bhi)
+                checked += 1
+    assert checked == len(sc.spheres)
+
+
+# ---- the oracle's two arithmetics and two trees agree on book-2 scenes -------------------------------
+@pytest.mark.parametrize("scene", [1, 2, 3, 4])
+def test_book2_books_vs_twin_statistical(scene):
+    sc = rrt.next_week_scene(scene, dict(image_width=48, samples_per_pixel=8, max_depth=10))
+    t, rt, _ = oracle.render(sc, oracle.TWIN, threads=8)
+    b, rb, _ = oracle.render(sc, oracle.BOOKS, threads=8)
+    per_chan = np.abs(t - b)[..., :3] / sc.spp
+    assert (per_chan <= 1e-4).mean() > 0.85
+    assert abs(t[..., :3].mean() - b[..., :3].mean()) / b[..., :3].mean() < 0.01
+    assert abs(rt - rb) / rb < 0.01
+
+
+@pytest.mark.parametrize("scene", [1, 2, 4])
+def test_book2_kbvh_agrees_with_books_tree(scene):
+    sc = rrt.next_week_scene(scene, dict(image_width=48, samples_per_pixel=4, max_depth=10))
+    a, ra, _ = oracle.render(sc, oracle.TWIN, threads=4)
+    nodes, order, info = build_bvh(sc)
+    b, rb, _ = oracle.render_kbvh(sc, nodes, order, 2, threads=4)
+    assert np.array_equal(a, b) and ra == rb
+
+
+def test_motion_blur_changes_the_image():
+    # the moving spheres are sampled along their motion: zeroing the motion changes the picture
+    sc = rrt.next_week_scene(1, dict(image_width=48, samples_per_pixel=8, max_depth=6))
+    a, _, _ = oracle.render(sc, oracle.TWIN, threads=8)
+    still = rrt.SceneData(sc.camera, sc.spheres, sc.materials, flags=sc.flags, motion=None)
+    b, _, _ = oracle.render(still, oracle.TWIN, threads=8)
+    assert not np.array_equal(a, b)
