@@ -53,7 +53,7 @@ int main(int argc, char **argv) {
     uint64_t seed = 0x5EED1234ull;
     int grid_half = 11;
     std::string out = "-";
-    bool p6 = false, host_quantise = false;
+    bool p6 = false, host_quantise = false, seed_set = false;
 
     for (int i = 1; i < argc; ++i) {
         std::string a = argv[i];
@@ -80,7 +80,7 @@ int main(int argc, char **argv) {
         else if (a == "--focus_dist") { ov.has_focus_dist = 1; ov.focus_dist = std::atof(next("--focus_dist")); }
         else if (a == "--background") { ov.has_background = parse3(next("--background"), ov.background); }
         else if (a == "--gpus") gpus = (uint32_t)std::atoi(next("--gpus"));
-        else if (a == "--seed") seed = std::strtoull(next("--seed"), nullptr, 0);
+        else if (a == "--seed") { seed = std::strtoull(next("--seed"), nullptr, 0); seed_set = true; }
         else if (a == "--grid_half") grid_half = std::atoi(next("--grid_half"));
         else if (a == "-o") out = next("-o");
         else if (a == "--p6") p6 = true;
@@ -103,32 +103,68 @@ int main(int argc, char **argv) {
         std::fprintf(stderr, "unknown backend '%s': expected hip (aliases: cuda, gpu)\n", backend.c_str());
         return 2;
     }
-    if (!(book == "inoneweekend" || book == "oneweekend" || book == "weekend")) {  // main.rs:59-70
-        std::fprintf(stderr, "HIP backend currently supports in_one_weekend only.\n");
+    const bool book1 = book == "inoneweekend" || book == "oneweekend" || book == "weekend";
+    const bool book2 = book == "thenextweek" || book == "nextweek" || book == "next";  // main.rs:89
+    const int scene = positional.size() > 1 ? std::atoi(positional[1].c_str()) : 0;  // main.rs:55
+    if (book2 && !(scene == 1 || scene == 2 || scene == 4)) {
+        std::fprintf(stderr, "HIP backend supports the_next_week scenes 1 (bouncing_spheres), 2 (checkered_spheres) "
+                             "and 4 (perlin_spheres); scene 3 (earth) needs the texture: use the Python API.\n");
+        return 2;
+    }
+    if (!book1 && !book2) {  // main.rs:59-70
+        std::fprintf(stderr, "HIP backend supports in_one_weekend and the_next_week scenes 1, 2, 4 only.\n");
         return 2;
     }
 
     RrtCamera cam;
-    uint32_t n = 0;
-    if (rrt_build_in_one_weekend_scene(&ov, seed, grid_half, &cam, nullptr, nullptr, 0, &n)) {
-        std::fprintf(stderr, "HIP render failed: %s\n", rrt_hip_last_error());
-        return 1;
+    uint32_t n = 0, n_perlin = 0;
+    std::vector<RrtSphere> spheres;
+    std::vector<RrtMaterial> materials;
+    std::vector<float> motion;
+    std::vector<RrtPerlin> perlin;
+    uint32_t flags = 0;
+    if (book1) {
+        if (rrt_build_in_one_weekend_scene(&ov, seed, grid_half, &cam, nullptr, nullptr, 0, &n)) {
+            std::fprintf(stderr, "HIP render failed: %s\n", rrt_hip_last_error());
+            return 1;
+        }
+        spheres.resize(n);
+        materials.resize(n);
+        if (rrt_build_in_one_weekend_scene(&ov, seed, grid_half, &cam, spheres.data(), materials.data(), n, &n)) {
+            std::fprintf(stderr, "HIP render failed: %s\n", rrt_hip_last_error());
+            return 1;
+        }
+    } else {
+        const uint64_t s2 = seed_set ? seed : 0xB00C0002ull;
+        if (rrt_build_next_week_scene(scene, &ov, s2, &cam, nullptr, nullptr, nullptr, 0, &n, nullptr, 0, &n_perlin)) {
+            std::fprintf(stderr, "HIP render failed: %s\n", rrt_hip_last_error());
+            return 1;
+        }
+        spheres.resize(n);
+        materials.resize(n);
+        motion.resize((size_t)n * 4);
+        perlin.resize(n_perlin);
+        if (rrt_build_next_week_scene(scene, &ov, s2, &cam, spheres.data(), materials.data(), motion.data(), n, &n,
+                                      perlin.data(), n_perlin, &n_perlin)) {
+            std::fprintf(stderr, "HIP render failed: %s\n", rrt_hip_last_error());
+            return 1;
+        }
+        flags = RRT_FLAG_RAY_TIME;  // book-2 camera (the_next_week/camera.rs:160)
     }
-    std::vector<RrtSphere> spheres(n);
-    std::vector<RrtMaterial> materials(n);
-    if (rrt_build_in_one_weekend_scene(&ov, seed, grid_half, &cam, spheres.data(), materials.data(), n, &n)) {
-        std::fprintf(stderr, "HIP render failed: %s\n", rrt_hip_last_error());
-        return 1;
-    }
+    RrtSceneExt ext{};
+    ext.sphere_motion = motion.empty() ? nullptr : motion.data();
+    ext.perlin = perlin.empty() ? nullptr : perlin.data();
+    ext.n_perlin = n_perlin;
     const uint32_t w = (uint32_t)cam.params_f[1], h = (uint32_t)cam.params_f[2];
     const uint32_t spp = (uint32_t)(cam.params_f[3] < 1.0f ? 1.0f : cam.params_f[3]);
     const auto t0 = std::chrono::steady_clock::now();
     std::vector<float> accum;
     std::vector<uint8_t> rgb8;
     int rc;
-    if (host_quantise && !p6) {  // the reference's path: float accum -> render_io P3 on the host
+    if (book2 || (host_quantise && !p6)) {  // float accum -> render_io on the host (book 2: rrt_hip_render_ex)
         accum.resize((size_t)w * h * 4);
-        rc = rrt_hip_render(&cam, spheres.data(), n, materials.data(), n, nullptr, 0, spp, gpus, 0, accum.data());
+        rc = rrt_hip_render_ex(&cam, spheres.data(), n, materials.data(), n, nullptr, 0, &ext, spp, gpus, flags,
+                               accum.data());
     } else {  // render_io quantiser on the device (identical bytes), 3 B/pixel to the host
         rgb8.resize((size_t)w * h * 3);
         rc = rrt_hip_render_rgb8(&cam, spheres.data(), n, materials.data(), n, nullptr, 0, spp, gpus, 0, rgb8.data());
@@ -139,6 +175,15 @@ int main(int argc, char **argv) {
     }
     const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     std::fprintf(stderr, "rendered %ux%u @ %u spp, %u spheres, %u GPU(s) in %.3f s\n", w, h, spp, n, gpus, secs);
+    if (!accum.empty() && p6) {  // book 2 with --p6: quantise on the host, then binary
+        rgb8.resize((size_t)w * h * 3);
+        rc = rrt_quantize_accum(w, h, accum.data(), spp, rgb8.data());
+        accum.clear();
+        if (rc) {
+            std::fprintf(stderr, "HIP render failed: %s\n", rrt_hip_last_error());
+            return 1;
+        }
+    }
     rc = accum.empty() ? rrt_write_pnm_from_rgb8(w, h, rgb8.data(), p6 ? 1 : 0, out.c_str())
                        : rrt_write_ppm_from_accum(w, h, accum.data(), spp, out.c_str());
     if (rc) {
