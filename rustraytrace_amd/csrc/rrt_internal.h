@@ -101,6 +101,7 @@ struct KParams {
     uint32_t leaf_frac;     // run the postponed-leaf loop when > live*leaf_frac/256 lanes wait on leaf tests
     uint32_t bvh_width;     // 2 or 4
     uint32_t min_waves;     // launch-bounds occupancy request (waves per SIMD)
+    uint32_t global_waves;  // the same for scenes read from L2 (not staged in LDS); < 6 = no bound
 
     // persistent work queue: units = (pixel, chunk of `chunk` samples), tile-major
     uint32_t chunk;           // samples per unit

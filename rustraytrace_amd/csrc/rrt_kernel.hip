@@ -1054,6 +1054,8 @@ hipError_t launch_width(const KParams &p, bool count, hipStream_t stream) {
     if (p.n_nodes > 65535u) return launch_variant<false, uint32_t, kWide, kBook2>(p, count, stream);
     if (!kWide && p.scene_in_lds && p.min_waves >= 6)
         return launch_variant<true, uint16_t, kWide, kBook2, kWavesPerSimd>(p, count, stream);
+    if (!kWide && !p.scene_in_lds && p.global_waves >= 6)
+        return launch_variant<false, uint16_t, kWide, kBook2, kWavesPerSimd>(p, count, stream);
     return p.scene_in_lds ? launch_variant<true, uint16_t, kWide, kBook2>(p, count, stream)
                           : launch_variant<false, uint16_t, kWide, kBook2>(p, count, stream);
 }
