@@ -26,7 +26,9 @@
 extern "C" {
 #endif
 
-#define RRT_ABI_VERSION 2u
+/* 1: book 1; 2: RrtSceneExt (motion, Perlin), kinds 5-6; 3: quads in RrtSceneExt, rrt_build_next_week_scene
+ * with separate material / quad outputs. */
+#define RRT_ABI_VERSION 3u
 
 /* ---- scene ABI (== src/gpu/mod.rs:13-42) ------------------------------------------ */
 
@@ -88,15 +90,29 @@ typedef struct RrtPerlin {
     uint16_t _pad[256];
 } RrtPerlin;
 
+/* == Quad (the_next_week/quad.rs:9-41), 64 B: corner q, edge vectors u, v (xyz; w unused) and
+ * its material. Instanced quads (RotateY / Translate, hittable.rs:65-170) are passed already
+ * transformed to world space (rrt_build_next_week_scene bakes make_box + RotateY + Translate). */
+typedef struct RrtQuad {
+    float q[4];
+    float u[4];
+    float v[4];
+    uint32_t material_index;
+    uint32_t _pad[3];
+} RrtQuad;
+
 /* Book-2 scene data beyond the flat sphere/material ABI. NULL = none.
  * sphere_motion: n_spheres x 4 floats, (center2 - center1).xyz of Sphere::new_moving
  * (the_next_week/sphere.rs:24-40; the sphere's center at ray time t is center1 + t*motion;
- * zero = static). Requires RRT_FLAG_RAY_TIME (rays carry the camera's time draw). */
+ * zero = static). Requires RRT_FLAG_RAY_TIME (rays carry the camera's time draw).
+ * quads: n_quads quads (materials: Lambertian, checker, noise, metal, dielectric or light;
+ * not image-textured). */
 typedef struct RrtSceneExt {
     const float *sphere_motion;
     const RrtPerlin *perlin;
     uint32_t n_perlin;
-    uint32_t _pad;
+    uint32_t n_quads;
+    const RrtQuad *quads;
 } RrtSceneExt;
 
 /* Image texture, RGB8 row-major (rtw_image.rs:57-67 `to_rgb8().into_raw()`). Borrowed. */
@@ -241,9 +257,10 @@ int32_t rrt_scene_bvh_info(const RrtScene *scene, RrtBvhInfo *out);
  * (info->node_bytes). Lets a checker walk exactly the tree the kernel walks. */
 int32_t rrt_build_bvh(const RrtSphere *spheres, uint32_t n_spheres, uint32_t width, uint32_t max_leaf,
                       void *nodes_out, size_t nodes_cap, uint32_t *prim_order_out, RrtBvhInfo *info);
-/* The same with moving spheres (motion: n_spheres x 4 floats as RrtSceneExt, or NULL): a moving
- * sphere's box spans both ends of its motion (Aabb::from_boxes, the_next_week/sphere.rs:31-33). */
-int32_t rrt_build_bvh_ex(const RrtSphere *spheres, uint32_t n_spheres, const float *motion, uint32_t width,
+/* The same over the book-2 scene (ext may be NULL): a moving sphere's box spans both ends of its
+ * motion (Aabb::from_boxes, the_next_week/sphere.rs:31-33); quads join the primitives as indices
+ * n_spheres + j (prim_order_out then holds n_spheres + n_quads entries). */
+int32_t rrt_build_bvh_ex(const RrtSphere *spheres, uint32_t n_spheres, const RrtSceneExt *ext, uint32_t width,
                          uint32_t max_leaf, void *nodes_out, size_t nodes_cap, uint32_t *prim_order_out,
                          RrtBvhInfo *info);
 
@@ -258,16 +275,18 @@ int32_t rrt_build_in_one_weekend_scene(const RrtOverrides *ov, uint64_t seed, in
                                        RrtCamera *cam, RrtSphere *spheres, RrtMaterial *materials,
                                        uint32_t sphere_cap, uint32_t *n_spheres);
 
-/* Book-2 scenes (the_next_week/mod.rs:68-255) flattened into the ABI: 1 bouncing_spheres,
- * 2 checkered_spheres, 3 earth, 4 perlin_spheres. Random draws come from SmallRng(seed)
- * in the books' order (the reference uses the entropy RNG: parity unpinned). Writes up to
- * sphere_cap spheres / materials / motion rows (motion may be NULL) and up to perlin_cap
- * Perlin tables; *n_spheres, *n_perlin = counts needed (call with caps 0 to size). The earth
- * texture (scene 3) is material texture index 0: the caller supplies the image. The camera
- * carries book 2's background (bg_mode 1); render with RRT_FLAG_RAY_TIME. */
+/* Book-2 scenes (the_next_week/mod.rs:68-431) flattened into the ABI: 1 bouncing_spheres,
+ * 2 checkered_spheres, 3 earth, 4 perlin_spheres, 5 quads, 6 simple_light, 7 cornell_box.
+ * Random draws come from SmallRng(seed) in the books' order (the reference uses the entropy
+ * RNG: parity unpinned). Writes up to sphere_cap spheres and motion rows (motion may be NULL),
+ * up to material_cap materials, up to quad_cap quads (instanced boxes baked to world space)
+ * and up to perlin_cap Perlin tables; the n_* outputs are the counts needed (call with caps 0
+ * to size). The earth texture (scene 3) is texture index 0: the caller supplies the image.
+ * The camera carries book 2's background (bg_mode 1); render with RRT_FLAG_RAY_TIME. */
 int32_t rrt_build_next_week_scene(int32_t scene, const RrtOverrides *ov, uint64_t seed, RrtCamera *cam,
-                                  RrtSphere *spheres, RrtMaterial *materials, float *motion,
-                                  uint32_t sphere_cap, uint32_t *n_spheres,
+                                  RrtSphere *spheres, float *motion, uint32_t sphere_cap, uint32_t *n_spheres,
+                                  RrtMaterial *materials, uint32_t material_cap, uint32_t *n_materials,
+                                  RrtQuad *quads, uint32_t quad_cap, uint32_t *n_quads,
                                   RrtPerlin *perlin, uint32_t perlin_cap, uint32_t *n_perlin);
 
 /* Camera::initialize (in_one_weekend/camera.rs:102-150) in f64, cast to the f32 ABI as

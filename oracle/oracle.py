@@ -54,6 +54,8 @@ def load() -> ctypes.CDLL:
     lib.oracle_quantize_render_io.argtypes = [c_uint32, P, c_uint32, P]
     lib.oracle_sphere_hit.restype = c_int
     lib.oracle_sphere_hit.argtypes = [c_int, P, c_double, P, P, c_double, c_double, P, P, P]
+    lib.oracle_quad_hit.restype = c_int
+    lib.oracle_quad_hit.argtypes = [c_int, P, P, P, P, P, c_double, c_double, P, P, P]
     lib.oracle_aabb_hit.restype = c_int
     lib.oracle_aabb_hit.argtypes = [c_int, P, P, P, P, c_double, c_double]
     lib.oracle_reflect_refract.restype = None
@@ -82,13 +84,15 @@ class _Tex(ctypes.Structure):
 
 
 class _Ext(ctypes.Structure):  # RrtSceneExt (include/rrt_hip.h)
-    _fields_ = [("sphere_motion", c_void_p), ("perlin", c_void_p), ("n_perlin", c_uint32), ("_pad", c_uint32)]
+    _fields_ = [("sphere_motion", c_void_p), ("perlin", c_void_p), ("n_perlin", c_uint32), ("n_quads", c_uint32),
+                ("quads", c_void_p)]
 
 
 def _ext(scene):
-    """(pointer to RrtSceneExt or None, keep-alive) from the scene's book-2 motion / Perlin data."""
+    """(pointer to RrtSceneExt or None, keep-alive) from the scene's book-2 motion / Perlin / quad data."""
     motion, perlin = getattr(scene, "motion", None), getattr(scene, "perlin", None)
-    if motion is None and perlin is None:
+    quads = getattr(scene, "quads", None)
+    if motion is None and perlin is None and quads is None:
         return None, []
     e, keep = _Ext(), []
     if motion is not None:
@@ -101,6 +105,12 @@ def _ext(scene):
         keep.append(t)
         e.perlin = t.ctypes.data
         e.n_perlin = len(t)
+    if quads is not None:
+        q = np.ascontiguousarray(quads)
+        assert q.dtype.itemsize == 64, "RrtQuad records"
+        keep.append(q)
+        e.quads = q.ctypes.data
+        e.n_quads = len(q)
     keep.append(e)
     return ctypes.cast(ctypes.byref(e), c_void_p), keep
 
@@ -203,6 +213,17 @@ def sphere_hit(center, radius, o, d, tmin=0.001, tmax=float("inf"), f32=False):
     c, oo, dd = (np.asarray(x, np.float64) for x in (center, o, d))
     hit = lib.oracle_sphere_hit(int(f32), _p(c), float(radius), _p(oo), _p(dd), tmin, tmax, ctypes.byref(t), _p(n),
                                 ctypes.byref(front))
+    return (t.value, n, bool(front.value)) if hit else None
+
+
+def quad_hit(q, u, v, o, d, tmin=0.001, tmax=float("inf"), f32=False):
+    """Quad::hit (the_next_week/quad.rs:61-87) -> (t, normal, front_face) or None."""
+    lib = load()
+    t = c_double(0)
+    n = np.zeros(3)
+    front = c_int(0)
+    a = [np.asarray(x, np.float64) for x in (q, u, v, o, d)]
+    hit = lib.oracle_quad_hit(int(f32), *(_p(x) for x in a), tmin, tmax, ctypes.byref(t), _p(n), ctypes.byref(front))
     return (t.value, n, bool(front.value)) if hit else None
 
 

@@ -87,6 +87,9 @@ template <class T> bool near_zero(Vec3<T> v) {  // vec3.rs:38-41
     const T s = L(1e-8);
     return std::fabs(v.e[0]) < s && std::fabs(v.e[1]) < s && std::fabs(v.e[2]) < s;
 }
+template <class T> Vec3<T> cross(Vec3<T> u, Vec3<T> v) {  // vec3.rs cross
+    return mk(u.e[1] * v.e[2] - u.e[2] * v.e[1], u.e[2] * v.e[0] - u.e[0] * v.e[2], u.e[0] * v.e[1] - u.e[1] * v.e[0]);
+}
 template <class T> Vec3<T> reflect(Vec3<T> v, Vec3<T> n) { return v - T(2) * dot(v, n) * n; }  // vec3.rs:201-203
 template <class T> T rmin(T a, T b) { return a < b ? a : b; }  // f64::min with a possibly NaN: returns b
 template <class T> Vec3<T> refract(Vec3<T> uv, Vec3<T> n, T etai_over_etat) {  // vec3.rs:205-210
@@ -176,6 +179,7 @@ template <class T> struct Interval {
     T min, max;
     T size() const { return max - min; }
     bool surrounds(T x) const { return min < x && x < max; }
+    bool contains(T x) const { return min <= x && x <= max; }
     T clamp(T x) const { return x < min ? min : (x > max ? max : x); }
     Interval expand(T delta) const { const T p = delta / T(2); return Interval{min - p, max + p}; }
 };
@@ -238,6 +242,34 @@ template <class T> struct Sphere {
     Vec3<T> motion;  // center2 - center1 (zero: static)
     Vec3<T> at(T time) const { return center + time * motion; }  // Ray::at (ray.rs: orig + t*dir)
 };
+// Quad::new (the_next_week/quad.rs:21-45). The derived plane (normal, D, w) is computed in f64
+// from the stored f32 corner and edges and rounded to T, as rrt_host.cpp does for the kernel.
+template <class T> struct QuadT {
+    Vec3<T> q, u, v, normal, w;
+    T D;
+    uint32_t mat;
+    Aabb<T> bbox;
+};
+template <class T> QuadT<T> make_quad(const RrtQuad &rq) {
+    const Vec3<double> q = mk<double>(rq.q[0], rq.q[1], rq.q[2]), u = mk<double>(rq.u[0], rq.u[1], rq.u[2]),
+                       v = mk<double>(rq.v[0], rq.v[1], rq.v[2]);
+    const Vec3<double> nv = cross(u, v);
+    const Vec3<double> normal = unit_vector(nv);
+    const double dd = dot(normal, q);
+    const Vec3<double> wv = nv / dot(nv, nv);
+    auto cast = [](Vec3<double> a) { return mk<T>((T)a[0], (T)a[1], (T)a[2]); };
+    QuadT<T> qd;
+    qd.q = cast(q);
+    qd.u = cast(u);
+    qd.v = cast(v);
+    qd.normal = cast(normal);
+    qd.w = cast(wv);
+    qd.D = (T)dd;
+    qd.mat = rq.material_index;
+    // set_bounding_box (quad.rs:40-45)
+    qd.bbox = from_boxes(from_points(qd.q, qd.q + qd.u + qd.v), from_points(qd.q + qd.u, qd.q + qd.v));
+    return qd;
+}
 template <class T> struct Material {
     uint32_t kind;
     Vec3<T> albedo;
@@ -273,6 +305,7 @@ template <class T> struct BvhNode {
 
 template <class T> struct World {
     std::vector<Sphere<T>> spheres;
+    std::vector<QuadT<T>> quads;  // primitive n_spheres + j
     std::vector<Material<T>> mats;
     std::vector<Texture> texs;
     std::vector<PerlinT<T>> perlin;
@@ -283,7 +316,7 @@ template <class T> struct World {
     ChildRef build(std::vector<int32_t> &objs, size_t lo, size_t hi) {  // bvh.rs:21-156
         const size_t span = hi - lo;
         Aabb<T> bbox = empty_box<T>();
-        for (size_t i = lo; i < hi; ++i) bbox = from_boxes(bbox, spheres[objs[i]].bbox);
+        for (size_t i = lo; i < hi; ++i) bbox = from_boxes(bbox, prim_box(objs[i]));
         const int32_t me = (int32_t)nodes.size();
         nodes.push_back(BvhNode<T>{});
         ChildRef left, right;
@@ -295,9 +328,9 @@ template <class T> struct World {
         } else {
             const int kBuckets = 12;
             const int axis = longest_axis(bbox);
-            auto cmp = [&](int32_t a, int32_t b) { return spheres[a].bbox.ax[axis].min < spheres[b].bbox.ax[axis].min; };
+            auto cmp = [&](int32_t a, int32_t b) { return prim_box(a).ax[axis].min < prim_box(b).ax[axis].min; };
             auto centroid = [&](int32_t o) {
-                const Interval<T> iv = spheres[o].bbox.ax[axis];
+                const Interval<T> iv = prim_box(o).ax[axis];
                 return T(0.5) * (iv.min + iv.max);
             };
             T cmin = std::numeric_limits<T>::infinity(), cmax = -std::numeric_limits<T>::infinity();
@@ -321,7 +354,7 @@ template <class T> struct World {
                 for (size_t i = lo; i < hi; ++i) {
                     const size_t b = bucket(objs[i]);
                     count[b]++;
-                    bb[b] = from_boxes(bb[b], spheres[objs[i]].bbox);
+                    bb[b] = from_boxes(bb[b], prim_box(objs[i]));
                 }
                 Aabb<T> rbox[12];
                 size_t rcnt[12];
@@ -368,6 +401,33 @@ template <class T> struct World {
         return ChildRef{false, me};
     }
 
+    const Aabb<T> &prim_box(int32_t p) const {
+        return (size_t)p < spheres.size() ? spheres[p].bbox : quads[p - spheres.size()].bbox;
+    }
+
+    // Quad::hit (the_next_week/quad.rs:61-87): t in the closed interval, (alpha, beta) in [0,1]^2.
+    bool hit_quad(int32_t j, Vec3<T> o, Vec3<T> d, Interval<T> ray_t, T &t_out, uint64_t *tests) const {
+        if (tests) ++*tests;
+        const QuadT<T> &qd = quads[j];
+        const T denom = dot(qd.normal, d);
+        if (std::fabs(denom) < L(1e-8)) return false;
+        const T t = (qd.D - dot(qd.normal, o)) / denom;
+        if (!ray_t.contains(t)) return false;
+        const Vec3<T> intersection = o + t * d;
+        const Vec3<T> planar = intersection - qd.q;
+        const T alpha = dot(qd.w, cross(planar, qd.v));
+        const T beta = dot(qd.w, cross(qd.u, planar));
+        const Interval<T> unit{T(0), T(1)};
+        if (!unit.contains(alpha) || !unit.contains(beta)) return false;
+        t_out = t;
+        return true;
+    }
+
+    bool hit_prim(int32_t p, Vec3<T> o, Vec3<T> d, T time, Interval<T> ray_t, T &t_out, uint64_t *tests) const {
+        if ((size_t)p < spheres.size()) return hit_sphere(p, o, d, time, ray_t, t_out, tests);
+        return hit_quad(p - (int32_t)spheres.size(), o, d, ray_t, t_out, tests);
+    }
+
     // Sphere::hit (sphere.rs:24-51): Some(t) iff a root lies in the open interval.
     bool hit_sphere(int32_t i, Vec3<T> o, Vec3<T> d, T time, Interval<T> ray_t, T &t_out, uint64_t *tests) const {
         if (tests) ++*tests;
@@ -393,7 +453,7 @@ template <class T> struct World {
     bool hit(ChildRef ref, Vec3<T> o, Vec3<T> d, T time, Interval<T> ray_t, Hit<T> &rec, uint64_t *tests) const {
         if (ref.is_sphere) {
             T t;
-            if (!hit_sphere(ref.index, o, d, time, ray_t, t, tests)) return false;
+            if (!hit_prim(ref.index, o, d, time, ray_t, t, tests)) return false;
             rec = Hit<T>{t, ref.index};
             return true;
         }
@@ -463,7 +523,7 @@ bool kbvh_hit(const World<float> &w, const KTree &kt, Vec3<float> o, Vec3<float>
     auto leaf = [&](int32_t first, int32_t count) {
         for (int32_t i = first; i < first + count; ++i) {
             float t;
-            if (w.hit_sphere((int32_t)kt.order[i], o, d, time, Interval<float>{kTmin, closest}, t, tests)) {
+            if (w.hit_prim((int32_t)kt.order[i], o, d, time, Interval<float>{kTmin, closest}, t, tests)) {
                 closest = t;
                 hit = i;
             }
@@ -589,6 +649,11 @@ void load_world(World<T> &w, Cam<T> &cam, const RrtCamera *c, const RrtSphere *s
         if (mm.kind == RRT_MAT_CHECKER_LAMBERTIAN || mm.kind == RRT_MAT_NOISE_LAMBERTIAN) w.book2 = true;
     }
     for (uint32_t i = 0; i < ntex; ++i) w.texs.push_back(Texture{tex[i].rgb8, tex[i].width, tex[i].height});
+    const uint32_t nq = ext && ext->quads ? ext->n_quads : 0u;
+    for (uint32_t j = 0; j < nq; ++j) {
+        w.quads.push_back(make_quad<T>(ext->quads[j]));
+        w.book2 = true;
+    }
     if (ext && ext->perlin)
         for (uint32_t t = 0; t < ext->n_perlin; ++t) {
             PerlinT<T> pt;
@@ -600,10 +665,11 @@ void load_world(World<T> &w, Cam<T> &cam, const RrtCamera *c, const RrtSphere *s
             }
             w.perlin.push_back(pt);
         }
-    if (n) {
-        std::vector<int32_t> objs(n);
-        for (uint32_t i = 0; i < n; ++i) objs[i] = (int32_t)i;
-        w.root = w.build(objs, 0, n);
+    const uint32_t np = n + nq;
+    if (np) {
+        std::vector<int32_t> objs(np);
+        for (uint32_t i = 0; i < np; ++i) objs[i] = (int32_t)i;
+        w.root = w.build(objs, 0, np);
     }
 }
 
@@ -629,9 +695,17 @@ bool world_hit(const World<T> &w, Vec3<T> o, Vec3<T> d, T time, Record<T> &rec, 
         if (w.root.index < 0) return false;
         if (!w.hit(w.root, o, d, time, Interval<T>{L(0.001), std::numeric_limits<T>::infinity()}, h, tests)) return false;
     }
+    rec.p = o + h.t * d;  // Ray::at
+    if ((size_t)h.sphere >= w.spheres.size()) {  // quad (quad.rs:79)
+        const QuadT<T> &qd = w.quads[h.sphere - w.spheres.size()];
+        rec.outward = qd.normal;
+        rec.front = dot(d, rec.outward) < T(0);
+        rec.normal = rec.front ? rec.outward : -rec.outward;
+        rec.mat = qd.mat;
+        return true;
+    }
     const Sphere<T> &s = w.spheres[h.sphere];
     const Vec3<T> center = w.book2 ? s.at(time) : s.center;
-    rec.p = o + h.t * d;                      // Ray::at
     rec.outward = (rec.p - center) / s.radius;  // sphere.rs:48 (current_center: the_next_week/sphere.rs:64)
     rec.front = dot(d, rec.outward) < T(0);       // hittable.rs:28-29
     rec.normal = rec.front ? rec.outward : -rec.outward;
@@ -1109,6 +1183,29 @@ int oracle_sphere_hit(int f32, const double *center, double radius, const double
         if (!w.hit_sphere(0, O, D, T(0), Interval<T>{(T)tmin, (T)tmax}, t, nullptr)) return 0;
         const Vec3<T> p = O + t * D;
         const Vec3<T> out = (p - c) / r;
+        const bool front = dot(D, out) < T(0);
+        const Vec3<T> n = front ? out : -out;
+        *t_out = t;
+        for (int i = 0; i < 3; ++i) normal_out[i] = n[i];
+        *front_out = front;
+        return 1;
+    };
+    return f32 ? run(0.0f) : run(0.0);
+}
+
+// Quad::hit for one quad (q, u, v: 3-vectors, rounded to f32 as RrtQuad stores them).
+int oracle_quad_hit(int f32, const double *q, const double *u, const double *v, const double *o, const double *d,
+                    double tmin, double tmax, double *t_out, double *normal_out, int *front_out) {
+    RrtQuad rq{};
+    for (int i = 0; i < 3; ++i) rq.q[i] = (float)q[i], rq.u[i] = (float)u[i], rq.v[i] = (float)v[i];
+    auto run = [&](auto tag) -> int {
+        using T = decltype(tag);
+        World<T> w;
+        w.quads.push_back(make_quad<T>(rq));
+        const Vec3<T> O = mk((T)o[0], (T)o[1], (T)o[2]), D = mk((T)d[0], (T)d[1], (T)d[2]);
+        T t;
+        if (!w.hit_quad(0, O, D, Interval<T>{(T)tmin, (T)tmax}, t, nullptr)) return 0;
+        const Vec3<T> out = w.quads[0].normal;
         const bool front = dot(D, out) < T(0);
         const Vec3<T> n = front ? out : -out;
         *t_out = t;

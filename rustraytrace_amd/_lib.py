@@ -81,8 +81,14 @@ PERLIN_DTYPE = np.dtype([("randvec", "<f4", (256, 4)), ("perm_x", "<u2", 256), (
                          ("perm_z", "<u2", 256), ("_pad", "<u2", 256)])
 
 
+# == RrtQuad (include/rrt_hip.h): corner q, edges u, v (xyz + pad), material index; 64 B
+QUAD_DTYPE = np.dtype([("q", "<f4", 4), ("u", "<f4", 4), ("v", "<f4", 4), ("material_index", "<u4"),
+                       ("_pad", "<u4", 3)])
+
+
 class RrtSceneExt(ctypes.Structure):
-    _fields_ = [("sphere_motion", c_void_p), ("perlin", c_void_p), ("n_perlin", c_uint32), ("_pad", c_uint32)]
+    _fields_ = [("sphere_motion", c_void_p), ("perlin", c_void_p), ("n_perlin", c_uint32), ("n_quads", c_uint32),
+                ("quads", c_void_p)]
 
 
 class RrtOverrides(ctypes.Structure):
@@ -201,7 +207,8 @@ def load() -> ctypes.CDLL:
         "rrt_hip_render_ex": (c_int32, [P, P, c_uint32, P, c_uint32, P, c_uint32, P, c_uint32, c_uint32, c_uint32, P]),
         "rrt_scene_create_ex": (c_int32, [P, P, c_uint32, P, c_uint32, P, c_uint32, P, c_uint32, c_int32, P]),
         "rrt_build_bvh_ex": (c_int32, [P, c_uint32, P, c_uint32, c_uint32, P, c_size_t, P, P]),
-        "rrt_build_next_week_scene": (c_int32, [c_int32, P, c_uint64, P, P, P, P, c_uint32, P, P, c_uint32, P]),
+        "rrt_build_next_week_scene": (c_int32, [c_int32, P, c_uint64, P, P, P, c_uint32, P, P, c_uint32, P, P, c_uint32, P,
+                                                P, c_uint32, P]),
         "rrt_device_count": (c_int32, [P]),
     }
     experiment = "RRT_LIB_PATH" in os.environ  # A/B of older builds: tolerate symbols they lack

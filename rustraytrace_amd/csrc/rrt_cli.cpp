@@ -106,20 +106,22 @@ int main(int argc, char **argv) {
     const bool book1 = book == "inoneweekend" || book == "oneweekend" || book == "weekend";
     const bool book2 = book == "thenextweek" || book == "nextweek" || book == "next";  // main.rs:89
     const int scene = positional.size() > 1 ? std::atoi(positional[1].c_str()) : 0;  // main.rs:55
-    if (book2 && !(scene == 1 || scene == 2 || scene == 4)) {
-        std::fprintf(stderr, "HIP backend supports the_next_week scenes 1 (bouncing_spheres), 2 (checkered_spheres) "
-                             "and 4 (perlin_spheres); scene 3 (earth) needs the texture: use the Python API.\n");
+    if (book2 && !(scene >= 1 && scene <= 7 && scene != 3)) {
+        std::fprintf(stderr, "HIP backend supports the_next_week scenes 1 (bouncing_spheres), 2 (checkered_spheres), "
+                             "4 (perlin_spheres), 5 (quads), 6 (simple_light) and 7 (cornell_box); scene 3 (earth) "
+                             "needs the texture: use the Python API.\n");
         return 2;
     }
     if (!book1 && !book2) {  // main.rs:59-70
-        std::fprintf(stderr, "HIP backend supports in_one_weekend and the_next_week scenes 1, 2, 4 only.\n");
+        std::fprintf(stderr, "HIP backend supports in_one_weekend and the_next_week scenes 1, 2, 4-7 only.\n");
         return 2;
     }
 
     RrtCamera cam;
-    uint32_t n = 0, n_perlin = 0;
+    uint32_t n = 0, n_mat = 0, n_quads = 0, n_perlin = 0;
     std::vector<RrtSphere> spheres;
     std::vector<RrtMaterial> materials;
+    std::vector<RrtQuad> quads;
     std::vector<float> motion;
     std::vector<RrtPerlin> perlin;
     uint32_t flags = 0;
@@ -134,18 +136,22 @@ int main(int argc, char **argv) {
             std::fprintf(stderr, "HIP render failed: %s\n", rrt_hip_last_error());
             return 1;
         }
+        n_mat = n;
     } else {
         const uint64_t s2 = seed_set ? seed : 0xB00C0002ull;
-        if (rrt_build_next_week_scene(scene, &ov, s2, &cam, nullptr, nullptr, nullptr, 0, &n, nullptr, 0, &n_perlin)) {
+        if (rrt_build_next_week_scene(scene, &ov, s2, &cam, nullptr, nullptr, 0, &n, nullptr, 0, &n_mat, nullptr, 0,
+                                      &n_quads, nullptr, 0, &n_perlin)) {
             std::fprintf(stderr, "HIP render failed: %s\n", rrt_hip_last_error());
             return 1;
         }
         spheres.resize(n);
-        materials.resize(n);
+        materials.resize(n_mat);
+        quads.resize(n_quads);
         motion.resize((size_t)n * 4);
         perlin.resize(n_perlin);
-        if (rrt_build_next_week_scene(scene, &ov, s2, &cam, spheres.data(), materials.data(), motion.data(), n, &n,
-                                      perlin.data(), n_perlin, &n_perlin)) {
+        if (rrt_build_next_week_scene(scene, &ov, s2, &cam, spheres.data(), motion.data(), n, &n, materials.data(),
+                                      n_mat, &n_mat, quads.data(), n_quads, &n_quads, perlin.data(), n_perlin,
+                                      &n_perlin)) {
             std::fprintf(stderr, "HIP render failed: %s\n", rrt_hip_last_error());
             return 1;
         }
@@ -155,6 +161,8 @@ int main(int argc, char **argv) {
     ext.sphere_motion = motion.empty() ? nullptr : motion.data();
     ext.perlin = perlin.empty() ? nullptr : perlin.data();
     ext.n_perlin = n_perlin;
+    ext.quads = quads.empty() ? nullptr : quads.data();
+    ext.n_quads = n_quads;
     const uint32_t w = (uint32_t)cam.params_f[1], h = (uint32_t)cam.params_f[2];
     const uint32_t spp = (uint32_t)(cam.params_f[3] < 1.0f ? 1.0f : cam.params_f[3]);
     const auto t0 = std::chrono::steady_clock::now();
@@ -163,11 +171,11 @@ int main(int argc, char **argv) {
     int rc;
     if (book2 || (host_quantise && !p6)) {  // float accum -> render_io on the host (book 2: rrt_hip_render_ex)
         accum.resize((size_t)w * h * 4);
-        rc = rrt_hip_render_ex(&cam, spheres.data(), n, materials.data(), n, nullptr, 0, &ext, spp, gpus, flags,
+        rc = rrt_hip_render_ex(&cam, spheres.data(), n, materials.data(), n_mat, nullptr, 0, &ext, spp, gpus, flags,
                                accum.data());
     } else {  // render_io quantiser on the device (identical bytes), 3 B/pixel to the host
         rgb8.resize((size_t)w * h * 3);
-        rc = rrt_hip_render_rgb8(&cam, spheres.data(), n, materials.data(), n, nullptr, 0, spp, gpus, 0, rgb8.data());
+        rc = rrt_hip_render_rgb8(&cam, spheres.data(), n, materials.data(), n_mat, nullptr, 0, spp, gpus, 0, rgb8.data());
     }
     if (rc) {
         std::fprintf(stderr, "HIP render failed: %s\n", rrt_hip_last_error());  // main.rs:60-65

@@ -512,9 +512,9 @@ void bvh_defaults(uint32_t &width, uint32_t &max_leaf) {
 // Sphere boxes (sphere.rs:16-21, aabb.rs:29-34: r = max(radius, 0), padded; a moving sphere's
 // box spans both ends, the_next_week/sphere.rs:31-33), SAH build, flatten. order[i] = original
 // index of the i-th primitive in leaf order.
-FlatBvh build_bvh(const RrtSphere *spheres, uint32_t n_spheres, const float *motion, uint32_t width,
-                  uint32_t max_leaf, std::vector<uint32_t> &order) {
-    std::vector<Aabb> boxes(n_spheres);
+FlatBvh build_bvh(const RrtSphere *spheres, uint32_t n_spheres, const float *motion, const RrtQuad *quads,
+                  uint32_t n_quads, uint32_t width, uint32_t max_leaf, std::vector<uint32_t> &order) {
+    std::vector<Aabb> boxes(n_spheres + (size_t)n_quads);
     for (uint32_t i = 0; i < n_spheres; ++i) {
         const double r = std::max((double)spheres[i].center_radius[3], 0.0);
         Aabb b;
@@ -528,18 +528,30 @@ FlatBvh build_bvh(const RrtSphere *spheres, uint32_t n_spheres, const float *mot
         }
         boxes[i] = pad(b);
     }
+    for (uint32_t j = 0; j < n_quads; ++j) {  // Quad::set_bounding_box (quad.rs:43-47)
+        const RrtQuad &qd = quads[j];
+        Aabb b;
+        for (int a = 0; a < 3; ++a) {
+            const double q = qd.q[a], u = qd.u[a], v = qd.v[a];
+            const double c[4] = {q, q + u + v, q + u, q + v};
+            b.ax[a] = Interval{std::min(std::min(c[0], c[1]), std::min(c[2], c[3])),
+                               std::max(std::max(c[0], c[1]), std::max(c[2], c[3]))};
+        }
+        boxes[n_spheres + j] = pad(b);
+    }
+    const uint32_t n_prims = n_spheres + n_quads;
     Builder bld(boxes, max_leaf);
     if (const char *e = std::getenv("RRT_BVH_SPLIT")) bld.sweep = std::strcmp(e, "binned") != 0;
     if (const char *e = std::getenv("RRT_SAH_CT")) bld.node_cost = std::atof(e);
     FlatBvh fb;
-    if (n_spheres == 0) {  // root with never-hit children
+    if (n_prims == 0) {  // root with never-hit children
         Builder::BNode empty;
         empty.box = never_hit_box();
         empty.leaf = true;
         bld.bin.push_back(empty);
         fb = width == 4 ? flatten4(bld, 0) : flatten2(bld, 0);
     } else {
-        const int32_t root = bld.build(0, n_spheres);
+        const int32_t root = bld.build(0, n_prims);
         fb = width == 4 ? flatten4(bld, root) : flatten2(bld, root);
     }
     order = bld.objs;
@@ -556,6 +568,7 @@ struct RrtScene {
     rrt::GMaterial *d_prim_mtl = nullptr;
     float4 *d_prim_motion = nullptr;
     rrt::GPerlin *d_perlin = nullptr;
+    rrt::GQuad *d_quads = nullptr;
     uint8_t *d_tex_pool = nullptr;
     rrt::GTexture *d_texs = nullptr;
     unsigned long long *d_counters = nullptr;       // 5 x u64, render launches
@@ -577,6 +590,7 @@ void free_scene(RrtScene *s) {
     (void)hipFree(s->d_prim_mtl);
     (void)hipFree(s->d_prim_motion);
     (void)hipFree(s->d_perlin);
+    (void)hipFree(s->d_quads);
     (void)hipFree(s->d_tex_pool);
     (void)hipFree(s->d_texs);
     (void)hipFree(s->d_counters);
@@ -677,6 +691,14 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
     if (!cam || !out) return fail(RRT_E_INVALID, "null camera or out pointer");
     const float *motion = ext ? ext->sphere_motion : nullptr;
     const uint32_t n_perlin = ext && ext->perlin ? ext->n_perlin : 0u;
+    const RrtQuad *quads = ext && ext->quads ? ext->quads : nullptr;
+    const uint32_t n_quads = quads ? ext->n_quads : 0u;
+    for (uint32_t j = 0; j < n_quads; ++j) {
+        if (quads[j].material_index >= n_materials)
+            return fail(RRT_E_INVALID, "quad " + std::to_string(j) + " material_index out of range");
+        if (materials[quads[j].material_index].kind == RRT_MAT_TEXTURED_LAMBERTIAN)
+            return fail(RRT_E_INVALID, "quad " + std::to_string(j) + ": image textures on quads are not supported");
+    }
     bool has_motion = false;
     if (motion)
         for (size_t i = 0; i < (size_t)n_spheres * 4 && !has_motion; ++i)
@@ -685,7 +707,7 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
         return fail(RRT_E_INVALID, "moving spheres need RRT_FLAG_RAY_TIME (rays carry the camera's time draw)");
     // Book-2 scenes (moving spheres or checker / noise materials) take the kernel variant that
     // supports them; it reads a motion row per sphere (zero for static spheres).
-    bool book2 = has_motion;
+    bool book2 = has_motion || n_quads > 0;
     for (uint32_t i = 0; i < n_materials && materials; ++i)
         book2 = book2 || materials[i].kind == RRT_MAT_CHECKER_LAMBERTIAN || materials[i].kind == RRT_MAT_NOISE_LAMBERTIAN;
     if (!has_motion) motion = nullptr;
@@ -716,11 +738,13 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
     bvh_defaults(width, max_leaf);
     if (book2) width = 2;  // the book-2 kernel variants are BVH2 only
     std::vector<uint32_t> order;
-    const FlatBvh fb = build_bvh(spheres, n_spheres, motion, width, max_leaf, order);
+    const FlatBvh fb = build_bvh(spheres, n_spheres, motion, quads, n_quads, width, max_leaf, order);
     if (fb.stack_need > (uint32_t)rrt::kMaxStackDepth)
         return fail(RRT_E_INVALID, "BVH depth " + std::to_string(fb.max_depth) + " exceeds the LDS stack");
     // postponed leaf tests pack (first primitive, count) as first | count << 28
-    if (fb.max_leaf > 15 || n_spheres >= (1u << 28)) return fail(RRT_E_INVALID, "leaf size > 15 or >= 2^28 spheres");
+    if (fb.max_leaf > 15 || (uint64_t)n_spheres + n_quads >= (1u << 24))
+        return fail(RRT_E_INVALID, "leaf size > 15 or >= 2^24 primitives");
+    const uint32_t n_prims = n_spheres + n_quads;
 
     std::vector<rrt::GMaterial> mats(n_materials);
     for (uint32_t i = 0; i < n_materials; ++i) {
@@ -734,10 +758,36 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
     }
     // Spheres in BVH leaf order, each with a copy of its material record: a hit reads one
     // 32-B record at the primitive's index (no dependent material-index fetch).
-    std::vector<float4> prim_cr(n_spheres);
-    std::vector<rrt::GMaterial> prim_mtl(n_spheres);
-    std::vector<float4> prim_motion(book2 ? n_spheres : 0, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
-    for (uint32_t i = 0; i < n_spheres; ++i) {
+    // Quads with their derived plane (quad.rs:21-37 in f64: n = cross(u, v), normal = n * (1/|n|),
+    // D = dot(normal, q), w = n * (1/dot(n, n)); Vec3 / f64 is `(1/rhs) * v`, vec3.rs:142-148).
+    std::vector<rrt::GQuad> gquads(n_quads);
+    for (uint32_t j = 0; j < n_quads; ++j) {
+        const RrtQuad &qd = quads[j];
+        const D3 q = d3(qd.q[0], qd.q[1], qd.q[2]), u = d3(qd.u[0], qd.u[1], qd.u[2]), v = d3(qd.v[0], qd.v[1], qd.v[2]);
+        const D3 n = cross(u, v);
+        const double nn = n.x * n.x + n.y * n.y + n.z * n.z;
+        const D3 normal = n * (1.0 / std::sqrt(nn));
+        const double dd = normal.x * q.x + normal.y * q.y + normal.z * q.z;
+        const D3 w = n * (1.0 / nn);
+        rrt::GQuad &g = gquads[j];
+        g.q = make_float4(qd.q[0], qd.q[1], qd.q[2], (float)dd);
+        g.u = make_float4(qd.u[0], qd.u[1], qd.u[2], 0.0f);
+        g.v = make_float4(qd.v[0], qd.v[1], qd.v[2], 0.0f);
+        g.n = make_float4((float)normal.x, (float)normal.y, (float)normal.z, 0.0f);
+        g.w = make_float4((float)w.x, (float)w.y, (float)w.z, 0.0f);
+    }
+    // Primitives in BVH leaf order (spheres, then quads as index n_spheres + j), each with a
+    // copy of its material record: a hit reads one 32-B record at the primitive's index.
+    std::vector<float4> prim_cr(n_prims);
+    std::vector<rrt::GMaterial> prim_mtl(n_prims);
+    std::vector<float4> prim_motion(book2 ? n_prims : 0, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+    for (uint32_t i = 0; i < n_prims; ++i) {
+        if (order[i] >= n_spheres) {  // quad j: tagged by a negative w (spheres have r >= 0)
+            const uint32_t j = order[i] - n_spheres;
+            prim_cr[i] = make_float4(0.0f, 0.0f, 0.0f, -(float)(j + 1));
+            prim_mtl[i] = mats[quads[j].material_index];
+            continue;
+        }
         const RrtSphere &sp = spheres[order[i]];
         prim_cr[i] = make_float4(sp.center_radius[0], sp.center_radius[1], sp.center_radius[2],
                                  std::max(sp.center_radius[3], 0.0f));
@@ -782,6 +832,7 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
         if ((rc = upload(&s->d_prim_mtl, prim_mtl.data(), prim_mtl.size(), "sphere materials"))) break;
         if (book2 && (rc = upload(&s->d_prim_motion, prim_motion.data(), prim_motion.size(), "sphere motion"))) break;
         if (n_perlin && (rc = upload(&s->d_perlin, perlin.data(), perlin.size(), "Perlin tables"))) break;
+        if (n_quads && (rc = upload(&s->d_quads, gquads.data(), gquads.size(), "quads"))) break;
         if ((rc = upload(&s->d_tex_pool, tex_pool.data(), tex_pool.size(), "textures"))) break;
         if ((rc = upload(&s->d_texs, texs.data(), texs.size(), "texture table"))) break;
         if (hipMalloc((void **)&s->d_counters, 8 * sizeof(unsigned long long)) != hipSuccess ||
@@ -808,6 +859,8 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
     p.prim_motion = s->d_prim_motion;
     p.perlin = s->d_perlin;
     p.n_perlin = n_perlin;
+    p.quads = s->d_quads;
+    p.n_quads = n_quads;
     p.tex_pool = s->d_tex_pool;
     p.texs = s->d_texs;
     p.counters = s->d_counters;
@@ -829,11 +882,11 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
     p.width = (uint32_t)wf;
     p.height = (uint32_t)hf;
     p.n_nodes = fb.n_nodes;
-    p.n_prims = n_spheres;
+    p.n_prims = n_prims;
     p.stack_depth = fb.stack_need;
     p.bvh_width = fb.width;
     const size_t scene_bytes =
-        fb.bytes.size() + (size_t)n_spheres * (rrt::kPrimBytes + (book2 ? rrt::kMotionBytes : 0));
+        fb.bytes.size() + (size_t)n_prims * (rrt::kPrimBytes + (book2 ? rrt::kMotionBytes : 0));
     p.scene_in_lds = scene_bytes <= rrt::kLdsSceneBudget;
     if (const char *e = std::getenv("RRT_SCENE_IN_LDS")) p.scene_in_lds = p.scene_in_lds && std::atoi(e) != 0;
     p.trav_frac = 32;
@@ -859,7 +912,8 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
     bi.node_bytes = fb.bytes.size();
     bi.width = fb.width;
     bi.max_leaf_param = max_leaf;
-    bi.prim_bytes = (uint64_t)n_spheres * (rrt::kPrimBytes + (book2 ? rrt::kMotionBytes : 0));
+    bi.prim_bytes = (uint64_t)n_prims * (rrt::kPrimBytes + (book2 ? rrt::kMotionBytes : 0)) +
+                    (uint64_t)n_quads * sizeof(rrt::GQuad);
     *out = s;
     return RRT_OK;
 }
@@ -886,10 +940,13 @@ int32_t rrt_build_bvh(const RrtSphere *spheres, uint32_t n_spheres, uint32_t wid
     return rrt_build_bvh_ex(spheres, n_spheres, nullptr, width, max_leaf, nodes_out, nodes_cap, prim_order_out, info);
 }
 
-int32_t rrt_build_bvh_ex(const RrtSphere *spheres, uint32_t n_spheres, const float *motion, uint32_t width,
+int32_t rrt_build_bvh_ex(const RrtSphere *spheres, uint32_t n_spheres, const RrtSceneExt *ext, uint32_t width,
                          uint32_t max_leaf, void *nodes_out, size_t nodes_cap, uint32_t *prim_order_out,
                          RrtBvhInfo *info) {
     if (n_spheres && !spheres) return fail(RRT_E_INVALID, "null spheres");
+    const float *motion = ext ? ext->sphere_motion : nullptr;
+    const RrtQuad *quads = ext && ext->quads ? ext->quads : nullptr;
+    const uint32_t n_quads = quads ? ext->n_quads : 0u;
     if (motion) {  // same rule as scene creation: an all-zero motion array is a static scene
         bool any = false;
         for (size_t i = 0; i < (size_t)n_spheres * 4 && !any; ++i) any = (i % 4 != 3) && motion[i] != 0.0f;
@@ -901,7 +958,7 @@ int32_t rrt_build_bvh_ex(const RrtSphere *spheres, uint32_t n_spheres, const flo
     if (max_leaf == 0) max_leaf = dl;
     if ((width != 2 && width != 4) || max_leaf > 15) return fail(RRT_E_INVALID, "width must be 2 or 4, max_leaf <= 15");
     std::vector<uint32_t> order;
-    const FlatBvh fb = build_bvh(spheres, n_spheres, motion, width, max_leaf, order);
+    const FlatBvh fb = build_bvh(spheres, n_spheres, motion, quads, n_quads, width, max_leaf, order);
     if (info) {
         *info = RrtBvhInfo{};
         info->n_nodes = fb.n_nodes;
@@ -914,10 +971,10 @@ int32_t rrt_build_bvh_ex(const RrtSphere *spheres, uint32_t n_spheres, const flo
         info->max_leaf_param = max_leaf;
     }
     if (nodes_cap == 0) return RRT_OK;
-    if (!nodes_out || nodes_cap < fb.bytes.size() || (n_spheres && !prim_order_out))
+    if (!nodes_out || nodes_cap < fb.bytes.size() || (order.size() && !prim_order_out))
         return fail(RRT_E_INVALID, "nodes buffer too small (need " + std::to_string(fb.bytes.size()) + " bytes)");
     std::memcpy(nodes_out, fb.bytes.data(), fb.bytes.size());
-    if (n_spheres) std::memcpy(prim_order_out, order.data(), order.size() * sizeof(uint32_t));
+    if (order.size()) std::memcpy(prim_order_out, order.data(), order.size() * sizeof(uint32_t));
     return RRT_OK;
 }
 
@@ -1292,11 +1349,14 @@ int32_t rrt_build_in_one_weekend_scene(const RrtOverrides *ov, uint64_t seed, in
 // random_double_range = gen_range(min..max), random_int(min,max) = random_double_range(min,
 // max+1) as i32 (rtweekend.rs:17-30). Parity unpinned (entropy RNG).
 int32_t rrt_build_next_week_scene(int32_t scene, const RrtOverrides *ov, uint64_t seed, RrtCamera *cam,
-                                  RrtSphere *spheres, RrtMaterial *materials, float *motion, uint32_t sphere_cap,
-                                  uint32_t *n_spheres, RrtPerlin *perlin, uint32_t perlin_cap, uint32_t *n_perlin) {
-    if (!n_spheres || !n_perlin) return fail(RRT_E_INVALID, "null n_spheres or n_perlin");
-    if (scene < 1 || scene > 4)
-        return fail(RRT_E_INVALID, "book-2 scene must be 1 bouncing_spheres, 2 checkered_spheres, 3 earth, 4 perlin_spheres");
+                                  RrtSphere *spheres, float *motion, uint32_t sphere_cap, uint32_t *n_spheres,
+                                  RrtMaterial *materials, uint32_t material_cap, uint32_t *n_materials,
+                                  RrtQuad *quads, uint32_t quad_cap, uint32_t *n_quads,
+                                  RrtPerlin *perlin, uint32_t perlin_cap, uint32_t *n_perlin) {
+    if (!n_spheres || !n_materials || !n_quads || !n_perlin) return fail(RRT_E_INVALID, "null count output");
+    if (scene < 1 || scene > 7)
+        return fail(RRT_E_INVALID, "book-2 scene must be 1 bouncing_spheres, 2 checkered_spheres, 3 earth, "
+                                   "4 perlin_spheres, 5 quads, 6 simple_light, 7 cornell_box");
     // Camera (the_next_week/mod.rs:137-150, 177-190, 203-216, 237-250)
     double aspect_ratio = 16.0 / 9.0;
     int32_t image_width = 400, samples_per_pixel = 100, max_depth = 50;
@@ -1307,6 +1367,20 @@ int32_t rrt_build_next_week_scene(int32_t scene, const RrtOverrides *ov, uint64_
     int32_t has_bg = 1;
     if (scene == 1) defocus_angle = 0.6;
     if (scene == 3) lookfrom[0] = 0.0, lookfrom[1] = 0.0, lookfrom[2] = 12.0;
+    if (scene == 5) {  // mod.rs:301-313
+        aspect_ratio = 1.0, vfov = 80.0;
+        lookfrom[0] = 0.0, lookfrom[1] = 0.0, lookfrom[2] = 9.0;
+    } else if (scene == 6) {  // mod.rs:342-354
+        vfov = 20.0;
+        lookfrom[0] = 26.0, lookfrom[1] = 3.0, lookfrom[2] = 6.0;
+        lookat[1] = 2.0;
+        background[0] = background[1] = background[2] = 0.0;
+    } else if (scene == 7) {  // mod.rs:412-423
+        aspect_ratio = 1.0, image_width = 600, samples_per_pixel = 200, vfov = 40.0;
+        lookfrom[0] = 278.0, lookfrom[1] = 278.0, lookfrom[2] = -800.0;
+        lookat[0] = 278.0, lookat[1] = 278.0, lookat[2] = 0.0;
+        background[0] = background[1] = background[2] = 0.0;
+    }
     rrt_apply_overrides(ov, 2, &aspect_ratio, &image_width, &samples_per_pixel, &max_depth, &vfov, lookfrom, lookat,
                         vup, &defocus_angle, &focus_dist, background, &has_bg);
 
@@ -1317,6 +1391,7 @@ int32_t rrt_build_next_week_scene(int32_t scene, const RrtOverrides *ov, uint64_
     std::vector<RrtMaterial> mat;
     std::vector<float> mot;
     std::vector<RrtPerlin> tables;
+    std::vector<RrtQuad> qds;
     auto bits = [](float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; };
     auto add_material = [&](uint32_t kind, float r, float g, float b, float w, float ref_idx, uint32_t p0, uint32_t p1) {
         RrtMaterial m{};
@@ -1341,6 +1416,66 @@ int32_t rrt_build_next_week_scene(int32_t scene, const RrtOverrides *ov, uint64_
         mot.insert(mot.end(), {(float)move.x, (float)move.y, (float)move.z, 0.0f});
     };
     const D3 still = d3(0.0, 0.0, 0.0);
+    // Quad::new (quad.rs:21-37) under an optional RotateY(deg) then Translate(offset)
+    // (hittable.rs:65-170), baked to world space in f64: a point p goes to
+    // (cos x + sin z, y, -sin x + cos z) + offset, an edge vector rotates only.
+    struct Xform {
+        double c = 1.0, s = 0.0;
+        D3 off = d3(0.0, 0.0, 0.0);
+    };
+    auto rot = [](const Xform &x, D3 a) { return d3(x.c * a.x + x.s * a.z, a.y, -x.s * a.x + x.c * a.z); };
+    auto add_quad = [&](D3 q, D3 u, D3 v, uint32_t m, const Xform &x) {
+        const D3 wq = rot(x, q) + x.off, wu = rot(x, u), wv = rot(x, v);
+        RrtQuad r{};
+        put4(r.q, (float)wq.x, (float)wq.y, (float)wq.z, 0.0f);
+        put4(r.u, (float)wu.x, (float)wu.y, (float)wu.z, 0.0f);
+        put4(r.v, (float)wv.x, (float)wv.y, (float)wv.z, 0.0f);
+        r.material_index = m;
+        qds.push_back(r);
+    };
+    const Xform ident;
+    auto make_box = [&](D3 a, D3 b, uint32_t m, const Xform &x) {  // quad.rs:95-119
+        const D3 lo = d3(std::min(a.x, b.x), std::min(a.y, b.y), std::min(a.z, b.z));
+        const D3 hi = d3(std::max(a.x, b.x), std::max(a.y, b.y), std::max(a.z, b.z));
+        const D3 dx = d3(hi.x - lo.x, 0.0, 0.0), dy = d3(0.0, hi.y - lo.y, 0.0), dz = d3(0.0, 0.0, hi.z - lo.z);
+        const D3 ndx = d3(-dx.x, 0.0, 0.0), ndz = d3(0.0, 0.0, -dz.z);
+        add_quad(d3(lo.x, lo.y, hi.z), dx, dy, m, x);
+        add_quad(d3(hi.x, lo.y, hi.z), ndz, dy, m, x);
+        add_quad(d3(hi.x, lo.y, lo.z), ndx, dy, m, x);
+        add_quad(d3(lo.x, lo.y, lo.z), dz, dy, m, x);
+        add_quad(d3(lo.x, hi.y, hi.z), dx, ndz, m, x);
+        add_quad(d3(lo.x, lo.y, lo.z), dx, dz, m, x);
+    };
+    auto rotate_translate = [](double deg, D3 off) {  // RotateY::new (hittable.rs:100-103)
+        Xform x;
+        const double rad = degrees_to_radians(deg);
+        x.s = std::sin(rad);
+        x.c = std::cos(rad);
+        x.off = off;
+        return x;
+    };
+    auto lambertian = [&](float r, float g, float b) { return add_material(RRT_MAT_LAMBERTIAN, r, g, b, 0.0f, 1.0f, 0, 0); };
+    auto diffuse_light = [&](float e) { return add_material(RRT_MAT_DIFFUSE_LIGHT, e, e, e, 0.0f, 1.0f, 0, 0); };
+    auto perlin_table = [&]() {  // Perlin::new (perlin.rs:12-22)
+        RrtPerlin t{};
+        for (int i = 0; i < 256; ++i) {
+            double v[3];
+            for (double &x : v) x = random_range(-1.0, 1.0);
+            const D3 u = unit_vector(d3(v[0], v[1], v[2]));
+            t.randvec[i][0] = (float)u.x;
+            t.randvec[i][1] = (float)u.y;
+            t.randvec[i][2] = (float)u.z;
+        }
+        for (uint16_t *perm : {t.perm_x, t.perm_y, t.perm_z}) {  // perlin_generate_perm / permute (perlin.rs:70-82)
+            for (int i = 0; i < 256; ++i) perm[i] = (uint16_t)i;
+            for (int i = 255; i > 0; --i) {
+                const int target = (int)random_range(0.0, (double)(i + 1));
+                std::swap(perm[i], perm[target]);
+            }
+        }
+        tables.push_back(t);
+        return (uint32_t)(tables.size() - 1);
+    };
     if (scene == 1) {  // bouncing_spheres (mod.rs:83-135)
         add_sphere(d3(0.0, -1000.0, 0.0), 1000.0, checker(), still);
         for (int a = -11; a < 11; ++a) {
@@ -1380,31 +1515,40 @@ int32_t rrt_build_next_week_scene(int32_t scene, const RrtOverrides *ov, uint64_
         add_sphere(d3(0.0, 10.0, 0.0), 10.0, checker(), still);
     } else if (scene == 3) {  // earth (mod.rs:196-201): the image is texture 0
         add_sphere(d3(0.0, 0.0, 0.0), 2.0, add_material(RRT_MAT_TEXTURED_LAMBERTIAN, 0, 0, 0, 0, 1.0f, 0, 0), still);
-    } else {  // perlin_spheres (mod.rs:222-235): one NoiseTexture(4) shared by both spheres
-        RrtPerlin t{};
-        for (int i = 0; i < 256; ++i) {  // Perlin::new (perlin.rs:12-22)
-            double v[3];
-            for (double &x : v) x = random_range(-1.0, 1.0);
-            const D3 u = unit_vector(d3(v[0], v[1], v[2]));
-            t.randvec[i][0] = (float)u.x;
-            t.randvec[i][1] = (float)u.y;
-            t.randvec[i][2] = (float)u.z;
+    } else if (scene == 4 || scene == 6) {
+        // perlin_spheres (mod.rs:222-235) / simple_light (mod.rs:318-340): one NoiseTexture(4)
+        // shared by the ground and the sphere
+        const uint32_t t = perlin_table();
+        const uint32_t m = add_material(RRT_MAT_NOISE_LAMBERTIAN, 0.5f, 0.5f, 0.5f, 4.0f, 1.0f, t, 0);
+        add_sphere(d3(0.0, -1000.0, 0.0), 1000.0, m, still);
+        add_sphere(d3(0.0, 2.0, 0.0), 2.0, m, still);
+        if (scene == 6) {
+            const uint32_t light = diffuse_light(4.0f);
+            add_sphere(d3(0.0, 7.0, 0.0), 2.0, light, still);
+            add_quad(d3(3.0, 1.0, -2.0), d3(2.0, 0.0, 0.0), d3(0.0, 2.0, 0.0), light, ident);
         }
-        for (uint16_t *perm : {t.perm_x, t.perm_y, t.perm_z}) {  // perlin_generate_perm / permute (perlin.rs:70-82)
-            for (int i = 0; i < 256; ++i) perm[i] = (uint16_t)i;
-            for (int i = 255; i > 0; --i) {
-                const int target = (int)random_range(0.0, (double)(i + 1));
-                std::swap(perm[i], perm[target]);
-            }
-        }
-        tables.push_back(t);
-        add_sphere(d3(0.0, -1000.0, 0.0), 1000.0, add_material(RRT_MAT_NOISE_LAMBERTIAN, 0.5f, 0.5f, 0.5f, 4.0f, 1.0f, 0, 0),
-                   still);
-        add_sphere(d3(0.0, 2.0, 0.0), 2.0, add_material(RRT_MAT_NOISE_LAMBERTIAN, 0.5f, 0.5f, 0.5f, 4.0f, 1.0f, 0, 0),
-                   still);
+    } else if (scene == 5) {  // quads (mod.rs:257-299)
+        add_quad(d3(-3, -2, 5), d3(0, 0, -4), d3(0, 4, 0), lambertian(1.0f, 0.2f, 0.2f), ident);
+        add_quad(d3(-2, -2, 0), d3(4, 0, 0), d3(0, 4, 0), lambertian(0.2f, 1.0f, 0.2f), ident);
+        add_quad(d3(3, -2, 1), d3(0, 0, 4), d3(0, 4, 0), lambertian(0.2f, 0.2f, 1.0f), ident);
+        add_quad(d3(-2, 3, 1), d3(4, 0, 0), d3(0, 0, 4), lambertian(1.0f, 0.5f, 0.0f), ident);
+        add_quad(d3(-2, -3, 5), d3(4, 0, 0), d3(0, 0, -4), lambertian(0.2f, 0.8f, 0.8f), ident);
+    } else {  // cornell_box (mod.rs:359-410)
+        const uint32_t red = lambertian(0.65f, 0.05f, 0.05f), white = lambertian(0.73f, 0.73f, 0.73f);
+        const uint32_t green = lambertian(0.12f, 0.45f, 0.15f), light = diffuse_light(15.0f);
+        add_quad(d3(555, 0, 0), d3(0, 555, 0), d3(0, 0, 555), green, ident);
+        add_quad(d3(0, 0, 0), d3(0, 555, 0), d3(0, 0, 555), red, ident);
+        add_quad(d3(343, 554, 332), d3(-130, 0, 0), d3(0, 0, -105), light, ident);
+        add_quad(d3(0, 0, 0), d3(555, 0, 0), d3(0, 0, 555), white, ident);
+        add_quad(d3(555, 555, 555), d3(-555, 0, 0), d3(0, 0, -555), white, ident);
+        add_quad(d3(0, 0, 555), d3(555, 0, 0), d3(0, 555, 0), white, ident);
+        make_box(d3(0, 0, 0), d3(165, 330, 165), white, rotate_translate(15.0, d3(265, 0, 295)));
+        make_box(d3(0, 0, 0), d3(165, 165, 165), white, rotate_translate(-18.0, d3(130, 0, 65)));
     }
     const uint32_t sample_seed = rng.next_u32();
     *n_spheres = (uint32_t)sph.size();
+    *n_materials = (uint32_t)mat.size();
+    *n_quads = (uint32_t)qds.size();
     *n_perlin = (uint32_t)tables.size();
     if (cam) {
         int rc = rrt_make_camera(aspect_ratio, image_width, samples_per_pixel, max_depth, vfov, lookfrom, lookat, vup,
@@ -1416,12 +1560,19 @@ int32_t rrt_build_next_week_scene(int32_t scene, const RrtOverrides *ov, uint64_
         if (perlin_cap < tables.size() || !perlin) return fail(RRT_E_INVALID, "perlin_cap too small");
         if (!tables.empty()) std::memcpy(perlin, tables.data(), tables.size() * sizeof(RrtPerlin));
     }
+    if (quad_cap) {
+        if (quad_cap < qds.size() || !quads) return fail(RRT_E_INVALID, "quad_cap too small");
+        if (!qds.empty()) std::memcpy(quads, qds.data(), qds.size() * sizeof(RrtQuad));
+    }
+    if (material_cap) {
+        if (material_cap < mat.size() || !materials) return fail(RRT_E_INVALID, "material_cap too small");
+        std::memcpy(materials, mat.data(), mat.size() * sizeof(RrtMaterial));
+    }
     if (sphere_cap == 0) return RRT_OK;
-    if (sphere_cap < sph.size() || !spheres || !materials)
+    if (sphere_cap < sph.size() || !spheres)
         return fail(RRT_E_INVALID, "sphere_cap too small (need " + std::to_string(sph.size()) + ")");
-    std::memcpy(spheres, sph.data(), sph.size() * sizeof(RrtSphere));
-    std::memcpy(materials, mat.data(), mat.size() * sizeof(RrtMaterial));
-    if (motion) std::memcpy(motion, mot.data(), mot.size() * sizeof(float));
+    if (!sph.empty()) std::memcpy(spheres, sph.data(), sph.size() * sizeof(RrtSphere));
+    if (motion && !mot.empty()) std::memcpy(motion, mot.data(), mot.size() * sizeof(float));
     return RRT_OK;
 }
 

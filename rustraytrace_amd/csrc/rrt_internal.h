@@ -47,6 +47,17 @@ struct alignas(16) GPerlin {
     uint32_t perm[256];
 };
 
+// Quad (the_next_week/quad.rs:9-41) with its derived plane: q.xyz corner, q.w = D = dot(n, q);
+// u, v edges; n = unit(cross(u, v)); w = cross(u, v) / |cross(u, v)|^2 (computed in f64 on the
+// host, quad.rs's `(1/x) * v` divisions, then rounded to f32). 80 B.
+struct alignas(16) GQuad {
+    float4 q;
+    float4 u;
+    float4 v;
+    float4 n;
+    float4 w;
+};
+
 struct GTexture {
     int32_t offset;  // byte offset into the texture pool
     int32_t width;
@@ -61,6 +72,7 @@ struct KParams {
     const GMaterial *prim_mtl;   // each primitive's material record, same order (one fetch per hit)
     const float4 *prim_motion;   // (center2 - center1).xyz per primitive, same order; null = static scene
     const GPerlin *perlin;       // Perlin tables (noise textures)
+    const GQuad *quads;          // quads; a quad's leaf-order primitive record is (0, 0, 0, -(1 + index))
     const uint8_t *tex_pool;
     const GTexture *texs;
     float4 *accum;               // tile-local rows * width
@@ -95,6 +107,7 @@ struct KParams {
     uint32_t n_nodes;
     uint32_t n_prims;
     uint32_t n_perlin;
+    uint32_t n_quads;
     uint32_t stack_depth;   // entries needed (BVH depth + 1)
     uint32_t scene_in_lds;  // stage nodes + spheres + their materials in LDS per block
     uint32_t trav_frac;     // leave the traversal loop when <= live*trav_frac/256 lanes still traverse

@@ -56,6 +56,9 @@ __device__ __forceinline__ V3 mul(V3 a, V3 b) { return v3(a.x * b.x, a.y * b.y, 
 __device__ __forceinline__ V3 muls(V3 a, float s) { return v3(a.x * s, a.y * s, a.z * s); }
 // vec3.rs:156-158 dot = (u0*v0 + u1*v1) + u2*v2
 __device__ __forceinline__ float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ V3 cross(V3 a, V3 b) {  // vec3.rs cross
+    return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
 // vec3.rs:168-170 unit_vector = v * (1/len)  (Div<f64> is `(1.0/rhs) * self`, vec3.rs:142-148)
 __device__ __forceinline__ V3 unit(V3 v) {
     const float inv = 1.0f / __builtin_sqrtf(dot(v, v));
@@ -231,11 +234,14 @@ __device__ __forceinline__ float div_by_a(float n, const RayK &rk) {
 // Sphere centers as the sphere test sees them: static, or (book-2 scenes) a moving sphere's
 // center at the ray's time, center1 + time * (center2 - center1) (the_next_week/sphere.rs:44:
 // Ray::at; static book-2 spheres carry a zero motion).
-template <bool kBook2>
+// kBook2: 0 = book-1 scenes, 1 = book 2 (motion, procedural textures), 2 = book 2 with quads
+template <int kBook2>
 struct Prims {
     const float4 *cr;
     const float4 *mo;
     float time;
+    const GQuad *qd;  // book-2 scenes: quads, tagged in cr by a negative w (-(1 + index))
+    static constexpr bool kHasQuads = kBook2 == 2;
     __device__ __forceinline__ float4 at(int i) const {
         float4 c = cr[i];
         if constexpr (kBook2) {
@@ -248,10 +254,30 @@ struct Prims {
     }
 };
 
+// Quad::hit (the_next_week/quad.rs:61-87) in f32: plane distance, then the hit point's (alpha,
+// beta) in the (u, v) frame. The t acceptance is Interval::contains (closed: a quad at exactly
+// the running closest t replaces the earlier hit), unlike the sphere's open `surrounds`.
+__device__ __forceinline__ bool quad_hit(const GQuad &g, V3 o, V3 d, float closest, float &t_out) {
+    const V3 n = v3(g.n.x, g.n.y, g.n.z);
+    const float denom = dot(n, d);
+    if (__builtin_fabsf(denom) < 1e-8f) return false;
+    const float t = (g.q.w - dot(n, o)) / denom;
+    if (!(0.001f <= t && t <= closest)) return false;
+    const V3 p = v3(o.x + t * d.x, o.y + t * d.y, o.z + t * d.z);  // Ray::at
+    const V3 hp = v3(p.x - g.q.x, p.y - g.q.y, p.z - g.q.z);
+    const V3 w = v3(g.w.x, g.w.y, g.w.z);
+    const float alpha = dot(w, cross(hp, v3(g.v.x, g.v.y, g.v.z)));
+    const float beta = dot(w, cross(v3(g.u.x, g.u.y, g.u.z), hp));
+    if (!(0.0f <= alpha && alpha <= 1.0f && 0.0f <= beta && beta <= 1.0f)) return false;  // is_interior
+    t_out = t;
+    return true;
+}
+
 // Sphere::hit (sphere.rs:24-51) root selection; returns true and shrinks `closest`.
 template <bool kCount, class PR>
 __device__ __forceinline__ void test_prims(const PR &prim_cr, int first, int count, V3 o, V3 d,
                                            float a, float &closest, int &hit_prim, Counters &cnt) {
+    static_assert(!PR::kHasQuads, "book-2 scenes (quads, motion) use the binary BVH");
     for (int i = first; i < first + count; ++i) {
         if (kCount) cnt.spheres++;
         const float4 cr = prim_cr.at(i);
@@ -285,6 +311,16 @@ __device__ __forceinline__ void test_prims2(const PR &prim_cr, int f0, int c0, i
             cnt.d1 += 1;
         }
         const float4 cr = prim_cr.at(i);
+        if constexpr (PR::kHasQuads) {
+            if (cr.w < 0.0f) {
+                float tq;
+                if (quad_hit(prim_cr.qd[(int)(-cr.w) - 1], o, d, closest, tq)) {
+                    closest = tq;
+                    hit_prim = i;
+                }
+                continue;
+            }
+        }
         const V3 oc = v3(cr.x - o.x, cr.y - o.y, cr.z - o.z);
         const float h = dot(d, oc);
         const float c = dot(oc, oc) - cr.w * cr.w;
@@ -637,7 +673,7 @@ __device__ __forceinline__ V3 texel(const KParams &P, int tex, float u, float v)
 // After the closest-hit query of the current segment (prim < 0: miss): background, or
 // emission / scatter / RR (camera.rs:182-209). Returns true when the path has ended; a
 // path ending at the sky or an emitter adds T*Le to `sum`.
-template <bool kBook2, typename C, class PR>
+template <int kBook2, typename C, class PR>
 __device__ __forceinline__ bool shade(const KParams &P, const PR &prims, const GMaterial *mtl, PathState &ps,
                                       float t, int prim, V3 &sum, C &cnt) {
     if constexpr (RRT_PHASE_TIMING == 4) {
@@ -659,8 +695,14 @@ __device__ __forceinline__ bool shade(const KParams &P, const PR &prims, const G
     // HitRecord (sphere.rs:47-50, hittable.rs:20-32)
     const float4 cr = prims.at(prim);  // the sphere's center at the ray's time (sphere.rs:48)
     const V3 p = v3(ps.o.x + ps.d.x * t, ps.o.y + ps.d.y * t, ps.o.z + ps.d.z * t);
-    const float inv_r = 1.0f / cr.w;
-    const V3 outward = v3((p.x - cr.x) * inv_r, (p.y - cr.y) * inv_r, (p.z - cr.z) * inv_r);
+    V3 outward;
+    if (PR::kHasQuads && cr.w < 0.0f) {  // a quad's plane normal (quad.rs:79)
+        const float4 qn = prims.qd[(int)(-cr.w) - 1].n;
+        outward = v3(qn.x, qn.y, qn.z);
+    } else {
+        const float inv_r = 1.0f / cr.w;
+        outward = v3((p.x - cr.x) * inv_r, (p.y - cr.y) * inv_r, (p.z - cr.z) * inv_r);
+    }
     const bool front = dot(ps.d, outward) < 0.0f;
     const V3 nrm = front ? outward : v3(-outward.x, -outward.y, -outward.z);
     const GMaterial m = mtl[prim];
@@ -731,7 +773,7 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
     return v;
 }
 
-template <bool kLds, bool kCount, typename StackT, bool kWide, bool kBook2>
+template <bool kLds, bool kCount, typename StackT, bool kWide, int kBook2>
 __device__ __forceinline__ void render_body(const KParams &P) {
     extern __shared__ uint4 lds_dyn[];
     // LDS layout: [traversal stack: stack_depth x kBlock x StackT, 16-B aligned][nodes][primitives]
@@ -856,7 +898,7 @@ __device__ __forceinline__ void render_body(const KParams &P) {
         }
         RayK rk;
         if (tracing) rk = ray_consts(ps.o, ps.d);
-        const Prims<kBook2> pr{prims, motion, ps.time};
+        const Prims<kBook2> pr{prims, motion, ps.time, P.quads};
         if constexpr (kWide) {
             for (;;) {
                 if constexpr (RRT_PHASE_TIMING == 2) {
@@ -903,7 +945,7 @@ __device__ __forceinline__ void render_body(const KParams &P) {
         }
         if (has && !need_ray && !tracing) {
             need_ray = true;
-            seg_done = shade<kBook2>(P, Prims<kBook2>{prims, motion, ps.time}, mtl, ps, tr.closest, tr.hit_prim, sum, cnt);
+            seg_done = shade<kBook2>(P, Prims<kBook2>{prims, motion, ps.time, P.quads}, mtl, ps, tr.closest, tr.hit_prim, sum, cnt);
         }
         w_paths += (uint32_t)__popcll(__ballot(seg_done));
         if (seg_done) {  // pixel_color += ray_color(..) (camera.rs:73-76): already in `sum`
@@ -958,7 +1000,7 @@ __device__ __forceinline__ void render_body(const KParams &P) {
     }
 }
 
-template <bool kLds, bool kCount, typename StackT, bool kWide, int kWaves, bool kBook2>
+template <bool kLds, bool kCount, typename StackT, bool kWide, int kWaves, int kBook2>
 __global__ __launch_bounds__(kBlock, kWaves) void rrt_render(KParams P) {
     render_body<kLds, kCount, StackT, kWide, kBook2>(P);
 }
@@ -1020,7 +1062,7 @@ __global__ __launch_bounds__(256) void rrt_quantize(const float4 *__restrict__ a
     }
 }
 
-template <bool kLds, typename StackT, bool kWide, bool kBook2, int kWaves = 1>
+template <bool kLds, typename StackT, bool kWide, int kBook2, int kWaves = 1>
 hipError_t launch_variant(const KParams &p, bool count, hipStream_t stream) {
     if (p.n_units == 0) return hipSuccess;
     size_t lds = ((size_t)p.stack_depth * kBlock * sizeof(StackT) + 15u) / 16u * 16u;
@@ -1048,10 +1090,17 @@ hipError_t launch_variant(const KParams &p, bool count, hipStream_t stream) {
     return hipGetLastError();
 }
 
-template <bool kWide, bool kBook2>
+template <bool kWide, int kBook2>
 hipError_t launch_width(const KParams &p, bool count, hipStream_t stream) {
     if (p.stack_depth > (uint32_t)kMaxStackDepth) return hipErrorInvalidValue;
     if (p.n_nodes > 65535u) return launch_variant<false, uint32_t, kWide, kBook2>(p, count, stream);
+    if constexpr (kBook2 != 0) {
+        // Book-2 variants (motion, textures, quads) need ~105 VGPRs: bounded to the 80 of 6
+        // waves/SIMD they spill 17-22 dwords and run 3-14% slower than unbounded (4 waves/SIMD);
+        // a 5-wave bound (96 VGPRs, 1-3 spills) measured 0-8% slower too.
+        return p.scene_in_lds ? launch_variant<true, uint16_t, kWide, kBook2>(p, count, stream)
+                              : launch_variant<false, uint16_t, kWide, kBook2>(p, count, stream);
+    }
     if (!kWide && p.scene_in_lds && p.min_waves >= 6)
         return launch_variant<true, uint16_t, kWide, kBook2, kWavesPerSimd>(p, count, stream);
     if (!kWide && !p.scene_in_lds && p.global_waves >= 6)
@@ -1067,8 +1116,11 @@ hipError_t launch_render_kernel(const KParams &p, bool count, hipStream_t stream
     // staged in LDS when the BVH + spheres fit the per-block budget (RTOW: ~20-26 KB).
     // Book-2 scenes (moving spheres, checker / noise textures): BVH2 only (the host builds a
     // binary tree for them); motion is always present (zero for static spheres).
-    if (p.prim_motion) return p.bvh_width == 2 ? launch_width<false, true>(p, count, stream) : hipErrorInvalidValue;
-    return p.bvh_width == 4 ? launch_width<true, false>(p, count, stream) : launch_width<false, false>(p, count, stream);
+    if (p.prim_motion) {  // book 2: the binary BVH only
+        if (p.bvh_width != 2) return hipErrorInvalidValue;
+        return p.n_quads ? launch_width<false, 2>(p, count, stream) : launch_width<false, 1>(p, count, stream);
+    }
+    return p.bvh_width == 4 ? launch_width<true, 0>(p, count, stream) : launch_width<false, 0>(p, count, stream);
 }
 
 hipError_t launch_render(const KParams &p, hipStream_t stream) { return launch_render_kernel(p, false, stream); }

@@ -32,8 +32,9 @@ def _textures(scene: SceneData):
 
 
 def scene_ext(scene: SceneData):
-    """(RrtSceneExt or None, keep-alive list) for the book-2 data of `scene` (motion, Perlin)."""
-    if scene.motion is None and scene.perlin is None:
+    """(RrtSceneExt or None, keep-alive list) for the book-2 data of `scene` (motion, Perlin, quads)."""
+    quads = getattr(scene, "quads", None)
+    if scene.motion is None and scene.perlin is None and quads is None:
         return None, []
     ext = _lib.RrtSceneExt()
     keep = []
@@ -47,6 +48,11 @@ def scene_ext(scene: SceneData):
         keep.append(t)
         ext.perlin = t.ctypes.data
         ext.n_perlin = len(t)
+    if quads is not None:
+        q = np.ascontiguousarray(quads, dtype=_lib.QUAD_DTYPE)
+        keep.append(q)
+        ext.quads = q.ctypes.data
+        ext.n_quads = len(q)
     return ext, keep
 
 
@@ -170,21 +176,22 @@ def build_bvh(scene: SceneData, width: int = 0, max_leaf: int = 0):
     lib = _lib.load()
     info = _lib.RrtBvhInfo()
     n = len(scene.spheres)
-    motion = None if scene.motion is None else np.ascontiguousarray(scene.motion, dtype=np.float32)
-    if scene.motion is not None or scene.perlin is not None or np.isin(scene.materials["kind"], (5, 6)).any():
+    ext, keep = scene_ext(scene)
+    n_prims = n + (0 if ext is None else ext.n_quads)
+    if ext is not None or np.isin(scene.materials["kind"], (5, 6)).any():
         width = 2  # book-2 scenes render with the BVH2 kernel variant (rrt_scene_create_ex)
     def build(nodes_p, cap, order_p):
-        if motion is None:
+        if ext is None:
             return lib.rrt_build_bvh(_lib.ptr(scene.spheres), n, width, max_leaf, nodes_p, cap, order_p,
                                      ctypes.byref(info))
-        return lib.rrt_build_bvh_ex(_lib.ptr(scene.spheres), n, _lib.ptr(motion), width, max_leaf, nodes_p, cap,
+        return lib.rrt_build_bvh_ex(_lib.ptr(scene.spheres), n, ctypes.byref(ext), width, max_leaf, nodes_p, cap,
                                     order_p, ctypes.byref(info))
 
     _lib.check(build(None, 0, None))
     nodes = np.zeros(info.node_bytes, dtype=np.uint8)
-    order = np.zeros(max(n, 1), dtype=np.uint32)
+    order = np.zeros(max(n_prims, 1), dtype=np.uint32)
     _lib.check(build(_lib.ptr(nodes), nodes.size, _lib.ptr(order)))
-    return nodes, order[:n], info.as_dict()
+    return nodes, order[:n_prims], info.as_dict()
 
 
 def make_tile(band_rows=16, rank=0, n_ranks=1, sample_begin=0, sample_end=0) -> _lib.RrtTile:

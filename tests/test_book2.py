@@ -115,7 +115,7 @@ def test_next_week_scene_structure():
     o = rrt.next_week_scene(2, dict(image_width=64, samples_per_pixel=3, background=(0.1, 0.2, 0.3)))
     assert (o.width, o.spp) == (64, 3) and np.allclose(o.camera["background"][0, :3], [0.1, 0.2, 0.3])
     with pytest.raises(rrt.RrtError):
-        rrt.next_week_scene(5)
+        rrt.next_week_scene(8)  # cornell_smoke (ConstantMedium) is not in the ABI yet
 
 
 def test_moving_sphere_boxes_span_both_ends():
@@ -143,7 +143,7 @@ def test_moving_sphere_boxes_span_both_ends():
 
 
 # ---- the oracle's two arithmetics and two trees agree on book-2 scenes -------------------------------
-@pytest.mark.parametrize("scene", [1, 2, 3, 4])
+@pytest.mark.parametrize("scene", [1, 2, 3, 4, 5, 6, 7])
 def test_book2_books_vs_twin_statistical(scene):
     sc = rrt.next_week_scene(scene, dict(image_width=48, samples_per_pixel=8, max_depth=10))
     t, rt, _ = oracle.render(sc, oracle.TWIN, threads=8)
@@ -154,7 +154,7 @@ def test_book2_books_vs_twin_statistical(scene):
     assert abs(rt - rb) / rb < 0.01
 
 
-@pytest.mark.parametrize("scene", [1, 2, 4])
+@pytest.mark.parametrize("scene", [1, 2, 4, 5, 6, 7])
 def test_book2_kbvh_agrees_with_books_tree(scene):
     sc = rrt.next_week_scene(scene, dict(image_width=48, samples_per_pixel=4, max_depth=10))
     a, ra, _ = oracle.render(sc, oracle.TWIN, threads=4)
@@ -170,3 +170,134 @@ def test_motion_blur_changes_the_image():
     still = rrt.SceneData(sc.camera, sc.spheres, sc.materials, flags=sc.flags, motion=None)
     b, _, _ = oracle.render(still, oracle.TWIN, threads=8)
     assert not np.array_equal(a, b)
+
+
+# ---- quads (the_next_week/quad.rs) and the quad scenes (mod.rs:257-431) --------------------------
+def numpy_quad_hit(q, u, v, o, d, tmin, tmax):
+    """quad.rs:21-37 + 61-87 in float64 numpy."""
+    q, u, v, o, d = (np.asarray(x, np.float64) for x in (q, u, v, o, d))
+    n = np.cross(u, v)
+    normal = n / np.sqrt(n @ n)
+    w = n / (n @ n)
+    denom = normal @ d
+    if abs(denom) < 1e-8:
+        return None
+    t = (normal @ q - normal @ o) / denom
+    if not (tmin <= t <= tmax):
+        return None
+    hp = o + t * d - q
+    alpha, beta = w @ np.cross(hp, v), w @ np.cross(u, hp)
+    if not (0 <= alpha <= 1 and 0 <= beta <= 1):
+        return None
+    front = d @ normal < 0
+    return t, (normal if front else -normal), front
+
+
+def test_quad_hit_matches_numpy_restatement():
+    rng = np.random.default_rng(11)
+    hits = 0
+    for _ in range(3000):
+        q, u, v = (np.float32(rng.uniform(-2, 2, 3)).astype(np.float64) for _ in range(3))
+        o = rng.uniform(-5, 5, 3)
+        target = q + rng.uniform(-0.2, 1.2) * u + rng.uniform(-0.2, 1.2) * v
+        d = target - o
+        got = oracle.quad_hit(q, u, v, o, d)
+        want = numpy_quad_hit(q, u, v, o, d, 0.001, np.inf)
+        assert (got is None) == (want is None) or abs(abs(np.cross(u, v) @ d)) < 1e-6
+        if got is not None and want is not None:
+            hits += 1
+            assert got[0] == pytest.approx(want[0], rel=1e-9)
+            assert np.allclose(got[1], want[1], atol=1e-12) and got[2] == want[2]
+    assert hits > 1000
+    # f32 twin: same decisions away from the edges, t to f32 precision
+    for _ in range(500):
+        q, u, v = (np.float32(rng.uniform(-2, 2, 3)).astype(np.float64) for _ in range(3))
+        o = rng.uniform(-5, 5, 3)
+        d = q + rng.uniform(0.05, 0.95) * u + rng.uniform(0.05, 0.95) * v - o
+        a, b = oracle.quad_hit(q, u, v, o, d, f32=True), oracle.quad_hit(q, u, v, o, d)
+        if b is not None and abs(np.cross(u, v) @ d) > 1e-3:
+            assert a is not None and a[0] == pytest.approx(b[0], rel=1e-4, abs=1e-4)
+
+
+def test_quad_hit_edges():
+    q, u, v = (0.0, 0.0, 0.0), (1.0, 0.0, 0.0), (0.0, 1.0, 0.0)
+    assert oracle.quad_hit(q, u, v, (0.5, 0.5, 1.0), (1.0, 0.0, 0.0)) is None  # parallel: |denom| < 1e-8
+    t, n, front = oracle.quad_hit(q, u, v, (0.5, 0.5, 2.0), (0.0, 0.0, -1.0))
+    assert t == 2.0 and front and list(n) == [0.0, 0.0, 1.0]  # normal = unit(cross(u, v)) = +z
+    t, n, front = oracle.quad_hit(q, u, v, (0.5, 0.5, -2.0), (0.0, 0.0, 1.0))
+    assert t == 2.0 and not front and list(n) == [0.0, 0.0, -1.0]  # back face: flipped
+    for f32 in (False, True):
+        # corners and edges are inside (Interval::contains is closed) ...
+        for x, y in ((0.0, 0.0), (1.0, 1.0), (1.0, 0.0), (0.0, 0.5)):
+            assert oracle.quad_hit(q, u, v, (x, y, 1.0), (0.0, 0.0, -1.0), f32=f32) is not None
+        assert oracle.quad_hit(q, u, v, (1.0 + 2 ** -20, 0.5, 1.0), (0.0, 0.0, -1.0), f32=f32) is None
+        # ... and so is t == ray_t.max / ray_t.min (a sphere's `surrounds` would reject both)
+        assert oracle.quad_hit(q, u, v, (0.5, 0.5, 1.0), (0.0, 0.0, -1.0), tmax=1.0, f32=f32) is not None
+        assert oracle.quad_hit(q, u, v, (0.5, 0.5, 1.0), (0.0, 0.0, -1.0), tmax=0.999, f32=f32) is None
+        assert oracle.quad_hit(q, u, v, (0.5, 0.5, 1.0), (0.0, 0.0, -1.0), tmin=1.0, f32=f32) is not None
+    # behind the origin / below tmin
+    assert oracle.quad_hit(q, u, v, (0.5, 0.5, 1.0), (0.0, 0.0, 1.0)) is None
+    assert oracle.quad_hit(q, u, v, (0.5, 0.5, 0.0005), (0.0, 0.0, -1.0)) is None
+
+
+def test_quad_scene_structure():
+    s5 = rrt.next_week_scene(5)
+    assert len(s5.spheres) == 0 and len(s5.quads) == 5 and len(s5.materials) == 5
+    assert (s5.width, s5.height, s5.spp) == (400, 400, 100)
+    assert np.allclose(s5.camera["background"][0, :3], [0.7, 0.8, 1.0])
+    s6 = rrt.next_week_scene(6)
+    assert len(s6.spheres) == 3 and len(s6.quads) == 1
+    kinds = s6.materials["kind"]
+    assert kinds[s6.spheres["material_index"]].tolist() == [6, 6, 4] and kinds[s6.quads["material_index"][0]] == 4
+    assert s6.spheres["material_index"][2] == s6.quads["material_index"][0]  # one shared DiffuseLight(4,4,4)
+    assert np.allclose(s6.camera["background"][0, :3], 0.0) and s6.perlin is not None and s6.motion is None
+    s7 = rrt.next_week_scene(7)
+    assert len(s7.spheres) == 0 and len(s7.quads) == 6 + 2 * 6 and len(s7.materials) == 4
+    assert (s7.width, s7.height, s7.spp) == (600, 600, 200)
+    lights = s7.materials["kind"][s7.quads["material_index"]] == 4
+    assert lights.sum() == 1 and np.allclose(s7.materials["albedo_fuzz"][s7.quads["material_index"][lights][0], :3], 15)
+
+
+def test_cornell_boxes_are_rotated_and_translated():
+    """make_box + RotateY + Translate (quad.rs:95-119, hittable.rs:65-170) baked into world-space
+    quads: the 8 corners of each box are the rotated, translated corners of the axis-aligned box."""
+    s7 = rrt.next_week_scene(7)
+    for k, (size, deg, off) in enumerate([((165, 330, 165), 15.0, (265, 0, 295)), ((165, 165, 165), -18.0, (130, 0, 65))]):
+        qs = s7.quads[6 + 6 * k: 12 + 6 * k]
+        corners = set()
+        for qd in qs:
+            q, u, v = (qd[f][:3].astype(np.float64) for f in ("q", "u", "v"))
+            for p in (q, q + u, q + v, q + u + v):
+                corners.add(tuple(np.round(p, 3)))
+        th = np.radians(deg)
+        want = set()
+        for x in (0, size[0]):
+            for y in (0, size[1]):
+                for z in (0, size[2]):
+                    want.add(tuple(np.round([np.cos(th) * x + np.sin(th) * z + off[0], y + off[1],
+                                             -np.sin(th) * x + np.cos(th) * z + off[2]], 3)))
+        assert len(corners) == 8 and all(min(np.abs(np.array(c) - np.array(w)).max() for w in want) < 2e-3
+                                         for c in corners)
+
+
+def test_quad_bvh_boxes_contain_quads():
+    sc = rrt.next_week_scene(7)
+    nodes, order, info = build_bvh(sc)
+    assert info["width"] == 2 and len(order) == 18 and sorted(order.tolist()) == list(range(18))
+    f = nodes.view(np.float32).reshape(-1, 16)
+    links = nodes.view(np.int32).reshape(-1, 16)[:, 12:16]
+    checked = 0
+    for n in range(len(f)):
+        for child, (lo, hi) in enumerate([((0, 2, 4), (1, 3, 5)), ((6, 8, 10), (7, 9, 11))]):
+            cnt = links[n, 2 + child]
+            if cnt <= 0:
+                continue
+            first = links[n, child]
+            blo, bhi = f[n, list(lo)], f[n, list(hi)]
+            for i in range(first, first + cnt):
+                qd = sc.quads[order[i]]
+                q, u, v = (qd[k][:3] for k in ("q", "u", "v"))
+                for p in (q, q + u, q + v, q + u + v):
+                    assert np.all(blo <= p) and np.all(p <= bhi)
+                checked += 1
+    assert checked == 18

@@ -27,6 +27,10 @@ def scenes(spp_scale):
     yield "NW2 checkered_spheres 1920x1080", rrt.next_week_scene(2, dict(hd, samples_per_pixel=s(256)))
     yield "NW3 earth 1920x1080", rrt.next_week_scene(3, dict(hd, samples_per_pixel=s(256)))
     yield "NW4 perlin_spheres 1920x1080", rrt.next_week_scene(4, dict(hd, samples_per_pixel=s(256)))
+    sq = dict(image_width=1080, max_depth=50)
+    yield "NW5 quads 1080x1080", rrt.next_week_scene(5, dict(sq, samples_per_pixel=s(256)))
+    yield "NW6 simple_light 1920x1080", rrt.next_week_scene(6, dict(hd, samples_per_pixel=s(256)))
+    yield "NW7 cornell_box 1080x1080", rrt.next_week_scene(7, dict(sq, samples_per_pixel=s(256)))
 
 
 def main():
@@ -59,7 +63,7 @@ def main():
         ds.close()
         rays = ctr["rays"] / a.iters
         row = dict(scene=name, width=sc.width, height=sc.height, spp=sc.spp, max_depth=sc.max_depth,
-                   spheres=len(sc.spheres), kernel_ms=round(ms, 3), rays_per_frame=int(rays),
+                   spheres=len(sc.spheres), quads=0 if sc.quads is None else len(sc.quads), kernel_ms=round(ms, 3), rays_per_frame=int(rays),
                    mrays_per_s=round(rays / ms / 1e3, 1), rays_per_path=round(rays / (sc.width * sc.height * sc.spp), 3),
                    bvh_nodes=info["n_nodes"])
         rows.append(row)
