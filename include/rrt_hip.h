@@ -26,8 +26,8 @@
 extern "C" {
 #endif
 
-/* 1: book 1; 2: RrtSceneExt (motion, Perlin), kinds 5-6; 3: quads in RrtSceneExt, rrt_build_next_week_scene
- * with separate material / quad outputs. */
+/* 1: book 1; 2: RrtSceneExt (motion, Perlin), kinds 5-6; 3: quads and constant-density media in
+ * RrtSceneExt, kind 7, rrt_build_next_week_scene with separate material / quad / medium outputs. */
 #define RRT_ABI_VERSION 3u
 
 /* ---- scene ABI (== src/gpu/mod.rs:13-42) ------------------------------------------ */
@@ -61,7 +61,9 @@ typedef struct RrtSphere {
  *   5 = Lambertian with a solid-colour CheckerTexture: albedo_fuzz.xyz = even colour,
  *       albedo_fuzz[3] = inv_scale (1/scale), odd colour = (ref_idx, bits of _pad[0], bits of _pad[1])
  *   6 = Lambertian with a NoiseTexture: albedo_fuzz[3] = scale, _pad[0] = Perlin table index
- *       into RrtSceneExt.perlin */
+ *       into RrtSceneExt.perlin
+ *   7 = Isotropic (material.rs:137-158), albedo_fuzz.xyz = albedo: the phase function of a
+ *       medium (RrtMedium); scatters into random_unit_vector() */
 typedef struct RrtMaterial {
     float albedo_fuzz[4];
     uint32_t kind;
@@ -76,7 +78,8 @@ enum {
     RRT_MAT_TEXTURED_LAMBERTIAN = 3,
     RRT_MAT_DIFFUSE_LIGHT = 4,
     RRT_MAT_CHECKER_LAMBERTIAN = 5,
-    RRT_MAT_NOISE_LAMBERTIAN = 6
+    RRT_MAT_NOISE_LAMBERTIAN = 6,
+    RRT_MAT_ISOTROPIC = 7
 };
 
 /* == Perlin (the_next_week/perlin.rs:4-22): 256 unit random vectors and the three
@@ -101,18 +104,45 @@ typedef struct RrtQuad {
     uint32_t _pad[3];
 } RrtQuad;
 
+/* == ConstantMedium (the_next_week/constant_medium.rs), 48 B: a volume of constant density inside a
+ * boundary — a sphere (boundary_kind 0: center xyz, radius in `sphere`) or a set of quads
+ * (boundary_kind 1: RrtSceneExt.boundary_quads[first .. first + count), e.g. a baked make_box).
+ * The boundary is not a surface of the scene (add it separately if it is one). material_index
+ * names the phase function (RRT_MAT_ISOTROPIC). Free-flight draw: the reference takes
+ * `random_double()` from its entropy stream inside hit(), so its stream position depends on the
+ * BVH walk; here the draw is u = splitmix64(path_rng ^ (bounce << 32) ^ medium) >> 40 (24 bits,
+ * times 2^-24) — one independent uniform per (path, segment, medium), the same whichever order a
+ * BVH tests the primitives in. hit_distance = (-1/density) * ln(u) in f32 (a Cephes logf). */
+typedef struct RrtMedium {
+    float sphere[4];
+    uint32_t boundary_kind;
+    uint32_t first;
+    uint32_t count;
+    uint32_t material_index;
+    float density;
+    uint32_t _pad[3];
+} RrtMedium;
+
+enum { RRT_BOUNDARY_SPHERE = 0, RRT_BOUNDARY_QUADS = 1 };
+
 /* Book-2 scene data beyond the flat sphere/material ABI. NULL = none.
  * sphere_motion: n_spheres x 4 floats, (center2 - center1).xyz of Sphere::new_moving
  * (the_next_week/sphere.rs:24-40; the sphere's center at ray time t is center1 + t*motion;
  * zero = static). Requires RRT_FLAG_RAY_TIME (rays carry the camera's time draw).
  * quads: n_quads quads (materials: Lambertian, checker, noise, metal, dielectric or light;
- * not image-textured). */
+ * not image-textured). media: n_media constant-density volumes; boundary_quads: the quads their
+ * quad boundaries index (material_index unused). Primitive order for rrt_build_bvh_ex:
+ * spheres, then quads (n_spheres + j), then media (n_spheres + n_quads + m). */
 typedef struct RrtSceneExt {
     const float *sphere_motion;
     const RrtPerlin *perlin;
     uint32_t n_perlin;
     uint32_t n_quads;
     const RrtQuad *quads;
+    const RrtMedium *media;
+    uint32_t n_media;
+    uint32_t n_boundary_quads;
+    const RrtQuad *boundary_quads;
 } RrtSceneExt;
 
 /* Image texture, RGB8 row-major (rtw_image.rs:57-67 `to_rgb8().into_raw()`). Borrowed. */
@@ -275,19 +305,36 @@ int32_t rrt_build_in_one_weekend_scene(const RrtOverrides *ov, uint64_t seed, in
                                        RrtCamera *cam, RrtSphere *spheres, RrtMaterial *materials,
                                        uint32_t sphere_cap, uint32_t *n_spheres);
 
-/* Book-2 scenes (the_next_week/mod.rs:68-431) flattened into the ABI: 1 bouncing_spheres,
- * 2 checkered_spheres, 3 earth, 4 perlin_spheres, 5 quads, 6 simple_light, 7 cornell_box.
- * Random draws come from SmallRng(seed) in the books' order (the reference uses the entropy
- * RNG: parity unpinned). Writes up to sphere_cap spheres and motion rows (motion may be NULL),
- * up to material_cap materials, up to quad_cap quads (instanced boxes baked to world space)
- * and up to perlin_cap Perlin tables; the n_* outputs are the counts needed (call with caps 0
- * to size). The earth texture (scene 3) is texture index 0: the caller supplies the image.
- * The camera carries book 2's background (bg_mode 1); render with RRT_FLAG_RAY_TIME. */
-int32_t rrt_build_next_week_scene(int32_t scene, const RrtOverrides *ov, uint64_t seed, RrtCamera *cam,
-                                  RrtSphere *spheres, float *motion, uint32_t sphere_cap, uint32_t *n_spheres,
-                                  RrtMaterial *materials, uint32_t material_cap, uint32_t *n_materials,
-                                  RrtQuad *quads, uint32_t quad_cap, uint32_t *n_quads,
-                                  RrtPerlin *perlin, uint32_t perlin_cap, uint32_t *n_perlin);
+/* Book-2 scenes (the_next_week/mod.rs:68-587) flattened into the ABI: 1 bouncing_spheres,
+ * 2 checkered_spheres, 3 earth, 4 perlin_spheres, 5 quads, 6 simple_light, 7 cornell_box,
+ * 8 cornell_smoke, 9 final_scene(800, 10000, 40), 10 final_scene(400, 250, 4) (main.rs's
+ * default arm). Random draws come from SmallRng(seed) in the books' order (the reference uses
+ * the entropy RNG: parity unpinned). Instanced geometry (make_box, RotateY, Translate, the
+ * rotated sphere cluster of final_scene) is baked to world space. The caller sets the *_cap
+ * fields and buffers (a buffer may be NULL with cap 0 to size); every n_* is set to the count
+ * needed. uses_texture0 = 1 when a material samples texture 0, the earth image the caller
+ * supplies. The camera carries book 2's background (bg_mode 1); render with RRT_FLAG_RAY_TIME
+ * and an RrtSceneExt over these arrays. */
+typedef struct RrtNextWeekScene {
+    RrtCamera camera;
+    RrtSphere *spheres;
+    float *sphere_motion; /* sphere_cap x 4 floats, may be NULL */
+    RrtMaterial *materials;
+    RrtQuad *quads;
+    RrtPerlin *perlin;
+    RrtMedium *media;
+    RrtQuad *boundary_quads;
+    uint32_t sphere_cap, n_spheres;
+    uint32_t material_cap, n_materials;
+    uint32_t quad_cap, n_quads;
+    uint32_t perlin_cap, n_perlin;
+    uint32_t media_cap, n_media;
+    uint32_t boundary_quad_cap, n_boundary_quads;
+    uint32_t uses_texture0;
+    uint32_t _pad;
+} RrtNextWeekScene;
+
+int32_t rrt_build_next_week_scene(int32_t scene, const RrtOverrides *ov, uint64_t seed, RrtNextWeekScene *out);
 
 /* Camera::initialize (in_one_weekend/camera.rs:102-150) in f64, cast to the f32 ABI as
  * gpu/mod.rs:278-298 does. lookfrom/lookat/vup are 3-vectors. */

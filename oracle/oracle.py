@@ -44,6 +44,10 @@ def load() -> ctypes.CDLL:
                                        c_uint32, c_uint32, c_uint32, c_uint32, c_int, P, P, P, c_uint32]
     lib.oracle_sin_f32.restype = None
     lib.oracle_sin_f32.argtypes = [c_uint32, P, P]
+    lib.oracle_log_f32.restype = None
+    lib.oracle_log_f32.argtypes = [c_uint32, P, P]
+    lib.oracle_medium_u.restype = None
+    lib.oracle_medium_u.argtypes = [c_uint32, P, P, P]
     lib.oracle_book2_textures.restype = None
     lib.oracle_book2_textures.argtypes = [c_int, P, c_double, c_double, c_uint32, P, P, P, P]
     lib.oracle_rtow_scene.restype = c_int
@@ -85,14 +89,16 @@ class _Tex(ctypes.Structure):
 
 class _Ext(ctypes.Structure):  # RrtSceneExt (include/rrt_hip.h)
     _fields_ = [("sphere_motion", c_void_p), ("perlin", c_void_p), ("n_perlin", c_uint32), ("n_quads", c_uint32),
-                ("quads", c_void_p)]
+                ("quads", c_void_p), ("media", c_void_p), ("n_media", c_uint32), ("n_boundary_quads", c_uint32),
+                ("boundary_quads", c_void_p)]
 
 
 def _ext(scene):
     """(pointer to RrtSceneExt or None, keep-alive) from the scene's book-2 motion / Perlin / quad data."""
     motion, perlin = getattr(scene, "motion", None), getattr(scene, "perlin", None)
-    quads = getattr(scene, "quads", None)
-    if motion is None and perlin is None and quads is None:
+    quads, media = getattr(scene, "quads", None), getattr(scene, "media", None)
+    bquads = getattr(scene, "boundary_quads", None)
+    if motion is None and perlin is None and quads is None and media is None:
         return None, []
     e, keep = _Ext(), []
     if motion is not None:
@@ -111,6 +117,18 @@ def _ext(scene):
         keep.append(q)
         e.quads = q.ctypes.data
         e.n_quads = len(q)
+    if media is not None:
+        md = np.ascontiguousarray(media)
+        assert md.dtype.itemsize == 48, "RrtMedium records"
+        keep.append(md)
+        e.media = md.ctypes.data
+        e.n_media = len(md)
+    if bquads is not None:
+        bq = np.ascontiguousarray(bquads)
+        assert bq.dtype.itemsize == 64, "RrtQuad records"
+        keep.append(bq)
+        e.boundary_quads = bq.ctypes.data
+        e.n_boundary_quads = len(bq)
     keep.append(e)
     return ctypes.cast(ctypes.byref(e), c_void_p), keep
 
@@ -254,6 +272,25 @@ def acos_atan2_f32(x, y):
     a, b = c_float(0), c_float(0)
     lib.oracle_acos_atan2_f32(x, y, ctypes.byref(a), ctypes.byref(b))
     return a.value, b.value
+
+
+def log_f32(x):
+    """The f32 Cephes log of the kernel (rrt_logf) at each element of x."""
+    lib = load()
+    xs = np.ascontiguousarray(x, dtype=np.float32).ravel()
+    out = np.zeros_like(xs)
+    lib.oracle_log_f32(xs.size, _p(xs), _p(out))
+    return out
+
+
+def medium_u(seg, medium):
+    """The media free-flight uniforms u(seg, medium) (include/rrt_hip.h RrtMedium)."""
+    lib = load()
+    sg = np.ascontiguousarray(seg, dtype=np.uint64).ravel()
+    md = np.ascontiguousarray(np.broadcast_to(medium, sg.shape), dtype=np.uint32)
+    out = np.zeros(sg.size, dtype=np.float32)
+    lib.oracle_medium_u(sg.size, _p(sg), _p(md), _p(out))
+    return out
 
 
 def sin_f32(x):

@@ -215,12 +215,16 @@ template <class T> T surface_area(const Aabb<T> &b) {
     const T a = b.ax[0].size(), c = b.ax[1].size(), d = b.ax[2].size();
     return T(2) * (a * c + a * d + c * d);
 }
-template <class T> bool aabb_hit(const Aabb<T> &box, Vec3<T> o, Vec3<T> d, Interval<T> ray_t) {  // aabb.rs:52-85
+// The slab arithmetic runs in f64 for both arithmetics: a box test only prunes, and in f32 the
+// reference's (min - o) * (1/d) loses the 1e-4 padding of a flat box at |o| ~ 1e3 (the Cornell
+// walls: 554.99994 + 800 rounds to 1355), rejecting rays that hit the face.
+template <class T> bool aabb_hit(const Aabb<T> &box, Vec3<T> o, Vec3<T> d, Interval<T> ray_in) {  // aabb.rs:52-85
+    Interval<double> ray_t{(double)ray_in.min, (double)ray_in.max};
     for (int axis = 0; axis < 3; ++axis) {
-        const Interval<T> ax = box.ax[axis];
-        const T adinv = T(1) / d[axis];
-        const T t0 = (ax.min - o[axis]) * adinv;
-        const T t1 = (ax.max - o[axis]) * adinv;
+        const Interval<double> ax{(double)box.ax[axis].min, (double)box.ax[axis].max};
+        const double adinv = 1.0 / (double)d[axis];
+        const double t0 = (ax.min - (double)o[axis]) * adinv;
+        const double t1 = (ax.max - (double)o[axis]) * adinv;
         if (t0 < t1) {
             if (t0 > ray_t.min) ray_t.min = t0;
             if (t1 < ray_t.max) ray_t.max = t1;
@@ -232,6 +236,34 @@ template <class T> bool aabb_hit(const Aabb<T> &box, Vec3<T> o, Vec3<T> d, Inter
     }
     return true;
 }
+
+// Cephes logf: the kernel's rrt_logf op for op (x > 0 finite or 0).
+float cephes_logf(float x) {
+    if (x == 0.0f) return -std::numeric_limits<float>::infinity();
+    uint32_t b;
+    std::memcpy(&b, &x, 4);
+    int e = (int)((b >> 23) & 255u) - 126;
+    const uint32_t mb = (b & 0x807fffffu) | 0x3f000000u;
+    float m;
+    std::memcpy(&m, &mb, 4);
+    if (m < 0.707106781186547524f) {
+        e -= 1;
+        m = m + m - 1.0f;
+    } else {
+        m = m - 1.0f;
+    }
+    const float z = m * m;
+    float y = ((((((((7.0376836292e-2f * m - 1.1514610310e-1f) * m + 1.1676998740e-1f) * m - 1.2420140846e-1f) * m +
+                   1.4249322787e-1f) * m - 1.6668057665e-1f) * m + 2.0000714765e-1f) * m - 2.4999993993e-1f) * m +
+               3.3333331174e-1f) * m * z;
+    const float fe = (float)e;
+    y = y + -2.12194440e-4f * fe;
+    y = y + -0.5f * z;
+    float r = m + y;
+    r = r + 0.693359375f * fe;
+    return r;
+}
+template <class T> T t_log(T x) { if constexpr (std::is_same_v<T, float>) return cephes_logf(x); else return std::log(x); }
 
 // ---- scene in T ---------------------------------------------------------------------------------
 template <class T> struct Sphere {
@@ -270,6 +302,16 @@ template <class T> QuadT<T> make_quad(const RrtQuad &rq) {
     qd.bbox = from_boxes(from_points(qd.q, qd.q + qd.u + qd.v), from_points(qd.q + qd.u, qd.q + qd.v));
     return qd;
 }
+// ConstantMedium (the_next_week/constant_medium.rs) over a boundary sphere or boundary quads.
+template <class T> struct MediumT {
+    uint32_t kind;  // 0 sphere, 1 quads [first, first + count) of World::bquads
+    Vec3<T> center;
+    T radius;
+    uint32_t first, count;
+    T neg_inv_density;  // -1/density in f64, rounded to T (constant_medium.rs:24)
+    uint32_t mat;
+    Aabb<T> bbox;
+};
 template <class T> struct Material {
     uint32_t kind;
     Vec3<T> albedo;
@@ -306,6 +348,8 @@ template <class T> struct BvhNode {
 template <class T> struct World {
     std::vector<Sphere<T>> spheres;
     std::vector<QuadT<T>> quads;  // primitive n_spheres + j
+    std::vector<MediumT<T>> media;  // primitive n_spheres + n_quads + m
+    std::vector<QuadT<T>> bquads;  // media boundaries
     std::vector<Material<T>> mats;
     std::vector<Texture> texs;
     std::vector<PerlinT<T>> perlin;
@@ -402,13 +446,17 @@ template <class T> struct World {
     }
 
     const Aabb<T> &prim_box(int32_t p) const {
-        return (size_t)p < spheres.size() ? spheres[p].bbox : quads[p - spheres.size()].bbox;
+        if ((size_t)p < spheres.size()) return spheres[p].bbox;
+        if ((size_t)p < spheres.size() + quads.size()) return quads[p - spheres.size()].bbox;
+        return media[p - spheres.size() - quads.size()].bbox;
     }
 
     // Quad::hit (the_next_week/quad.rs:61-87): t in the closed interval, (alpha, beta) in [0,1]^2.
     bool hit_quad(int32_t j, Vec3<T> o, Vec3<T> d, Interval<T> ray_t, T &t_out, uint64_t *tests) const {
         if (tests) ++*tests;
-        const QuadT<T> &qd = quads[j];
+        return quad_hit(quads[j], o, d, ray_t, t_out);
+    }
+    static bool quad_hit(const QuadT<T> &qd, Vec3<T> o, Vec3<T> d, Interval<T> ray_t, T &t_out) {
         const T denom = dot(qd.normal, d);
         if (std::fabs(denom) < L(1e-8)) return false;
         const T t = (qd.D - dot(qd.normal, o)) / denom;
@@ -423,9 +471,70 @@ template <class T> struct World {
         return true;
     }
 
-    bool hit_prim(int32_t p, Vec3<T> o, Vec3<T> d, T time, Interval<T> ray_t, T &t_out, uint64_t *tests) const {
+    bool hit_prim(int32_t p, Vec3<T> o, Vec3<T> d, T time, Interval<T> ray_t, T &t_out, uint64_t *tests,
+                  uint64_t seg) const {
         if ((size_t)p < spheres.size()) return hit_sphere(p, o, d, time, ray_t, t_out, tests);
-        return hit_quad(p - (int32_t)spheres.size(), o, d, ray_t, t_out, tests);
+        const size_t j = p - spheres.size();
+        if (j < quads.size()) return hit_quad((int32_t)j, o, d, ray_t, t_out, tests);
+        if (tests) ++*tests;
+        return hit_medium((uint32_t)(j - quads.size()), o, d, ray_t, t_out, seg);
+    }
+
+    // ConstantMedium::hit (constant_medium.rs:40-84). The boundary's hits over (-inf, inf) and
+    // after t1 + 0.0001; the free-flight uniform is the per-(path, segment, medium) draw of
+    // include/rrt_hip.h (seg = path RNG state ^ bounce << 32), ln by Cephes logf in f32.
+    bool hit_medium(uint32_t m, Vec3<T> o, Vec3<T> d, Interval<T> ray_t, T &t_out, uint64_t seg) const {
+        const MediumT<T> &md = media[m];
+        const T inf = std::numeric_limits<T>::infinity();
+        T t1, t2;
+        if (md.kind == RRT_BOUNDARY_SPHERE) {
+            if (!sphere_root(md.center, md.radius, o, d, Interval<T>{-inf, inf}, t1)) return false;
+            if (!sphere_root(md.center, md.radius, o, d, Interval<T>{t1 + L(0.0001), inf}, t2)) return false;
+        } else {
+            auto list_hit = [&](Interval<T> iv, T &t_hit) {  // HittableList::hit over the boundary
+                bool any = false;
+                for (uint32_t k = 0; k < md.count; ++k) {
+                    T t;
+                    if (quad_hit(bquads[md.first + k], o, d, iv, t)) {
+                        any = true;
+                        iv.max = t;
+                        t_hit = t;
+                    }
+                }
+                return any;
+            };
+            if (!list_hit(Interval<T>{-inf, inf}, t1)) return false;
+            if (!list_hit(Interval<T>{t1 + L(0.0001), inf}, t2)) return false;
+        }
+        if (t1 < ray_t.min) t1 = ray_t.min;
+        if (t2 > ray_t.max) t2 = ray_t.max;
+        if (t1 >= t2) return false;
+        if (t1 < T(0)) t1 = T(0);
+        const T ray_length = length(d);
+        const T inside = (t2 - t1) * ray_length;
+        const T u = (T)(uint32_t)(splitmix64(seg ^ (uint64_t)m) >> 40) * lit<T>(0x1.0p-24, 0x1.0p-24f);
+        const T hit_distance = md.neg_inv_density * t_log<T>(u);
+        if (hit_distance > inside) return false;
+        t_out = t1 + hit_distance / ray_length;
+        return true;
+    }
+
+    // Sphere::hit's root selection for a static sphere and an interval.
+    static bool sphere_root(Vec3<T> center, T radius, Vec3<T> o, Vec3<T> d, Interval<T> ray_t, T &t_out) {
+        const Vec3<T> oc = center - o;
+        const T a = length_squared(d);
+        const T h = dot(d, oc);
+        const T c = length_squared(oc) - radius * radius;
+        const T disc = h * h - a * c;
+        if (disc < T(0)) return false;
+        const T sqrtd = std::sqrt(disc);
+        T root = (h - sqrtd) / a;
+        if (!ray_t.surrounds(root)) {
+            root = (h + sqrtd) / a;
+            if (!ray_t.surrounds(root)) return false;
+        }
+        t_out = root;
+        return true;
     }
 
     // Sphere::hit (sphere.rs:24-51): Some(t) iff a root lies in the open interval.
@@ -450,18 +559,19 @@ template <class T> struct World {
 
     // HittableObject::hit dispatch + BvhNode::hit (bvh.rs:159-172), left first, right with
     // max = left.t, result = right.or(left).
-    bool hit(ChildRef ref, Vec3<T> o, Vec3<T> d, T time, Interval<T> ray_t, Hit<T> &rec, uint64_t *tests) const {
+    bool hit(ChildRef ref, Vec3<T> o, Vec3<T> d, T time, Interval<T> ray_t, Hit<T> &rec, uint64_t *tests,
+             uint64_t seg) const {
         if (ref.is_sphere) {
             T t;
-            if (!hit_prim(ref.index, o, d, time, ray_t, t, tests)) return false;
+            if (!hit_prim(ref.index, o, d, time, ray_t, t, tests, seg)) return false;
             rec = Hit<T>{t, ref.index};
             return true;
         }
         const BvhNode<T> &n = nodes[ref.index];
         if (!aabb_hit(n.bbox, o, d, ray_t)) return false;
         Hit<T> hl, hr;
-        const bool l = hit(n.left, o, d, time, ray_t, hl, tests);
-        const bool r = hit(n.right, o, d, time, Interval<T>{ray_t.min, l ? hl.t : ray_t.max}, hr, tests);
+        const bool l = hit(n.left, o, d, time, ray_t, hl, tests, seg);
+        const bool r = hit(n.right, o, d, time, Interval<T>{ray_t.min, l ? hl.t : ray_t.max}, hr, tests, seg);
         if (r) { rec = hr; return true; }
         if (l) { rec = hl; return true; }
         return false;
@@ -509,7 +619,7 @@ static inline float max_num(float a, float b) { return (b != b) ? a : ((a != a) 
 // (results are identical either way: fmaf is correctly rounded in both).
 __attribute__((target_clones("fma", "default")))
 bool kbvh_hit(const World<float> &w, const KTree &kt, Vec3<float> o, Vec3<float> d, float time, Hit<float> &rec,
-              uint64_t *tests) {
+              uint64_t *tests, uint64_t seg) {
     KRay r;
     r.ix = 1.0f / d[0];
     r.iy = 1.0f / d[1];
@@ -523,7 +633,7 @@ bool kbvh_hit(const World<float> &w, const KTree &kt, Vec3<float> o, Vec3<float>
     auto leaf = [&](int32_t first, int32_t count) {
         for (int32_t i = first; i < first + count; ++i) {
             float t;
-            if (w.hit_prim((int32_t)kt.order[i], o, d, time, Interval<float>{kTmin, closest}, t, tests)) {
+            if (w.hit_prim((int32_t)kt.order[i], o, d, time, Interval<float>{kTmin, closest}, t, tests, seg)) {
                 closest = t;
                 hit = i;
             }
@@ -654,6 +764,29 @@ void load_world(World<T> &w, Cam<T> &cam, const RrtCamera *c, const RrtSphere *s
         w.quads.push_back(make_quad<T>(ext->quads[j]));
         w.book2 = true;
     }
+    const uint32_t nbq = ext && ext->boundary_quads ? ext->n_boundary_quads : 0u;
+    for (uint32_t j = 0; j < nbq; ++j) w.bquads.push_back(make_quad<T>(ext->boundary_quads[j]));
+    const uint32_t nmd = ext && ext->media ? ext->n_media : 0u;
+    for (uint32_t k = 0; k < nmd; ++k) {
+        const RrtMedium &rm = ext->media[k];
+        MediumT<T> md;
+        md.kind = rm.boundary_kind;
+        md.center = v3(rm.sphere);
+        md.radius = std::max((T)rm.sphere[3], T(0));
+        md.first = rm.first;
+        md.count = rm.count;
+        md.neg_inv_density = (T)(-1.0 / (double)rm.density);
+        md.mat = rm.material_index;
+        if (md.kind == RRT_BOUNDARY_SPHERE) {
+            const Vec3<T> rv = mk(md.radius, md.radius, md.radius);
+            md.bbox = from_points(md.center - rv, md.center + rv);
+        } else {  // HittableList::bounding_box of the boundary faces
+            md.bbox = empty_box<T>();
+            for (uint32_t q = 0; q < md.count; ++q) md.bbox = from_boxes(md.bbox, w.bquads[md.first + q].bbox);
+        }
+        w.media.push_back(md);
+        w.book2 = true;
+    }
     if (ext && ext->perlin)
         for (uint32_t t = 0; t < ext->n_perlin; ++t) {
             PerlinT<T> pt;
@@ -665,7 +798,7 @@ void load_world(World<T> &w, Cam<T> &cam, const RrtCamera *c, const RrtSphere *s
             }
             w.perlin.push_back(pt);
         }
-    const uint32_t np = n + nq;
+    const uint32_t np = n + nq + nmd;
     if (np) {
         std::vector<int32_t> objs(np);
         for (uint32_t i = 0; i < np; ++i) objs[i] = (int32_t)i;
@@ -680,22 +813,29 @@ template <class T> struct Record {
 };
 
 template <class T>
-bool world_hit(const World<T> &w, Vec3<T> o, Vec3<T> d, T time, Record<T> &rec, uint64_t *tests,
+bool world_hit(const World<T> &w, Vec3<T> o, Vec3<T> d, T time, uint64_t seg, Record<T> &rec, uint64_t *tests,
                const KTree *kt = nullptr) {  // camera.rs:187
     Hit<T> h;
     if constexpr (std::is_same_v<T, float>) {
         if (kt) {
-            if (!kbvh_hit(w, *kt, o, d, time, h, tests)) return false;
+            if (!kbvh_hit(w, *kt, o, d, time, h, tests, seg)) return false;
         } else {
             if (w.root.index < 0) return false;
-            if (!w.hit(w.root, o, d, time, Interval<T>{L(0.001), std::numeric_limits<T>::infinity()}, h, tests))
+            if (!w.hit(w.root, o, d, time, Interval<T>{L(0.001), std::numeric_limits<T>::infinity()}, h, tests, seg))
                 return false;
         }
     } else {
         if (w.root.index < 0) return false;
-        if (!w.hit(w.root, o, d, time, Interval<T>{L(0.001), std::numeric_limits<T>::infinity()}, h, tests)) return false;
+        if (!w.hit(w.root, o, d, time, Interval<T>{L(0.001), std::numeric_limits<T>::infinity()}, h, tests, seg))
+            return false;
     }
     rec.p = o + h.t * d;  // Ray::at
+    if ((size_t)h.sphere >= w.spheres.size() + w.quads.size()) {  // medium (constant_medium.rs:76-82)
+        rec.outward = rec.normal = mk(T(1), T(0), T(0));
+        rec.front = true;
+        rec.mat = w.media[h.sphere - w.spheres.size() - w.quads.size()].mat;
+        return true;
+    }
     if ((size_t)h.sphere >= w.spheres.size()) {  // quad (quad.rs:79)
         const QuadT<T> &qd = w.quads[h.sphere - w.spheres.size()];
         rec.outward = qd.normal;
@@ -867,6 +1007,10 @@ bool scatter(const World<T> &w, PathRng &rng, Vec3<T> d_in, const Record<T> &rec
             else dir = refract(ud, rec.normal, ri);
             return true;
         }
+        case RRT_MAT_ISOTROPIC:  // material.rs:153-158
+            dir = random_unit_vector<T>(rng);
+            att = m.albedo;
+            return true;
         default:  // DiffuseLight: scatter -> None
             return false;
     }
@@ -904,7 +1048,8 @@ Vec3<T> ray_color_books(const World<T> &w, const Cam<T> &cam, PathRng &rng, Vec3
     if (depth <= 0) return mk(T(0), T(0), T(0));
     tl.rays++;
     Record<T> rec;
-    if (!world_hit(w, o, d, time, rec, &tl.tests)) return miss_color(cam, d);
+    if (!world_hit(w, o, d, time, rng.s ^ ((uint64_t)(cam.max_depth - depth) << 32), rec, &tl.tests))
+        return miss_color(cam, d);
     const Vec3<T> em = emitted(w, rec);
     Vec3<T> att, dir;
     if (!scatter(w, rng, d, rec, att, dir)) return em;
@@ -925,7 +1070,7 @@ Vec3<T> ray_color_twin(const World<T> &w, const Cam<T> &cam, PathRng &rng, Vec3<
     for (uint32_t k = 0; k < cam.max_depth; ++k) {
         tl.rays++;
         Record<T> rec;
-        if (!world_hit(w, o, d, time, rec, &tl.tests, kt)) return Lp + Tp * miss_color(cam, d);
+        if (!world_hit(w, o, d, time, rng.s ^ ((uint64_t)k << 32), rec, &tl.tests, kt)) return Lp + Tp * miss_color(cam, d);
         const Material<T> &m = w.mats[rec.mat];
         if (m.kind == RRT_MAT_DIFFUSE_LIGHT) return Lp + Tp * m.albedo;
         Vec3<T> att, dir;
@@ -1257,6 +1402,15 @@ void oracle_acos_atan2_f32(float x, float y, float *acos_out, float *atan2_out) 
 // value / checker parity at points p[n][3] with table `pt` (f32 != 0: twin arithmetic).
 void oracle_sin_f32(uint32_t n, const float *x, float *out) {
     for (uint32_t i = 0; i < n; ++i) out[i] = cephes_sinf(x[i]);
+}
+
+void oracle_log_f32(uint32_t n, const float *x, float *out) {
+    for (uint32_t i = 0; i < n; ++i) out[i] = cephes_logf(x[i]);
+}
+
+// The media free-flight uniform of include/rrt_hip.h for (seg, medium) pairs.
+void oracle_medium_u(uint32_t n, const uint64_t *seg, const uint32_t *medium, float *out) {
+    for (uint32_t i = 0; i < n; ++i) out[i] = (float)(uint32_t)(splitmix64(seg[i] ^ (uint64_t)medium[i]) >> 40) * 0x1.0p-24f;
 }
 
 void oracle_book2_textures(int f32, const RrtPerlin *pt, double scale, double inv_scale, uint32_t n, const double *p,

@@ -86,9 +86,24 @@ QUAD_DTYPE = np.dtype([("q", "<f4", 4), ("u", "<f4", 4), ("v", "<f4", 4), ("mate
                        ("_pad", "<u4", 3)])
 
 
+# == RrtMedium (include/rrt_hip.h): boundary sphere or quad range, phase material, density; 48 B
+MEDIUM_DTYPE = np.dtype([("sphere", "<f4", 4), ("boundary_kind", "<u4"), ("first", "<u4"), ("count", "<u4"),
+                         ("material_index", "<u4"), ("density", "<f4"), ("_pad", "<u4", 3)])
+
+
 class RrtSceneExt(ctypes.Structure):
     _fields_ = [("sphere_motion", c_void_p), ("perlin", c_void_p), ("n_perlin", c_uint32), ("n_quads", c_uint32),
-                ("quads", c_void_p)]
+                ("quads", c_void_p), ("media", c_void_p), ("n_media", c_uint32), ("n_boundary_quads", c_uint32),
+                ("boundary_quads", c_void_p)]
+
+
+class RrtNextWeekScene(ctypes.Structure):
+    _fields_ = [("camera", ctypes.c_uint8 * 144), ("spheres", c_void_p), ("sphere_motion", c_void_p),
+                ("materials", c_void_p), ("quads", c_void_p), ("perlin", c_void_p), ("media", c_void_p),
+                ("boundary_quads", c_void_p)] + [
+        (f, c_uint32) for f in ("sphere_cap", "n_spheres", "material_cap", "n_materials", "quad_cap", "n_quads",
+                                "perlin_cap", "n_perlin", "media_cap", "n_media", "boundary_quad_cap",
+                                "n_boundary_quads", "uses_texture0", "_pad")]
 
 
 class RrtOverrides(ctypes.Structure):
@@ -207,8 +222,7 @@ def load() -> ctypes.CDLL:
         "rrt_hip_render_ex": (c_int32, [P, P, c_uint32, P, c_uint32, P, c_uint32, P, c_uint32, c_uint32, c_uint32, P]),
         "rrt_scene_create_ex": (c_int32, [P, P, c_uint32, P, c_uint32, P, c_uint32, P, c_uint32, c_int32, P]),
         "rrt_build_bvh_ex": (c_int32, [P, c_uint32, P, c_uint32, c_uint32, P, c_size_t, P, P]),
-        "rrt_build_next_week_scene": (c_int32, [c_int32, P, c_uint64, P, P, P, c_uint32, P, P, c_uint32, P, P, c_uint32, P,
-                                                P, c_uint32, P]),
+        "rrt_build_next_week_scene": (c_int32, [c_int32, P, c_uint64, P]),
         "rrt_device_count": (c_int32, [P]),
     }
     experiment = "RRT_LIB_PATH" in os.environ  # A/B of older builds: tolerate symbols they lack

@@ -106,14 +106,15 @@ int main(int argc, char **argv) {
     const bool book1 = book == "inoneweekend" || book == "oneweekend" || book == "weekend";
     const bool book2 = book == "thenextweek" || book == "nextweek" || book == "next";  // main.rs:89
     const int scene = positional.size() > 1 ? std::atoi(positional[1].c_str()) : 0;  // main.rs:55
-    if (book2 && !(scene >= 1 && scene <= 7 && scene != 3)) {
+    if (book2 && !(scene >= 1 && scene <= 8 && scene != 3)) {
         std::fprintf(stderr, "HIP backend supports the_next_week scenes 1 (bouncing_spheres), 2 (checkered_spheres), "
-                             "4 (perlin_spheres), 5 (quads), 6 (simple_light) and 7 (cornell_box); scene 3 (earth) "
-                             "needs the texture: use the Python API.\n");
+                             "4 (perlin_spheres), 5 (quads), 6 (simple_light), 7 (cornell_box) and 8 "
+                             "(cornell_smoke); scenes 3 (earth) and 9/other (final_scene) need the earth texture: "
+                             "use the Python API.\n");
         return 2;
     }
     if (!book1 && !book2) {  // main.rs:59-70
-        std::fprintf(stderr, "HIP backend supports in_one_weekend and the_next_week scenes 1, 2, 4-7 only.\n");
+        std::fprintf(stderr, "HIP backend supports in_one_weekend and the_next_week scenes 1, 2, 4-8 only.\n");
         return 2;
     }
 
@@ -121,7 +122,8 @@ int main(int argc, char **argv) {
     uint32_t n = 0, n_mat = 0, n_quads = 0, n_perlin = 0;
     std::vector<RrtSphere> spheres;
     std::vector<RrtMaterial> materials;
-    std::vector<RrtQuad> quads;
+    std::vector<RrtQuad> quads, boundary_quads;
+    std::vector<RrtMedium> media;
     std::vector<float> motion;
     std::vector<RrtPerlin> perlin;
     uint32_t flags = 0;
@@ -139,22 +141,30 @@ int main(int argc, char **argv) {
         n_mat = n;
     } else {
         const uint64_t s2 = seed_set ? seed : 0xB00C0002ull;
-        if (rrt_build_next_week_scene(scene, &ov, s2, &cam, nullptr, nullptr, 0, &n, nullptr, 0, &n_mat, nullptr, 0,
-                                      &n_quads, nullptr, 0, &n_perlin)) {
+        RrtNextWeekScene nw{};
+        if (rrt_build_next_week_scene(scene, &ov, s2, &nw)) {  // sizing pass
             std::fprintf(stderr, "HIP render failed: %s\n", rrt_hip_last_error());
             return 1;
         }
-        spheres.resize(n);
-        materials.resize(n_mat);
-        quads.resize(n_quads);
-        motion.resize((size_t)n * 4);
-        perlin.resize(n_perlin);
-        if (rrt_build_next_week_scene(scene, &ov, s2, &cam, spheres.data(), motion.data(), n, &n, materials.data(),
-                                      n_mat, &n_mat, quads.data(), n_quads, &n_quads, perlin.data(), n_perlin,
-                                      &n_perlin)) {
+        spheres.resize(nw.n_spheres);
+        motion.resize((size_t)nw.n_spheres * 4);
+        materials.resize(nw.n_materials);
+        quads.resize(nw.n_quads);
+        perlin.resize(nw.n_perlin);
+        media.resize(nw.n_media);
+        boundary_quads.resize(nw.n_boundary_quads);
+        nw.spheres = spheres.data(), nw.sphere_cap = nw.n_spheres, nw.sphere_motion = motion.data();
+        nw.materials = materials.data(), nw.material_cap = nw.n_materials;
+        nw.quads = quads.data(), nw.quad_cap = nw.n_quads;
+        nw.perlin = perlin.data(), nw.perlin_cap = nw.n_perlin;
+        nw.media = media.data(), nw.media_cap = nw.n_media;
+        nw.boundary_quads = boundary_quads.data(), nw.boundary_quad_cap = nw.n_boundary_quads;
+        if (rrt_build_next_week_scene(scene, &ov, s2, &nw)) {
             std::fprintf(stderr, "HIP render failed: %s\n", rrt_hip_last_error());
             return 1;
         }
+        cam = nw.camera;
+        n = nw.n_spheres, n_mat = nw.n_materials, n_quads = nw.n_quads, n_perlin = nw.n_perlin;
         flags = RRT_FLAG_RAY_TIME;  // book-2 camera (the_next_week/camera.rs:160)
     }
     RrtSceneExt ext{};
@@ -163,6 +173,10 @@ int main(int argc, char **argv) {
     ext.n_perlin = n_perlin;
     ext.quads = quads.empty() ? nullptr : quads.data();
     ext.n_quads = n_quads;
+    ext.media = media.empty() ? nullptr : media.data();
+    ext.n_media = (uint32_t)media.size();
+    ext.boundary_quads = boundary_quads.empty() ? nullptr : boundary_quads.data();
+    ext.n_boundary_quads = (uint32_t)boundary_quads.size();
     const uint32_t w = (uint32_t)cam.params_f[1], h = (uint32_t)cam.params_f[2];
     const uint32_t spp = (uint32_t)(cam.params_f[3] < 1.0f ? 1.0f : cam.params_f[3]);
     const auto t0 = std::chrono::steady_clock::now();

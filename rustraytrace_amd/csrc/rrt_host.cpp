@@ -509,12 +509,46 @@ void bvh_defaults(uint32_t &width, uint32_t &max_leaf) {
     if (const char *e = std::getenv("RRT_BVH_WIDTH")) width = std::atoi(e) == 4 ? 4 : 2;
 }
 
+// Quad::set_bounding_box (quad.rs:43-47): the box of the four corners, padded.
+static Aabb quad_box(const RrtQuad &qd) {
+    Aabb b;
+    for (int a = 0; a < 3; ++a) {
+        const double q = qd.q[a], u = qd.u[a], v = qd.v[a];
+        const double c[4] = {q, q + u + v, q + u, q + v};
+        b.ax[a] = Interval{std::min(std::min(c[0], c[1]), std::min(c[2], c[3])),
+                           std::max(std::max(c[0], c[1]), std::max(c[2], c[3]))};
+    }
+    return pad(b);
+}
+
+// Book-2 extension arrays with null-safe counts.
+struct ExtView {
+    const float *motion = nullptr;
+    const RrtQuad *quads = nullptr;
+    uint32_t n_quads = 0;
+    const RrtMedium *media = nullptr;
+    uint32_t n_media = 0;
+    const RrtQuad *bquads = nullptr;
+    uint32_t n_bquads = 0;
+    explicit ExtView(const RrtSceneExt *e) {
+        if (!e) return;
+        motion = e->sphere_motion;
+        if (e->quads) quads = e->quads, n_quads = e->n_quads;
+        if (e->media) media = e->media, n_media = e->n_media;
+        if (e->boundary_quads) bquads = e->boundary_quads, n_bquads = e->n_boundary_quads;
+    }
+};
+
 // Sphere boxes (sphere.rs:16-21, aabb.rs:29-34: r = max(radius, 0), padded; a moving sphere's
-// box spans both ends, the_next_week/sphere.rs:31-33), SAH build, flatten. order[i] = original
-// index of the i-th primitive in leaf order.
-FlatBvh build_bvh(const RrtSphere *spheres, uint32_t n_spheres, const float *motion, const RrtQuad *quads,
-                  uint32_t n_quads, uint32_t width, uint32_t max_leaf, std::vector<uint32_t> &order) {
-    std::vector<Aabb> boxes(n_spheres + (size_t)n_quads);
+// box spans both ends, the_next_week/sphere.rs:31-33), quad boxes, medium boxes (the boundary's:
+// constant_medium.rs bounding_box), SAH build, flatten. Primitives: spheres, then quads
+// (n_spheres + j), then media (n_spheres + n_quads + m). order[i] = original index of the i-th
+// primitive in leaf order. The medium ranges are validated by the caller.
+FlatBvh build_bvh(const RrtSphere *spheres, uint32_t n_spheres, const ExtView &ex, uint32_t width,
+                  uint32_t max_leaf, std::vector<uint32_t> &order) {
+    const float *motion = ex.motion;
+    const uint32_t n_quads = ex.n_quads;
+    std::vector<Aabb> boxes(n_spheres + (size_t)n_quads + ex.n_media);
     for (uint32_t i = 0; i < n_spheres; ++i) {
         const double r = std::max((double)spheres[i].center_radius[3], 0.0);
         Aabb b;
@@ -528,18 +562,20 @@ FlatBvh build_bvh(const RrtSphere *spheres, uint32_t n_spheres, const float *mot
         }
         boxes[i] = pad(b);
     }
-    for (uint32_t j = 0; j < n_quads; ++j) {  // Quad::set_bounding_box (quad.rs:43-47)
-        const RrtQuad &qd = quads[j];
-        Aabb b;
-        for (int a = 0; a < 3; ++a) {
-            const double q = qd.q[a], u = qd.u[a], v = qd.v[a];
-            const double c[4] = {q, q + u + v, q + u, q + v};
-            b.ax[a] = Interval{std::min(std::min(c[0], c[1]), std::min(c[2], c[3])),
-                               std::max(std::max(c[0], c[1]), std::max(c[2], c[3]))};
+    for (uint32_t j = 0; j < n_quads; ++j) boxes[n_spheres + j] = quad_box(ex.quads[j]);
+    for (uint32_t m = 0; m < ex.n_media; ++m) {
+        const RrtMedium &md = ex.media[m];
+        Aabb b = aabb_empty();
+        if (md.boundary_kind == RRT_BOUNDARY_SPHERE) {
+            const double r = std::max((double)md.sphere[3], 0.0);
+            for (int a = 0; a < 3; ++a) b.ax[a] = Interval{md.sphere[a] - r, md.sphere[a] + r};
+            b = pad(b);
+        } else {
+            for (uint32_t k = 0; k < md.count; ++k) b = aabb_union(b, quad_box(ex.bquads[md.first + k]));
         }
-        boxes[n_spheres + j] = pad(b);
+        boxes[n_spheres + n_quads + m] = b;
     }
-    const uint32_t n_prims = n_spheres + n_quads;
+    const uint32_t n_prims = n_spheres + n_quads + ex.n_media;
     Builder bld(boxes, max_leaf);
     if (const char *e = std::getenv("RRT_BVH_SPLIT")) bld.sweep = std::strcmp(e, "binned") != 0;
     if (const char *e = std::getenv("RRT_SAH_CT")) bld.node_cost = std::atof(e);
@@ -569,6 +605,7 @@ struct RrtScene {
     float4 *d_prim_motion = nullptr;
     rrt::GPerlin *d_perlin = nullptr;
     rrt::GQuad *d_quads = nullptr;
+    rrt::GMedium *d_media = nullptr;
     uint8_t *d_tex_pool = nullptr;
     rrt::GTexture *d_texs = nullptr;
     unsigned long long *d_counters = nullptr;       // 5 x u64, render launches
@@ -591,6 +628,7 @@ void free_scene(RrtScene *s) {
     (void)hipFree(s->d_prim_motion);
     (void)hipFree(s->d_perlin);
     (void)hipFree(s->d_quads);
+    (void)hipFree(s->d_media);
     (void)hipFree(s->d_tex_pool);
     (void)hipFree(s->d_texs);
     (void)hipFree(s->d_counters);
@@ -689,15 +727,31 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
                             uint32_t n_textures, const RrtSceneExt *ext, uint32_t flags, int32_t device,
                             RrtScene **out) {
     if (!cam || !out) return fail(RRT_E_INVALID, "null camera or out pointer");
-    const float *motion = ext ? ext->sphere_motion : nullptr;
+    ExtView ex(ext);
+    const float *motion = ex.motion;
     const uint32_t n_perlin = ext && ext->perlin ? ext->n_perlin : 0u;
-    const RrtQuad *quads = ext && ext->quads ? ext->quads : nullptr;
-    const uint32_t n_quads = quads ? ext->n_quads : 0u;
+    const RrtQuad *quads = ex.quads;
+    const uint32_t n_quads = ex.n_quads;
     for (uint32_t j = 0; j < n_quads; ++j) {
         if (quads[j].material_index >= n_materials)
             return fail(RRT_E_INVALID, "quad " + std::to_string(j) + " material_index out of range");
         if (materials[quads[j].material_index].kind == RRT_MAT_TEXTURED_LAMBERTIAN)
             return fail(RRT_E_INVALID, "quad " + std::to_string(j) + ": image textures on quads are not supported");
+    }
+    const uint32_t n_media = ex.n_media;
+    for (uint32_t m = 0; m < n_media; ++m) {
+        const RrtMedium &md = ex.media[m];
+        const std::string what = "medium " + std::to_string(m);
+        if (md.material_index >= n_materials || materials[md.material_index].kind != RRT_MAT_ISOTROPIC)
+            return fail(RRT_E_INVALID, what + ": material_index must name an RRT_MAT_ISOTROPIC material");
+        if (!(md.density > 0.0f) || !std::isfinite(md.density))
+            return fail(RRT_E_INVALID, what + ": density must be positive and finite");
+        if (md.boundary_kind == RRT_BOUNDARY_QUADS) {
+            if (md.count == 0 || (uint64_t)md.first + md.count > ex.n_bquads)
+                return fail(RRT_E_INVALID, what + ": boundary quad range out of bounds");
+        } else if (md.boundary_kind != RRT_BOUNDARY_SPHERE) {
+            return fail(RRT_E_INVALID, what + ": unknown boundary_kind");
+        }
     }
     bool has_motion = false;
     if (motion)
@@ -707,9 +761,10 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
         return fail(RRT_E_INVALID, "moving spheres need RRT_FLAG_RAY_TIME (rays carry the camera's time draw)");
     // Book-2 scenes (moving spheres or checker / noise materials) take the kernel variant that
     // supports them; it reads a motion row per sphere (zero for static spheres).
-    bool book2 = has_motion || n_quads > 0;
+    bool book2 = has_motion || n_quads > 0 || n_media > 0;
     for (uint32_t i = 0; i < n_materials && materials; ++i)
-        book2 = book2 || materials[i].kind == RRT_MAT_CHECKER_LAMBERTIAN || materials[i].kind == RRT_MAT_NOISE_LAMBERTIAN;
+        book2 = book2 || materials[i].kind == RRT_MAT_CHECKER_LAMBERTIAN || materials[i].kind == RRT_MAT_NOISE_LAMBERTIAN ||
+                materials[i].kind == RRT_MAT_ISOTROPIC;
     if (!has_motion) motion = nullptr;
     if (n_spheres && !spheres) return fail(RRT_E_INVALID, "null spheres");
     if (n_materials && !materials) return fail(RRT_E_INVALID, "null materials");
@@ -722,7 +777,7 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
         if (spheres[i].material_index >= n_materials)
             return fail(RRT_E_INVALID, "sphere " + std::to_string(i) + " material_index out of range");
     for (uint32_t i = 0; i < n_materials; ++i) {
-        if (materials[i].kind > RRT_MAT_NOISE_LAMBERTIAN)
+        if (materials[i].kind > RRT_MAT_ISOTROPIC)
             return fail(RRT_E_INVALID, "material " + std::to_string(i) + " has unknown kind");
         if (materials[i].kind == RRT_MAT_TEXTURED_LAMBERTIAN && materials[i]._pad[0] >= n_textures)
             return fail(RRT_E_INVALID, "material " + std::to_string(i) + " texture index out of range");
@@ -738,13 +793,15 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
     bvh_defaults(width, max_leaf);
     if (book2) width = 2;  // the book-2 kernel variants are BVH2 only
     std::vector<uint32_t> order;
-    const FlatBvh fb = build_bvh(spheres, n_spheres, motion, quads, n_quads, width, max_leaf, order);
+    if ((uint64_t)n_spheres + n_quads + n_media >= (1u << 24) || (uint64_t)n_quads + ex.n_bquads >= (1u << 24))
+        return fail(RRT_E_INVALID, ">= 2^24 primitives or quads");
+    if (!has_motion) ex.motion = nullptr;
+    const FlatBvh fb = build_bvh(spheres, n_spheres, ex, width, max_leaf, order);
     if (fb.stack_need > (uint32_t)rrt::kMaxStackDepth)
         return fail(RRT_E_INVALID, "BVH depth " + std::to_string(fb.max_depth) + " exceeds the LDS stack");
     // postponed leaf tests pack (first primitive, count) as first | count << 28
-    if (fb.max_leaf > 15 || (uint64_t)n_spheres + n_quads >= (1u << 24))
-        return fail(RRT_E_INVALID, "leaf size > 15 or >= 2^24 primitives");
-    const uint32_t n_prims = n_spheres + n_quads;
+    if (fb.max_leaf > 15) return fail(RRT_E_INVALID, "leaf size > 15");
+    const uint32_t n_prims = n_spheres + n_quads + n_media;
 
     std::vector<rrt::GMaterial> mats(n_materials);
     for (uint32_t i = 0; i < n_materials; ++i) {
@@ -760,9 +817,9 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
     // 32-B record at the primitive's index (no dependent material-index fetch).
     // Quads with their derived plane (quad.rs:21-37 in f64: n = cross(u, v), normal = n * (1/|n|),
     // D = dot(normal, q), w = n * (1/dot(n, n)); Vec3 / f64 is `(1/rhs) * v`, vec3.rs:142-148).
-    std::vector<rrt::GQuad> gquads(n_quads);
-    for (uint32_t j = 0; j < n_quads; ++j) {
-        const RrtQuad &qd = quads[j];
+    std::vector<rrt::GQuad> gquads(n_quads + (size_t)ex.n_bquads);
+    for (uint32_t j = 0; j < gquads.size(); ++j) {
+        const RrtQuad &qd = j < n_quads ? quads[j] : ex.bquads[j - n_quads];
         const D3 q = d3(qd.q[0], qd.q[1], qd.q[2]), u = d3(qd.u[0], qd.u[1], qd.u[2]), v = d3(qd.v[0], qd.v[1], qd.v[2]);
         const D3 n = cross(u, v);
         const double nn = n.x * n.x + n.y * n.y + n.z * n.z;
@@ -782,10 +839,10 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
     std::vector<rrt::GMaterial> prim_mtl(n_prims);
     std::vector<float4> prim_motion(book2 ? n_prims : 0, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
     for (uint32_t i = 0; i < n_prims; ++i) {
-        if (order[i] >= n_spheres) {  // quad j: tagged by a negative w (spheres have r >= 0)
+        if (order[i] >= n_spheres) {  // quad j / medium j - n_quads: tagged by a negative w (spheres have r >= 0)
             const uint32_t j = order[i] - n_spheres;
             prim_cr[i] = make_float4(0.0f, 0.0f, 0.0f, -(float)(j + 1));
-            prim_mtl[i] = mats[quads[j].material_index];
+            prim_mtl[i] = mats[j < n_quads ? quads[j].material_index : ex.media[j - n_quads].material_index];
             continue;
         }
         const RrtSphere &sp = spheres[order[i]];
@@ -796,6 +853,17 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
             const float *m = motion + 4 * (size_t)order[i];
             prim_motion[i] = make_float4(m[0], m[1], m[2], 0.0f);
         }
+    }
+    // Media: boundary quads follow the scene's quads in the GQuad array.
+    std::vector<rrt::GMedium> gmedia(n_media);
+    for (uint32_t m = 0; m < n_media; ++m) {
+        const RrtMedium &md = ex.media[m];
+        rrt::GMedium &g = gmedia[m];
+        g.sphere = make_float4(md.sphere[0], md.sphere[1], md.sphere[2], std::max(md.sphere[3], 0.0f));
+        g.kind = md.boundary_kind;
+        g.first = n_quads + md.first;
+        g.count = md.count;
+        g.neg_inv_density = (float)(-1.0 / (double)md.density);  // constant_medium.rs:24
     }
     std::vector<rrt::GPerlin> perlin(n_perlin);
     for (uint32_t t = 0; t < n_perlin; ++t) {
@@ -832,7 +900,8 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
         if ((rc = upload(&s->d_prim_mtl, prim_mtl.data(), prim_mtl.size(), "sphere materials"))) break;
         if (book2 && (rc = upload(&s->d_prim_motion, prim_motion.data(), prim_motion.size(), "sphere motion"))) break;
         if (n_perlin && (rc = upload(&s->d_perlin, perlin.data(), perlin.size(), "Perlin tables"))) break;
-        if (n_quads && (rc = upload(&s->d_quads, gquads.data(), gquads.size(), "quads"))) break;
+        if (!gquads.empty() && (rc = upload(&s->d_quads, gquads.data(), gquads.size(), "quads"))) break;
+        if (n_media && (rc = upload(&s->d_media, gmedia.data(), gmedia.size(), "media"))) break;
         if ((rc = upload(&s->d_tex_pool, tex_pool.data(), tex_pool.size(), "textures"))) break;
         if ((rc = upload(&s->d_texs, texs.data(), texs.size(), "texture table"))) break;
         if (hipMalloc((void **)&s->d_counters, 8 * sizeof(unsigned long long)) != hipSuccess ||
@@ -861,6 +930,8 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
     p.n_perlin = n_perlin;
     p.quads = s->d_quads;
     p.n_quads = n_quads;
+    p.media = s->d_media;
+    p.n_media = n_media;
     p.tex_pool = s->d_tex_pool;
     p.texs = s->d_texs;
     p.counters = s->d_counters;
@@ -913,7 +984,7 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
     bi.width = fb.width;
     bi.max_leaf_param = max_leaf;
     bi.prim_bytes = (uint64_t)n_prims * (rrt::kPrimBytes + (book2 ? rrt::kMotionBytes : 0)) +
-                    (uint64_t)n_quads * sizeof(rrt::GQuad);
+                    (uint64_t)gquads.size() * sizeof(rrt::GQuad) + (uint64_t)n_media * sizeof(rrt::GMedium);
     *out = s;
     return RRT_OK;
 }
@@ -944,21 +1015,18 @@ int32_t rrt_build_bvh_ex(const RrtSphere *spheres, uint32_t n_spheres, const Rrt
                          uint32_t max_leaf, void *nodes_out, size_t nodes_cap, uint32_t *prim_order_out,
                          RrtBvhInfo *info) {
     if (n_spheres && !spheres) return fail(RRT_E_INVALID, "null spheres");
-    const float *motion = ext ? ext->sphere_motion : nullptr;
-    const RrtQuad *quads = ext && ext->quads ? ext->quads : nullptr;
-    const uint32_t n_quads = quads ? ext->n_quads : 0u;
-    if (motion) {  // same rule as scene creation: an all-zero motion array is a static scene
-        bool any = false;
-        for (size_t i = 0; i < (size_t)n_spheres * 4 && !any; ++i) any = (i % 4 != 3) && motion[i] != 0.0f;
-        if (!any) motion = nullptr;
-    }
+    const ExtView ex(ext);
+    for (uint32_t m = 0; m < ex.n_media; ++m)
+        if (ex.media[m].boundary_kind == RRT_BOUNDARY_QUADS &&
+            (ex.media[m].count == 0 || (uint64_t)ex.media[m].first + ex.media[m].count > ex.n_bquads))
+            return fail(RRT_E_INVALID, "medium " + std::to_string(m) + ": boundary quad range out of bounds");
     uint32_t dw, dl;
     bvh_defaults(dw, dl);
     if (width == 0) width = dw;
     if (max_leaf == 0) max_leaf = dl;
     if ((width != 2 && width != 4) || max_leaf > 15) return fail(RRT_E_INVALID, "width must be 2 or 4, max_leaf <= 15");
     std::vector<uint32_t> order;
-    const FlatBvh fb = build_bvh(spheres, n_spheres, motion, quads, n_quads, width, max_leaf, order);
+    const FlatBvh fb = build_bvh(spheres, n_spheres, ex, width, max_leaf, order);
     if (info) {
         *info = RrtBvhInfo{};
         info->n_nodes = fb.n_nodes;
@@ -966,7 +1034,10 @@ int32_t rrt_build_bvh_ex(const RrtSphere *spheres, uint32_t n_spheres, const Rrt
         info->max_depth = fb.max_depth;
         info->max_leaf_size = fb.max_leaf;
         info->node_bytes = fb.bytes.size();
-        info->prim_bytes = (uint64_t)n_spheres * (rrt::kPrimBytes + (motion ? rrt::kMotionBytes : 0));
+        const bool book2 = ex.motion || ex.n_quads || ex.n_media;
+        info->prim_bytes = (uint64_t)order.size() * (rrt::kPrimBytes + (book2 ? rrt::kMotionBytes : 0)) +
+                           ((uint64_t)ex.n_quads + ex.n_bquads) * sizeof(rrt::GQuad) +
+                           (uint64_t)ex.n_media * sizeof(rrt::GMedium);
         info->width = fb.width;
         info->max_leaf_param = max_leaf;
     }
@@ -1348,15 +1419,12 @@ int32_t rrt_build_in_one_weekend_scene(const RrtOverrides *ov, uint64_t seed, in
 // draws, in the same order, come from SmallRng(seed): random_double() = gen_range(0.0..1.0),
 // random_double_range = gen_range(min..max), random_int(min,max) = random_double_range(min,
 // max+1) as i32 (rtweekend.rs:17-30). Parity unpinned (entropy RNG).
-int32_t rrt_build_next_week_scene(int32_t scene, const RrtOverrides *ov, uint64_t seed, RrtCamera *cam,
-                                  RrtSphere *spheres, float *motion, uint32_t sphere_cap, uint32_t *n_spheres,
-                                  RrtMaterial *materials, uint32_t material_cap, uint32_t *n_materials,
-                                  RrtQuad *quads, uint32_t quad_cap, uint32_t *n_quads,
-                                  RrtPerlin *perlin, uint32_t perlin_cap, uint32_t *n_perlin) {
-    if (!n_spheres || !n_materials || !n_quads || !n_perlin) return fail(RRT_E_INVALID, "null count output");
-    if (scene < 1 || scene > 7)
+int32_t rrt_build_next_week_scene(int32_t scene, const RrtOverrides *ov, uint64_t seed, RrtNextWeekScene *out) {
+    if (!out) return fail(RRT_E_INVALID, "null output");
+    if (scene < 1 || scene > 10)
         return fail(RRT_E_INVALID, "book-2 scene must be 1 bouncing_spheres, 2 checkered_spheres, 3 earth, "
-                                   "4 perlin_spheres, 5 quads, 6 simple_light, 7 cornell_box");
+                                   "4 perlin_spheres, 5 quads, 6 simple_light, 7 cornell_box, 8 cornell_smoke, "
+                                   "9 final_scene(800, 10000, 40), 10 final_scene(400, 250, 4)");
     // Camera (the_next_week/mod.rs:137-150, 177-190, 203-216, 237-250)
     double aspect_ratio = 16.0 / 9.0;
     int32_t image_width = 400, samples_per_pixel = 100, max_depth = 50;
@@ -1375,9 +1443,17 @@ int32_t rrt_build_next_week_scene(int32_t scene, const RrtOverrides *ov, uint64_
         lookfrom[0] = 26.0, lookfrom[1] = 3.0, lookfrom[2] = 6.0;
         lookat[1] = 2.0;
         background[0] = background[1] = background[2] = 0.0;
-    } else if (scene == 7) {  // mod.rs:412-423
+    } else if (scene == 7 || scene == 8) {  // mod.rs:412-423, 490-501
         aspect_ratio = 1.0, image_width = 600, samples_per_pixel = 200, vfov = 40.0;
         lookfrom[0] = 278.0, lookfrom[1] = 278.0, lookfrom[2] = -800.0;
+        lookat[0] = 278.0, lookat[1] = 278.0, lookat[2] = 0.0;
+        background[0] = background[1] = background[2] = 0.0;
+    } else if (scene >= 9) {  // final_scene (mod.rs:570-585), main.rs:78-79 arguments
+        aspect_ratio = 1.0, vfov = 40.0;
+        image_width = scene == 9 ? 800 : 400;
+        samples_per_pixel = scene == 9 ? 10000 : 250;
+        max_depth = scene == 9 ? 40 : 4;
+        lookfrom[0] = 478.0, lookfrom[1] = 278.0, lookfrom[2] = -600.0;
         lookat[0] = 278.0, lookat[1] = 278.0, lookat[2] = 0.0;
         background[0] = background[1] = background[2] = 0.0;
     }
@@ -1391,7 +1467,9 @@ int32_t rrt_build_next_week_scene(int32_t scene, const RrtOverrides *ov, uint64_
     std::vector<RrtMaterial> mat;
     std::vector<float> mot;
     std::vector<RrtPerlin> tables;
-    std::vector<RrtQuad> qds;
+    std::vector<RrtQuad> qds, bqs;
+    std::vector<RrtMedium> meds;
+    uint32_t uses_texture0 = 0;
     auto bits = [](float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; };
     auto add_material = [&](uint32_t kind, float r, float g, float b, float w, float ref_idx, uint32_t p0, uint32_t p1) {
         RrtMaterial m{};
@@ -1424,27 +1502,47 @@ int32_t rrt_build_next_week_scene(int32_t scene, const RrtOverrides *ov, uint64_
         D3 off = d3(0.0, 0.0, 0.0);
     };
     auto rot = [](const Xform &x, D3 a) { return d3(x.c * a.x + x.s * a.z, a.y, -x.s * a.x + x.c * a.z); };
-    auto add_quad = [&](D3 q, D3 u, D3 v, uint32_t m, const Xform &x) {
+    auto add_quad_to = [&](std::vector<RrtQuad> &dst, D3 q, D3 u, D3 v, uint32_t m, const Xform &x) {
         const D3 wq = rot(x, q) + x.off, wu = rot(x, u), wv = rot(x, v);
         RrtQuad r{};
         put4(r.q, (float)wq.x, (float)wq.y, (float)wq.z, 0.0f);
         put4(r.u, (float)wu.x, (float)wu.y, (float)wu.z, 0.0f);
         put4(r.v, (float)wv.x, (float)wv.y, (float)wv.z, 0.0f);
         r.material_index = m;
-        qds.push_back(r);
+        dst.push_back(r);
     };
+    auto add_quad = [&](D3 q, D3 u, D3 v, uint32_t m, const Xform &x) { add_quad_to(qds, q, u, v, m, x); };
     const Xform ident;
-    auto make_box = [&](D3 a, D3 b, uint32_t m, const Xform &x) {  // quad.rs:95-119
+    // make_box (quad.rs:95-119): six faces into `dst` (the scene's quads, or a medium boundary)
+    auto make_box_to = [&](std::vector<RrtQuad> &dst, D3 a, D3 b, uint32_t m, const Xform &x) {
         const D3 lo = d3(std::min(a.x, b.x), std::min(a.y, b.y), std::min(a.z, b.z));
         const D3 hi = d3(std::max(a.x, b.x), std::max(a.y, b.y), std::max(a.z, b.z));
         const D3 dx = d3(hi.x - lo.x, 0.0, 0.0), dy = d3(0.0, hi.y - lo.y, 0.0), dz = d3(0.0, 0.0, hi.z - lo.z);
         const D3 ndx = d3(-dx.x, 0.0, 0.0), ndz = d3(0.0, 0.0, -dz.z);
-        add_quad(d3(lo.x, lo.y, hi.z), dx, dy, m, x);
-        add_quad(d3(hi.x, lo.y, hi.z), ndz, dy, m, x);
-        add_quad(d3(hi.x, lo.y, lo.z), ndx, dy, m, x);
-        add_quad(d3(lo.x, lo.y, lo.z), dz, dy, m, x);
-        add_quad(d3(lo.x, hi.y, hi.z), dx, ndz, m, x);
-        add_quad(d3(lo.x, lo.y, lo.z), dx, dz, m, x);
+        add_quad_to(dst, d3(lo.x, lo.y, hi.z), dx, dy, m, x);
+        add_quad_to(dst, d3(hi.x, lo.y, hi.z), ndz, dy, m, x);
+        add_quad_to(dst, d3(hi.x, lo.y, lo.z), ndx, dy, m, x);
+        add_quad_to(dst, d3(lo.x, lo.y, lo.z), dz, dy, m, x);
+        add_quad_to(dst, d3(lo.x, hi.y, hi.z), dx, ndz, m, x);
+        add_quad_to(dst, d3(lo.x, lo.y, lo.z), dx, dz, m, x);
+    };
+    auto make_box = [&](D3 a, D3 b, uint32_t m, const Xform &x) { make_box_to(qds, a, b, m, x); };
+    // ConstantMedium::from_color (constant_medium.rs:30-36): Isotropic(albedo) phase function
+    auto medium = [&](uint32_t kind, D3 c, double r, uint32_t first, uint32_t count, double density, D3 albedo) {
+        RrtMedium md{};
+        put4(md.sphere, (float)c.x, (float)c.y, (float)c.z, (float)r);
+        md.boundary_kind = kind;
+        md.first = first;
+        md.count = count;
+        md.material_index = add_material(RRT_MAT_ISOTROPIC, (float)albedo.x, (float)albedo.y, (float)albedo.z, 0.0f,
+                                         1.0f, 0, 0);
+        md.density = (float)density;
+        meds.push_back(md);
+    };
+    auto box_medium = [&](D3 a, D3 b, const Xform &x, double density, D3 albedo) {
+        const uint32_t first = (uint32_t)bqs.size();
+        make_box_to(bqs, a, b, 0, x);
+        medium(RRT_BOUNDARY_QUADS, d3(0, 0, 0), 0.0, first, 6, density, albedo);
     };
     auto rotate_translate = [](double deg, D3 off) {  // RotateY::new (hittable.rs:100-103)
         Xform x;
@@ -1515,6 +1613,7 @@ int32_t rrt_build_next_week_scene(int32_t scene, const RrtOverrides *ov, uint64_
         add_sphere(d3(0.0, 10.0, 0.0), 10.0, checker(), still);
     } else if (scene == 3) {  // earth (mod.rs:196-201): the image is texture 0
         add_sphere(d3(0.0, 0.0, 0.0), 2.0, add_material(RRT_MAT_TEXTURED_LAMBERTIAN, 0, 0, 0, 0, 1.0f, 0, 0), still);
+        uses_texture0 = 1;
     } else if (scene == 4 || scene == 6) {
         // perlin_spheres (mod.rs:222-235) / simple_light (mod.rs:318-340): one NoiseTexture(4)
         // shared by the ground and the sphere
@@ -1533,7 +1632,7 @@ int32_t rrt_build_next_week_scene(int32_t scene, const RrtOverrides *ov, uint64_
         add_quad(d3(3, -2, 1), d3(0, 0, 4), d3(0, 4, 0), lambertian(0.2f, 0.2f, 1.0f), ident);
         add_quad(d3(-2, 3, 1), d3(4, 0, 0), d3(0, 0, 4), lambertian(1.0f, 0.5f, 0.0f), ident);
         add_quad(d3(-2, -3, 5), d3(4, 0, 0), d3(0, 0, -4), lambertian(0.2f, 0.8f, 0.8f), ident);
-    } else {  // cornell_box (mod.rs:359-410)
+    } else if (scene == 7) {  // cornell_box (mod.rs:359-410)
         const uint32_t red = lambertian(0.65f, 0.05f, 0.05f), white = lambertian(0.73f, 0.73f, 0.73f);
         const uint32_t green = lambertian(0.12f, 0.45f, 0.15f), light = diffuse_light(15.0f);
         add_quad(d3(555, 0, 0), d3(0, 555, 0), d3(0, 0, 555), green, ident);
@@ -1544,35 +1643,76 @@ int32_t rrt_build_next_week_scene(int32_t scene, const RrtOverrides *ov, uint64_
         add_quad(d3(0, 0, 555), d3(555, 0, 0), d3(0, 555, 0), white, ident);
         make_box(d3(0, 0, 0), d3(165, 330, 165), white, rotate_translate(15.0, d3(265, 0, 295)));
         make_box(d3(0, 0, 0), d3(165, 165, 165), white, rotate_translate(-18.0, d3(130, 0, 65)));
+    } else if (scene == 8) {  // cornell_smoke (mod.rs:432-488): the two boxes become media
+        const uint32_t red = lambertian(0.65f, 0.05f, 0.05f), white = lambertian(0.73f, 0.73f, 0.73f);
+        const uint32_t green = lambertian(0.12f, 0.45f, 0.15f), light = diffuse_light(7.0f);
+        add_quad(d3(555, 0, 0), d3(0, 555, 0), d3(0, 0, 555), green, ident);
+        add_quad(d3(0, 0, 0), d3(0, 555, 0), d3(0, 0, 555), red, ident);
+        add_quad(d3(113, 554, 127), d3(330, 0, 0), d3(0, 0, 305), light, ident);
+        add_quad(d3(0, 555, 0), d3(555, 0, 0), d3(0, 0, 555), white, ident);
+        add_quad(d3(0, 0, 0), d3(555, 0, 0), d3(0, 0, 555), white, ident);
+        add_quad(d3(0, 0, 555), d3(555, 0, 0), d3(0, 555, 0), white, ident);
+        box_medium(d3(0, 0, 0), d3(165, 330, 165), rotate_translate(15.0, d3(265, 0, 295)), 0.01, d3(0, 0, 0));
+        box_medium(d3(0, 0, 0), d3(165, 165, 165), rotate_translate(-18.0, d3(130, 0, 65)), 0.01, d3(1, 1, 1));
+    } else {  // final_scene (mod.rs:503-587)
+        const uint32_t ground = lambertian(0.48f, 0.83f, 0.53f);
+        for (int i = 0; i < 20; ++i)
+            for (int j = 0; j < 20; ++j) {
+                const double w = 100.0;
+                const double x0 = -1000.0 + i * w, z0 = -1000.0 + j * w, y0 = 0.0;
+                const double x1 = x0 + w, y1 = random_double() * 100.0 + 1.0, z1 = z0 + w;
+                make_box(d3(x0, y0, z0), d3(x1, y1, z1), ground, ident);
+            }
+        add_quad(d3(123, 554, 147), d3(300, 0, 0), d3(0, 0, 265), diffuse_light(7.0f), ident);
+        const D3 center1 = d3(400, 400, 200);
+        add_sphere(center1, 50.0, lambertian(0.7f, 0.3f, 0.1f), d3(30, 0, 0));  // new_moving: center2 - center1
+        add_sphere(d3(260, 150, 45), 50.0, add_material(RRT_MAT_DIELECTRIC, 1, 1, 1, 0, 1.5f, 0, 0), still);
+        add_sphere(d3(0, 150, 145), 50.0, add_material(RRT_MAT_METAL, 0.8f, 0.8f, 0.9f, 1.0f, 1.0f, 0, 0), still);
+        // boundary sphere: a dielectric surface and the boundary of a medium
+        add_sphere(d3(360, 150, 145), 70.0, add_material(RRT_MAT_DIELECTRIC, 1, 1, 1, 0, 1.5f, 0, 0), still);
+        medium(RRT_BOUNDARY_SPHERE, d3(360, 150, 145), 70.0, 0, 0, 0.2, d3(0.2, 0.4, 0.9));
+        medium(RRT_BOUNDARY_SPHERE, d3(0, 0, 0), 5000.0, 0, 0, 0.0001, d3(1, 1, 1));  // boundary only
+        add_sphere(d3(400, 200, 400), 100.0, add_material(RRT_MAT_TEXTURED_LAMBERTIAN, 0, 0, 0, 0, 1.0f, 0, 0), still);
+        uses_texture0 = 1;
+        const uint32_t t = perlin_table();  // NoiseTexture::new(0.2)
+        add_sphere(d3(220, 280, 300), 80.0, add_material(RRT_MAT_NOISE_LAMBERTIAN, 0.5f, 0.5f, 0.5f, 0.2f, 1.0f, t, 0),
+                   still);
+        const uint32_t white = lambertian(0.73f, 0.73f, 0.73f);
+        const Xform xf = rotate_translate(15.0, d3(-100, 270, 395));
+        for (int k = 0; k < 1000; ++k) {  // Vec3::random_range(0, 165): x, y, z draws
+            double c[3];
+            for (double &v : c) v = random_range(0.0, 165.0);
+            add_sphere(rot(xf, d3(c[0], c[1], c[2])) + xf.off, 10.0, white, still);
+        }
     }
     const uint32_t sample_seed = rng.next_u32();
-    *n_spheres = (uint32_t)sph.size();
-    *n_materials = (uint32_t)mat.size();
-    *n_quads = (uint32_t)qds.size();
-    *n_perlin = (uint32_t)tables.size();
-    if (cam) {
-        int rc = rrt_make_camera(aspect_ratio, image_width, samples_per_pixel, max_depth, vfov, lookfrom, lookat, vup,
-                                 defocus_angle, focus_dist, has_bg ? background : nullptr, sample_seed,
-                                 (uint32_t)sph.size(), cam);
-        if (rc) return rc;
-    }
-    if (perlin_cap) {
-        if (perlin_cap < tables.size() || !perlin) return fail(RRT_E_INVALID, "perlin_cap too small");
-        if (!tables.empty()) std::memcpy(perlin, tables.data(), tables.size() * sizeof(RrtPerlin));
-    }
-    if (quad_cap) {
-        if (quad_cap < qds.size() || !quads) return fail(RRT_E_INVALID, "quad_cap too small");
-        if (!qds.empty()) std::memcpy(quads, qds.data(), qds.size() * sizeof(RrtQuad));
-    }
-    if (material_cap) {
-        if (material_cap < mat.size() || !materials) return fail(RRT_E_INVALID, "material_cap too small");
-        std::memcpy(materials, mat.data(), mat.size() * sizeof(RrtMaterial));
-    }
-    if (sphere_cap == 0) return RRT_OK;
-    if (sphere_cap < sph.size() || !spheres)
-        return fail(RRT_E_INVALID, "sphere_cap too small (need " + std::to_string(sph.size()) + ")");
-    if (!sph.empty()) std::memcpy(spheres, sph.data(), sph.size() * sizeof(RrtSphere));
-    if (motion && !mot.empty()) std::memcpy(motion, mot.data(), mot.size() * sizeof(float));
+    RrtNextWeekScene &o = *out;
+    o.n_spheres = (uint32_t)sph.size();
+    o.n_materials = (uint32_t)mat.size();
+    o.n_quads = (uint32_t)qds.size();
+    o.n_perlin = (uint32_t)tables.size();
+    o.n_media = (uint32_t)meds.size();
+    o.n_boundary_quads = (uint32_t)bqs.size();
+    o.uses_texture0 = uses_texture0;
+    int rc = rrt_make_camera(aspect_ratio, image_width, samples_per_pixel, max_depth, vfov, lookfrom, lookat, vup,
+                             defocus_angle, focus_dist, has_bg ? background : nullptr, sample_seed,
+                             (uint32_t)sph.size(), &o.camera);
+    if (rc) return rc;
+    // copy out each array whose cap is set (cap 0 = sizing only)
+    auto put = [&](auto *dst, uint32_t cap, const auto &src, const char *what) -> int32_t {
+        if (cap == 0) return RRT_OK;
+        if (cap < src.size() || !dst)
+            return fail(RRT_E_INVALID, std::string(what) + "_cap too small (need " + std::to_string(src.size()) + ")");
+        if (!src.empty()) std::memcpy(dst, src.data(), src.size() * sizeof(src[0]));
+        return RRT_OK;
+    };
+    if ((rc = put(o.spheres, o.sphere_cap, sph, "sphere")) || (rc = put(o.materials, o.material_cap, mat, "material")) ||
+        (rc = put(o.quads, o.quad_cap, qds, "quad")) || (rc = put(o.perlin, o.perlin_cap, tables, "perlin")) ||
+        (rc = put(o.media, o.media_cap, meds, "media")) ||
+        (rc = put(o.boundary_quads, o.boundary_quad_cap, bqs, "boundary_quad")))
+        return rc;
+    if (o.sphere_motion && o.sphere_cap >= sph.size() && !mot.empty())
+        std::memcpy(o.sphere_motion, mot.data(), mot.size() * sizeof(float));
     return RRT_OK;
 }
 

@@ -58,6 +58,17 @@ struct alignas(16) GQuad {
     float4 w;
 };
 
+// ConstantMedium (the_next_week/constant_medium.rs): boundary sphere (xyz, r) or quads
+// [first, first + count) of KParams.quads (after the scene's own quads); neg_inv_density =
+// -1/density (f64 on the host, rounded to f32). 32 B.
+struct alignas(16) GMedium {
+    float4 sphere;
+    uint32_t kind;  // 0 sphere, 1 quads
+    uint32_t first;
+    uint32_t count;
+    float neg_inv_density;
+};
+
 struct GTexture {
     int32_t offset;  // byte offset into the texture pool
     int32_t width;
@@ -72,7 +83,9 @@ struct KParams {
     const GMaterial *prim_mtl;   // each primitive's material record, same order (one fetch per hit)
     const float4 *prim_motion;   // (center2 - center1).xyz per primitive, same order; null = static scene
     const GPerlin *perlin;       // Perlin tables (noise textures)
-    const GQuad *quads;          // quads; a quad's leaf-order primitive record is (0, 0, 0, -(1 + index))
+    const GQuad *quads;          // quads, then media boundary quads; a quad's leaf-order primitive record is
+                                 // (0, 0, 0, -(1 + index)), a medium's (0, 0, 0, -(1 + n_quads + index))
+    const GMedium *media;
     const uint8_t *tex_pool;
     const GTexture *texs;
     float4 *accum;               // tile-local rows * width
@@ -107,7 +120,8 @@ struct KParams {
     uint32_t n_nodes;
     uint32_t n_prims;
     uint32_t n_perlin;
-    uint32_t n_quads;
+    uint32_t n_quads;       // the scene's quads (boundary quads follow them)
+    uint32_t n_media;
     uint32_t stack_depth;   // entries needed (BVH depth + 1)
     uint32_t scene_in_lds;  // stage nodes + spheres + their materials in LDS per block
     uint32_t trav_frac;     // leave the traversal loop when <= live*trav_frac/256 lanes still traverse

@@ -234,14 +234,19 @@ __device__ __forceinline__ float div_by_a(float n, const RayK &rk) {
 // Sphere centers as the sphere test sees them: static, or (book-2 scenes) a moving sphere's
 // center at the ray's time, center1 + time * (center2 - center1) (the_next_week/sphere.rs:44:
 // Ray::at; static book-2 spheres carry a zero motion).
-// kBook2: 0 = book-1 scenes, 1 = book 2 (motion, procedural textures), 2 = book 2 with quads
+// kBook2: 0 = book-1 scenes, 1 = book 2 (motion, procedural textures), 2 = book 2 with quads,
+// 3 = book 2 with quads and media
 template <int kBook2>
 struct Prims {
     const float4 *cr;
     const float4 *mo;
     float time;
     const GQuad *qd;  // book-2 scenes: quads, tagged in cr by a negative w (-(1 + index))
-    static constexpr bool kHasQuads = kBook2 == 2;
+    const GMedium *md;  // media, tagged -(1 + n_quads + index)
+    uint32_t n_quads;
+    uint64_t seg;  // the path's RNG state at this segment ^ (bounce << 32): key of the media draws
+    static constexpr bool kHasQuads = kBook2 >= 2;
+    static constexpr bool kHasMedia = kBook2 == 3;
     __device__ __forceinline__ float4 at(int i) const {
         float4 c = cr[i];
         if constexpr (kBook2) {
@@ -257,12 +262,12 @@ struct Prims {
 // Quad::hit (the_next_week/quad.rs:61-87) in f32: plane distance, then the hit point's (alpha,
 // beta) in the (u, v) frame. The t acceptance is Interval::contains (closed: a quad at exactly
 // the running closest t replaces the earlier hit), unlike the sphere's open `surrounds`.
-__device__ __forceinline__ bool quad_hit(const GQuad &g, V3 o, V3 d, float closest, float &t_out) {
+__device__ __forceinline__ bool quad_hit(const GQuad &g, V3 o, V3 d, float tmin, float closest, float &t_out) {
     const V3 n = v3(g.n.x, g.n.y, g.n.z);
     const float denom = dot(n, d);
     if (__builtin_fabsf(denom) < 1e-8f) return false;
     const float t = (g.q.w - dot(n, o)) / denom;
-    if (!(0.001f <= t && t <= closest)) return false;
+    if (!(tmin <= t && t <= closest)) return false;
     const V3 p = v3(o.x + t * d.x, o.y + t * d.y, o.z + t * d.z);  // Ray::at
     const V3 hp = v3(p.x - g.q.x, p.y - g.q.y, p.z - g.q.z);
     const V3 w = v3(g.w.x, g.w.y, g.w.z);
@@ -270,6 +275,87 @@ __device__ __forceinline__ bool quad_hit(const GQuad &g, V3 o, V3 d, float close
     const float beta = dot(w, cross(v3(g.u.x, g.u.y, g.u.z), hp));
     if (!(0.0f <= alpha && alpha <= 1.0f && 0.0f <= beta && beta <= 1.0f)) return false;  // is_interior
     t_out = t;
+    return true;
+}
+
+// ln(x) in f32 with only + - * and exponent extraction, bit-reproducible by the oracle: Cephes
+// logf (x = m * 2^e, m in [sqrt(1/2), sqrt(2)), minimax polynomial in m - 1, ln 2 in two
+// parts). x = 0 gives -inf; only called with the media draws, u in [0, 1) on a 2^-24 grid.
+__device__ __forceinline__ float rrt_logf(float x) {
+    if (x == 0.0f) return -__builtin_inff();
+    const uint32_t b = __float_as_uint(x);
+    int e = (int)((b >> 23) & 255u) - 126;
+    float m = __uint_as_float((b & 0x807fffffu) | 0x3f000000u);  // frexpf: m in [0.5, 1)
+    if (m < 0.707106781186547524f) {
+        e -= 1;
+        m = m + m - 1.0f;
+    } else {
+        m = m - 1.0f;
+    }
+    const float z = m * m;
+    float y = ((((((((7.0376836292e-2f * m - 1.1514610310e-1f) * m + 1.1676998740e-1f) * m - 1.2420140846e-1f) * m +
+                   1.4249322787e-1f) * m - 1.6668057665e-1f) * m + 2.0000714765e-1f) * m - 2.4999993993e-1f) * m +
+               3.3333331174e-1f) * m * z;
+    const float fe = (float)e;
+    y = y + -2.12194440e-4f * fe;
+    y = y + -0.5f * z;
+    float r = m + y;
+    r = r + 0.693359375f * fe;
+    return r;
+}
+
+// ConstantMedium::hit (constant_medium.rs:40-84) in f32: the boundary's first hit over
+// (-inf, inf) and its next hit after t1 + 0.0001 (Sphere::hit / HittableList over the boundary
+// quads), clipped to [0.001, closest]; a free flight of -ln(u)/density along the ray (u: the
+// per-(path, segment, medium) draw, include/rrt_hip.h). Returns the scatter t or false.
+template <class PR>
+__device__ __forceinline__ bool medium_hit(const PR &pr, int m, V3 o, V3 d, const RayK &rk, float closest, float &t_out) {
+    const GMedium g = pr.md[m];
+    const float inf = __builtin_inff();
+    float t1, t2;
+    if (g.kind == 0u) {
+        const V3 oc = v3(g.sphere.x - o.x, g.sphere.y - o.y, g.sphere.z - o.z);
+        const float h = dot(d, oc);
+        const float c = dot(oc, oc) - g.sphere.w * g.sphere.w;
+        const float disc = h * h - rk.a * c;
+        if (disc < 0.0f) return false;
+        const float sq = __builtin_sqrtf(disc);
+        const float r0 = div_by_a(h - sq, rk), r1 = div_by_a(h + sq, rk);
+        // Sphere::hit over (-inf, inf), then over (t1 + 0.0001, inf)
+        if (-inf < r0 && r0 < inf) t1 = r0;
+        else if (-inf < r1 && r1 < inf) t1 = r1;
+        else return false;
+        const float lo = t1 + 0.0001f;
+        if (lo < r0 && r0 < inf) t2 = r0;
+        else if (lo < r1 && r1 < inf) t2 = r1;
+        else return false;
+    } else {
+        t1 = inf;
+        bool h1 = false;
+        for (uint32_t k = 0; k < g.count; ++k) {
+            float t;
+            if (quad_hit(pr.qd[g.first + k], o, d, -inf, t1, t)) t1 = t, h1 = true;
+        }
+        if (!h1) return false;
+        const float lo = t1 + 0.0001f;
+        t2 = inf;
+        bool h2 = false;
+        for (uint32_t k = 0; k < g.count; ++k) {
+            float t;
+            if (quad_hit(pr.qd[g.first + k], o, d, lo, t2, t)) t2 = t, h2 = true;
+        }
+        if (!h2) return false;
+    }
+    if (t1 < 0.001f) t1 = 0.001f;
+    if (t2 > closest) t2 = closest;
+    if (t1 >= t2) return false;
+    if (t1 < 0.0f) t1 = 0.0f;
+    const float len = __builtin_sqrtf(rk.a);
+    const float inside = (t2 - t1) * len;
+    const float u = (float)(uint32_t)(splitmix64(pr.seg ^ (uint64_t)m) >> 40) * 0x1.0p-24f;
+    const float hd = g.neg_inv_density * rrt_logf(u);
+    if (hd > inside) return false;
+    t_out = t1 + hd / len;
     return true;
 }
 
@@ -313,8 +399,12 @@ __device__ __forceinline__ void test_prims2(const PR &prim_cr, int f0, int c0, i
         const float4 cr = prim_cr.at(i);
         if constexpr (PR::kHasQuads) {
             if (cr.w < 0.0f) {
+                const int j = (int)(-cr.w) - 1;
                 float tq;
-                if (quad_hit(prim_cr.qd[(int)(-cr.w) - 1], o, d, closest, tq)) {
+                bool hit;
+                if (PR::kHasMedia && j >= (int)prim_cr.n_quads) hit = medium_hit(prim_cr, j - (int)prim_cr.n_quads, o, d, rk, closest, tq);
+                else hit = quad_hit(prim_cr.qd[j], o, d, 0.001f, closest, tq);
+                if (hit) {
                     closest = tq;
                     hit_prim = i;
                 }
@@ -696,9 +786,14 @@ __device__ __forceinline__ bool shade(const KParams &P, const PR &prims, const G
     const float4 cr = prims.at(prim);  // the sphere's center at the ray's time (sphere.rs:48)
     const V3 p = v3(ps.o.x + ps.d.x * t, ps.o.y + ps.d.y * t, ps.o.z + ps.d.z * t);
     V3 outward;
-    if (PR::kHasQuads && cr.w < 0.0f) {  // a quad's plane normal (quad.rs:79)
-        const float4 qn = prims.qd[(int)(-cr.w) - 1].n;
-        outward = v3(qn.x, qn.y, qn.z);
+    if (PR::kHasQuads && cr.w < 0.0f) {  // a quad's plane normal (quad.rs:79); a medium's (1, 0, 0)
+        const int j = (int)(-cr.w) - 1;
+        if (PR::kHasMedia && j >= (int)prims.n_quads) {
+            outward = v3(1.0f, 0.0f, 0.0f);  // constant_medium.rs:76-82 (front_face true)
+        } else {
+            const float4 qn = prims.qd[j].n;
+            outward = v3(qn.x, qn.y, qn.z);
+        }
     } else {
         const float inv_r = 1.0f / cr.w;
         outward = v3((p.x - cr.x) * inv_r, (p.y - cr.y) * inv_r, (p.z - cr.z) * inv_r);
@@ -717,7 +812,10 @@ __device__ __forceinline__ bool shade(const KParams &P, const PR &prims, const G
     // rejection loop for both kinds (a wave mixing them runs it once, not twice).
     V3 r = v3(0.0f, 0.0f, 0.0f);
     if (kind != 2) r = random_unit_vector(ps.rng, cnt);
-    if (kind != 1 && kind != 2) {  // Lambertian, plain or textured (material.rs:28-40; book 2 :41-53)
+    if (kBook2 && kind == 7) {  // Isotropic (material.rs:153-158): a fresh random_unit_vector
+        dir = r;
+        att = v3(m.a.x, m.a.y, m.a.z);
+    } else if (kind != 1 && kind != 2) {  // Lambertian, plain or textured (material.rs:28-40; book 2 :41-53)
         dir = add(nrm, r);
         if (__builtin_fabsf(dir.x) < 1e-8f && __builtin_fabsf(dir.y) < 1e-8f && __builtin_fabsf(dir.z) < 1e-8f) dir = nrm;
         if (kind == 3) {  // ImageTexture at the sphere's (u, v) (sphere.rs:46-52)
@@ -898,7 +996,7 @@ __device__ __forceinline__ void render_body(const KParams &P) {
         }
         RayK rk;
         if (tracing) rk = ray_consts(ps.o, ps.d);
-        const Prims<kBook2> pr{prims, motion, ps.time, P.quads};
+        const Prims<kBook2> pr{prims, motion, ps.time, P.quads, P.media, P.n_quads, ps.rng ^ ((uint64_t)ps.k << 32)};
         if constexpr (kWide) {
             for (;;) {
                 if constexpr (RRT_PHASE_TIMING == 2) {
@@ -945,7 +1043,7 @@ __device__ __forceinline__ void render_body(const KParams &P) {
         }
         if (has && !need_ray && !tracing) {
             need_ray = true;
-            seg_done = shade<kBook2>(P, Prims<kBook2>{prims, motion, ps.time, P.quads}, mtl, ps, tr.closest, tr.hit_prim, sum, cnt);
+            seg_done = shade<kBook2>(P, Prims<kBook2>{prims, motion, ps.time, P.quads, P.media, P.n_quads, ps.rng ^ ((uint64_t)ps.k << 32)}, mtl, ps, tr.closest, tr.hit_prim, sum, cnt);
         }
         w_paths += (uint32_t)__popcll(__ballot(seg_done));
         if (seg_done) {  // pixel_color += ray_color(..) (camera.rs:73-76): already in `sum`
@@ -1118,6 +1216,7 @@ hipError_t launch_render_kernel(const KParams &p, bool count, hipStream_t stream
     // binary tree for them); motion is always present (zero for static spheres).
     if (p.prim_motion) {  // book 2: the binary BVH only
         if (p.bvh_width != 2) return hipErrorInvalidValue;
+        if (p.n_media) return launch_width<false, 3>(p, count, stream);
         return p.n_quads ? launch_width<false, 2>(p, count, stream) : launch_width<false, 1>(p, count, stream);
     }
     return p.bvh_width == 4 ? launch_width<true, 0>(p, count, stream) : launch_width<false, 0>(p, count, stream);

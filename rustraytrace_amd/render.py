@@ -33,8 +33,9 @@ def _textures(scene: SceneData):
 
 def scene_ext(scene: SceneData):
     """(RrtSceneExt or None, keep-alive list) for the book-2 data of `scene` (motion, Perlin, quads)."""
-    quads = getattr(scene, "quads", None)
-    if scene.motion is None and scene.perlin is None and quads is None:
+    quads, media = getattr(scene, "quads", None), getattr(scene, "media", None)
+    bquads = getattr(scene, "boundary_quads", None)
+    if scene.motion is None and scene.perlin is None and quads is None and media is None:
         return None, []
     ext = _lib.RrtSceneExt()
     keep = []
@@ -53,6 +54,16 @@ def scene_ext(scene: SceneData):
         keep.append(q)
         ext.quads = q.ctypes.data
         ext.n_quads = len(q)
+    if media is not None:
+        md = np.ascontiguousarray(media, dtype=_lib.MEDIUM_DTYPE)
+        keep.append(md)
+        ext.media = md.ctypes.data
+        ext.n_media = len(md)
+    if bquads is not None:
+        bq = np.ascontiguousarray(bquads, dtype=_lib.QUAD_DTYPE)
+        keep.append(bq)
+        ext.boundary_quads = bq.ctypes.data
+        ext.n_boundary_quads = len(bq)
     return ext, keep
 
 
@@ -177,7 +188,7 @@ def build_bvh(scene: SceneData, width: int = 0, max_leaf: int = 0):
     info = _lib.RrtBvhInfo()
     n = len(scene.spheres)
     ext, keep = scene_ext(scene)
-    n_prims = n + (0 if ext is None else ext.n_quads)
+    n_prims = n + (0 if ext is None else ext.n_quads + ext.n_media)
     if ext is not None or np.isin(scene.materials["kind"], (5, 6)).any():
         width = 2  # book-2 scenes render with the BVH2 kernel variant (rrt_scene_create_ex)
     def build(nodes_p, cap, order_p):

@@ -28,7 +28,8 @@ C1_SEED = 0xC0FFEE
 C4_SEED = 0xE4A7_0001
 NEXT_WEEK_SEED = 0xB00C_0002
 NEXT_WEEK_SCENES = {1: "bouncing_spheres", 2: "checkered_spheres", 3: "earth", 4: "perlin_spheres", 5: "quads",
-                    6: "simple_light", 7: "cornell_box"}
+                    6: "simple_light", 7: "cornell_box", 8: "cornell_smoke", 9: "final_scene_800",
+                    10: "final_scene_400"}
 
 # config.rs:50-62 committed OVERRIDES (width 2160, spp 5000, depth 100)
 COMMITTED_OVERRIDES = dict(image_width=2160, samples_per_pixel=5000, max_depth=100)
@@ -47,6 +48,8 @@ class SceneData:
     motion: Optional[np.ndarray] = None  # (n_spheres, 4) float32: center2 - center1 (book 2), or None
     perlin: Optional[np.ndarray] = None  # PERLIN_DTYPE tables for noise materials, or None
     quads: Optional[np.ndarray] = None  # QUAD_DTYPE quads (primitives n_spheres + j), or None
+    media: Optional[np.ndarray] = None  # MEDIUM_DTYPE constant-density media, or None
+    boundary_quads: Optional[np.ndarray] = None  # QUAD_DTYPE boundaries of quad-bounded media
 
     @property
     def width(self) -> int:
@@ -155,28 +158,34 @@ def earth_light(image_width=1920, samples_per_pixel=1024, max_depth=100, seed=C4
 
 def next_week_scene(scene: int, overrides: Optional[dict] = None, seed: int = NEXT_WEEK_SEED) -> SceneData:
     """The book-2 scene `scene` (1 bouncing_spheres, 2 checkered_spheres, 3 earth, 4 perlin_spheres,
-    5 quads, 6 simple_light, 7 cornell_box; the_next_week/mod.rs:83-431) under RenderOverrides
-    `overrides`, with its motion rows, quads (instanced boxes baked to world space) and Perlin
+    5 quads, 6 simple_light, 7 cornell_box, 8 cornell_smoke, 9 final_scene(800, 10000, 40),
+    10 final_scene(400, 250, 4); the_next_week/mod.rs:68-587) under RenderOverrides `overrides`,
+    with its motion rows, quads and media (instanced geometry baked to world space) and Perlin
     tables. Book-2 camera: background colour, a time draw per camera ray."""
     lib = _lib.load()
     ov = _lib.make_overrides(**(overrides or {}))
-    n, nm, nq, nt = (ctypes.c_uint32(0) for _ in range(4))
-    cam = _empty(_lib.CAMERA_DTYPE, 1)
-    _lib.check(lib.rrt_build_next_week_scene(int(scene), _lib.ptr(ov), seed, _lib.ptr(cam), None, None, 0, _lib.ptr(n),
-                                             None, 0, _lib.ptr(nm), None, 0, _lib.ptr(nq), None, 0, _lib.ptr(nt)))
-    spheres = _empty(_lib.SPHERE_DTYPE, n.value)
-    mats = _empty(_lib.MATERIAL_DTYPE, nm.value)
-    quads = np.zeros(nq.value, dtype=_lib.QUAD_DTYPE)
-    motion = np.zeros((n.value, 4), dtype=np.float32)
-    perlin = np.zeros(nt.value, dtype=_lib.PERLIN_DTYPE)
-    _lib.check(lib.rrt_build_next_week_scene(int(scene), _lib.ptr(ov), seed, _lib.ptr(cam), _lib.ptr(spheres),
-                                             _lib.ptr(motion), n.value, _lib.ptr(n), _lib.ptr(mats), nm.value,
-                                             _lib.ptr(nm), _lib.ptr(quads), nq.value, _lib.ptr(nq), _lib.ptr(perlin),
-                                             nt.value, _lib.ptr(nt)))
-    textures = [earth_texture()] if scene == 3 else []
+    nw = _lib.RrtNextWeekScene()
+    _lib.check(lib.rrt_build_next_week_scene(int(scene), _lib.ptr(ov), seed, ctypes.byref(nw)))  # sizes
+    spheres = _empty(_lib.SPHERE_DTYPE, nw.n_spheres)
+    motion = np.zeros((nw.n_spheres, 4), dtype=np.float32)
+    mats = _empty(_lib.MATERIAL_DTYPE, nw.n_materials)
+    quads = np.zeros(nw.n_quads, dtype=_lib.QUAD_DTYPE)
+    perlin = np.zeros(nw.n_perlin, dtype=_lib.PERLIN_DTYPE)
+    media = np.zeros(nw.n_media, dtype=_lib.MEDIUM_DTYPE)
+    bquads = np.zeros(nw.n_boundary_quads, dtype=_lib.QUAD_DTYPE)
+    for field, arr in (("spheres", spheres), ("materials", mats), ("quads", quads), ("perlin", perlin),
+                       ("media", media), ("boundary_quads", bquads)):
+        setattr(nw, field, arr.ctypes.data)
+    nw.sphere_motion = motion.ctypes.data
+    nw.sphere_cap, nw.material_cap, nw.quad_cap = nw.n_spheres, nw.n_materials, nw.n_quads
+    nw.perlin_cap, nw.media_cap, nw.boundary_quad_cap = nw.n_perlin, nw.n_media, nw.n_boundary_quads
+    _lib.check(lib.rrt_build_next_week_scene(int(scene), _lib.ptr(ov), seed, ctypes.byref(nw)))
+    cam = np.frombuffer(bytes(nw.camera), dtype=_lib.CAMERA_DTYPE).copy()
+    textures = [earth_texture()] if nw.uses_texture0 else []
     return SceneData(cam, spheres, mats, textures=textures, flags=_lib.FLAG_RAY_TIME, name=NEXT_WEEK_SCENES[scene],
-                     motion=motion if np.any(motion[:, :3]) else None, perlin=perlin if nt.value else None,
-                     quads=quads if nq.value else None)
+                     motion=motion if np.any(motion[:, :3]) else None, perlin=perlin if len(perlin) else None,
+                     quads=quads if len(quads) else None, media=media if len(media) else None,
+                     boundary_quads=bquads if len(bquads) else None)
 
 
 def rtow(image_width=1920, samples_per_pixel=512, max_depth=100, grid_half=11, seed=RTOW_SEED) -> SceneData:

@@ -114,8 +114,9 @@ def test_next_week_scene_structure():
     assert not np.array_equal(rrt.next_week_scene(1, seed=5).spheres["center_radius"], s1.spheres["center_radius"])
     o = rrt.next_week_scene(2, dict(image_width=64, samples_per_pixel=3, background=(0.1, 0.2, 0.3)))
     assert (o.width, o.spp) == (64, 3) and np.allclose(o.camera["background"][0, :3], [0.1, 0.2, 0.3])
-    with pytest.raises(rrt.RrtError):
-        rrt.next_week_scene(8)  # cornell_smoke (ConstantMedium) is not in the ABI yet
+    for bad in (0, 11):
+        with pytest.raises(rrt.RrtError):
+            rrt.next_week_scene(bad)
 
 
 def test_moving_sphere_boxes_span_both_ends():
@@ -143,24 +144,31 @@ def test_moving_sphere_boxes_span_both_ends():
 
 
 # ---- the oracle's two arithmetics and two trees agree on book-2 scenes -------------------------------
-@pytest.mark.parametrize("scene", [1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("scene", [1, 2, 3, 4, 5, 6, 7, 8, 10])
 def test_book2_books_vs_twin_statistical(scene):
-    sc = rrt.next_week_scene(scene, dict(image_width=48, samples_per_pixel=8, max_depth=10))
+    sc = rrt.next_week_scene(scene, dict(image_width=48, samples_per_pixel=8, max_depth=4 if scene == 10 else 10))
     t, rt, _ = oracle.render(sc, oracle.TWIN, threads=8)
     b, rb, _ = oracle.render(sc, oracle.BOOKS, threads=8)
     per_chan = np.abs(t - b)[..., :3] / sc.spp
     assert (per_chan <= 1e-4).mean() > 0.85
-    assert abs(t[..., :3].mean() - b[..., :3].mean()) / b[..., :3].mean() < 0.01
-    assert abs(rt - rb) / rb < 0.01
+    # final_scene sits at |p| ~ 500-1000, where an f32 hit point is off its surface by ~6e-5: a
+    # Lambertian bounce with d.n < ~0.06 then re-hits the same sphere past tmin = 0.001 (f64
+    # never does). At the scene's depth 4 that is ~1.2 % more segments and -1.8 % mean radiance,
+    # stable from 8 to 256 spp — the f32 arithmetic, matched bit for bit by the kernel
+    tol_mean, tol_rays = (0.03, 0.02) if scene == 10 else (0.01, 0.01)
+    assert abs(t[..., :3].mean() - b[..., :3].mean()) / b[..., :3].mean() < tol_mean
+    assert abs(rt - rb) / rb < tol_rays
 
 
-@pytest.mark.parametrize("scene", [1, 2, 4, 5, 6, 7])
+@pytest.mark.parametrize("scene", [1, 2, 4, 5, 6, 7, 8, 10])
 def test_book2_kbvh_agrees_with_books_tree(scene):
     sc = rrt.next_week_scene(scene, dict(image_width=48, samples_per_pixel=4, max_depth=10))
     a, ra, _ = oracle.render(sc, oracle.TWIN, threads=4)
     nodes, order, info = build_bvh(sc)
     b, rb, _ = oracle.render_kbvh(sc, nodes, order, 2, threads=4)
-    assert np.array_equal(a, b) and ra == rb
+    # quads: exact t-ties at shared edges go to the first quad tested, which can turn a
+    # zero-contribution path differently in the two trees (tests/test_gpu_book2.py)
+    assert np.array_equal(a, b) and (ra == rb or sc.quads is not None)
 
 
 def test_motion_blur_changes_the_image():
@@ -301,3 +309,78 @@ def test_quad_bvh_boxes_contain_quads():
                     assert np.all(blo <= p) and np.all(p <= bhi)
                 checked += 1
     assert checked == 18
+
+
+# ---- constant-density media (the_next_week/constant_medium.rs) and scenes 8-10 -------------------
+def test_log_f32_accuracy():
+    x = (np.arange(1, 1 << 24, 61, dtype=np.float64) * 2.0 ** -24).astype(np.float32)
+    got = oracle.log_f32(x).astype(np.float64)
+    want = np.log(x.astype(np.float64))
+    assert np.max(np.abs(got - want)) < 1e-6 and np.max(np.abs(got - want) / np.abs(want)) < 2e-7
+    assert oracle.log_f32([0.0])[0] == -np.inf and oracle.log_f32([1.0])[0] == 0.0
+
+
+def test_medium_draw_is_uniform_and_keyed():
+    rng = np.random.default_rng(5)
+    seg = rng.integers(0, 2 ** 63, 200000, dtype=np.uint64)
+    u0, u1 = oracle.medium_u(seg, 0), oracle.medium_u(seg, 1)
+    for u in (u0, u1):
+        assert 0.0 <= u.min() and u.max() < 1.0 and abs(u.mean() - 0.5) < 0.003
+        assert np.all(u * 2 ** 24 == np.floor(u * 2 ** 24))  # 24-bit grid
+        assert abs(np.histogram(u, 16, (0, 1))[0] / len(u) - 1 / 16).max() < 0.003
+    assert abs(np.corrcoef(u0, u1)[0, 1]) < 0.01  # media of one segment draw independently
+
+
+def medium_box_scene(density, width=32, spp=64):
+    """A black-phase medium filling the box [-1, 1]^3 in front of a white background: a camera
+    ray survives (pixel value 1) iff it does not scatter, probability exp(-density * chord)."""
+    from rustraytrace_amd.scenes import _material, make_camera
+
+    cam = make_camera(aspect_ratio=1.0, image_width=width, samples_per_pixel=spp, max_depth=2, vfov=10.0,
+                      lookfrom=(0.0, 0.0, 6.0), lookat=(0.0, 0.0, 0.0), background=(1.0, 1.0, 1.0), seed=77)
+    mats = _material(7, (0.0, 0.0, 0.0))  # RRT_MAT_ISOTROPIC, black: a scattered path carries nothing
+    bq = np.zeros(6, dtype=rrt._lib.QUAD_DTYPE)
+    faces = [((-1, -1, 1), (2, 0, 0), (0, 2, 0)), ((1, -1, 1), (0, 0, -2), (0, 2, 0)), ((1, -1, -1), (-2, 0, 0), (0, 2, 0)),
+             ((-1, -1, -1), (0, 0, 2), (0, 2, 0)), ((-1, 1, 1), (2, 0, 0), (0, 0, -2)), ((-1, -1, -1), (2, 0, 0), (0, 0, 2))]
+    for k, (q, u, v) in enumerate(faces):
+        bq[k]["q"][:3], bq[k]["u"][:3], bq[k]["v"][:3] = q, u, v
+    md = np.zeros(1, dtype=rrt._lib.MEDIUM_DTYPE)
+    md[0]["boundary_kind"], md[0]["first"], md[0]["count"] = 1, 0, 6
+    md[0]["material_index"], md[0]["density"] = 0, density
+    return rrt.SceneData(cam, np.zeros(0, dtype=rrt._lib.SPHERE_DTYPE), mats, flags=rrt._lib.FLAG_RAY_TIME,
+                         name="medium_box", media=md, boundary_quads=bq)
+
+
+@pytest.mark.parametrize("density", [0.2, 0.7])
+def test_medium_transmittance_matches_beer_lambert(density):
+    sc = medium_box_scene(density)
+    for mode in (oracle.TWIN, oracle.BOOKS):
+        img, _, _ = oracle.render(sc, mode, threads=8)
+        centre = img[12:20, 12:20, 0] / sc.spp  # rays within ~0.1 of the axis: chord ~2
+        want = np.exp(-2.0 * density)
+        assert abs(centre.mean() - want) < 4 * np.sqrt(want * (1 - want) / (64 * sc.spp)) + 0.01
+
+
+def test_media_scene_structure():
+    s8 = rrt.next_week_scene(8)
+    assert len(s8.spheres) == 0 and len(s8.quads) == 6 and len(s8.media) == 2 and len(s8.boundary_quads) == 12
+    kinds = s8.materials["kind"][s8.media["material_index"]]
+    assert kinds.tolist() == [7, 7] and np.allclose(s8.media["density"], 0.01)
+    assert np.allclose(s8.materials["albedo_fuzz"][s8.media["material_index"], :3], [[0, 0, 0], [1, 1, 1]])
+    assert (s8.media["boundary_kind"] == 1).all() and s8.media["first"].tolist() == [0, 6]
+    s10 = rrt.next_week_scene(10)
+    assert (s10.width, s10.spp, s10.max_depth) == (400, 250, 4) and len(s10.textures) == 1
+    assert len(s10.quads) == 20 * 20 * 6 + 1 and len(s10.spheres) == 6 + 1000 and len(s10.media) == 2
+    assert s10.media["boundary_kind"].tolist() == [0, 0] and s10.media["sphere"][:, 3].tolist() == [70.0, 5000.0]
+    assert s10.motion is not None and np.count_nonzero(s10.motion[:, 0]) == 1  # the one moving sphere (+30 x)
+    heights = s10.quads["q"][:2400:6, 1] + s10.quads["v"][:2400:6, 1]  # y1 of each ground box
+    assert heights.min() >= 1.0 and heights.max() < 101.0 and len(np.unique(heights)) > 390
+    cluster = s10.spheres["center_radius"][-1000:, :3]  # RotateY(15) + Translate(-100, 270, 395) baked
+    th = np.radians(15.0)
+    local_x = np.cos(th) * (cluster[:, 0] + 100) - np.sin(th) * (cluster[:, 2] - 395)
+    local_z = np.sin(th) * (cluster[:, 0] + 100) + np.cos(th) * (cluster[:, 2] - 395)
+    for c in (local_x, cluster[:, 1] - 270, local_z):
+        assert c.min() > -1e-3 and c.max() < 165 + 1e-3
+    s9 = rrt.next_week_scene(9)
+    assert (s9.width, s9.spp, s9.max_depth) == (800, 10000, 40)
+    assert len(s9.spheres) == len(s10.spheres) and len(s9.quads) == len(s10.quads)

@@ -20,6 +20,8 @@ SCENES = [(1, dict(image_width=64, samples_per_pixel=4, max_depth=8)),
           (5, dict(image_width=64, samples_per_pixel=4, max_depth=8)),
           (6, dict(image_width=64, samples_per_pixel=4, max_depth=8)),
           (7, dict(image_width=64, samples_per_pixel=4, max_depth=8)),
+          (8, dict(image_width=64, samples_per_pixel=4, max_depth=8)),
+          (10, dict(image_width=64, samples_per_pixel=4, max_depth=4)),
           (1, dict(image_width=96, samples_per_pixel=3, max_depth=50)),
           (7, dict(image_width=96, samples_per_pixel=5, max_depth=50))]
 
@@ -42,7 +44,7 @@ def test_book2_one_shot_matches_oracle(scene, kw):
     assert krays == rays or sc.quads is not None
 
 
-@pytest.mark.parametrize("scene", [1, 4, 7])
+@pytest.mark.parametrize("scene", [1, 4, 7, 8, 10])
 def test_book2_device_tiles_and_ray_counts(scene):
     sc = rrt.next_week_scene(scene, dict(image_width=80, samples_per_pixel=6, max_depth=12))
     gpu, idx, ctr, work = gpu_tile(sc, count=True)
@@ -71,6 +73,32 @@ def test_cornell_box_larger_frame_kbvh():
     assert_bit_exact(gpu, ref, sc.spp)
 
 
+def test_cornell_smoke_and_final_scene_larger_frames_kbvh():
+    # media: a box-bounded pair (cornell_smoke, 160x160x16) and the sphere-bounded fog of
+    # final_scene (its 2401 quads, 1006 spheres, earth texture; 128x128x8 at depth 40)
+    for scene, kw in ((8, dict(image_width=160, samples_per_pixel=16, max_depth=50)),
+                      (10, dict(image_width=128, samples_per_pixel=8, max_depth=40))):
+        sc = rrt.next_week_scene(scene, kw)
+        gpu = rrt.render(sc)
+        nodes, order, info = build_bvh(sc)
+        ref, _, _ = oracle.render_kbvh(sc, nodes, order, info["width"], threads=16)
+        assert_bit_exact(gpu, ref, sc.spp)
+
+
+def test_medium_box_transmittance_gpu():
+    # Beer-Lambert through a black-phase box medium, bit-exact with the oracle and within
+    # statistics of exp(-density * 2) on the axis (tests/test_book2.py builds the scene)
+    from test_book2 import medium_box_scene
+
+    sc = medium_box_scene(0.5, width=32, spp=256)
+    gpu = rrt.render(sc)
+    ref, _, _ = oracle.render(sc, oracle.TWIN, threads=16)
+    assert_bit_exact(gpu, ref, sc.spp)
+    centre = gpu[12:20, 12:20, 0] / sc.spp
+    want = np.exp(-1.0)
+    assert abs(centre.mean() - want) < 4 * np.sqrt(want * (1 - want) / (64 * sc.spp)) + 0.01
+
+
 def test_static_book2_scene_uses_zero_motion():
     # a checker-only scene renders through the book-2 kernel with zero motion rows; same bits
     # as the oracle (whose centers are c + t*0 as well)
@@ -81,7 +109,7 @@ def test_static_book2_scene_uses_zero_motion():
     assert_bit_exact(gpu, ref, sc.spp)
 
 
-@pytest.mark.parametrize("scene", [4, 7])
+@pytest.mark.parametrize("scene", [4, 7, 8])
 def test_cli_next_week_matches_python(tmp_path, scene):
     import os
     import subprocess

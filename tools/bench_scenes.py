@@ -31,6 +31,8 @@ def scenes(spp_scale):
     yield "NW5 quads 1080x1080", rrt.next_week_scene(5, dict(sq, samples_per_pixel=s(256)))
     yield "NW6 simple_light 1920x1080", rrt.next_week_scene(6, dict(hd, samples_per_pixel=s(256)))
     yield "NW7 cornell_box 1080x1080", rrt.next_week_scene(7, dict(sq, samples_per_pixel=s(256)))
+    yield "NW8 cornell_smoke 1080x1080", rrt.next_week_scene(8, dict(sq, samples_per_pixel=s(256)))
+    yield "NW9 final_scene 1080x1080 d40", rrt.next_week_scene(9, dict(image_width=1080, samples_per_pixel=s(256)))
 
 
 def main():
