@@ -26,8 +26,9 @@
 extern "C" {
 #endif
 
-/* 1: book 1; 2: RrtSceneExt (motion, Perlin), kinds 5-6; 3: quads and constant-density media in
- * RrtSceneExt, kind 7, rrt_build_next_week_scene with separate material / quad / medium outputs. */
+/* 1: book 1; 2: RrtSceneExt (motion, Perlin), kinds 5-6; 3: quads, constant-density media and
+ * book-3 light lists in RrtSceneExt, kind 7, RRT_FLAG_BOOK3, rrt_build_next_week_scene /
+ * rrt_build_rest_of_your_life_scene with struct outputs. */
 #define RRT_ABI_VERSION 3u
 
 /* ---- scene ABI (== src/gpu/mod.rs:13-42) ------------------------------------------ */
@@ -125,6 +126,20 @@ typedef struct RrtMedium {
 
 enum { RRT_BOUNDARY_SPHERE = 0, RRT_BOUNDARY_QUADS = 1 };
 
+/* == a book-3 light-list entry (the_rest_of_your_life/mod.rs `lights`, sampled by HittablePdf,
+ * pdf.rs:58-78): a Quad (kind 0: corner q = a.xyz, edges u, v; quad.rs:93-107 pdf_value /
+ * random) or a Sphere (kind 1: center a.xyz, radius a[3]; sphere.rs:55-66, 102-122). 64 B.
+ * Sampling targets only: not surfaces of the scene (add those separately). */
+typedef struct RrtLight {
+    uint32_t kind;
+    uint32_t _pad[3];
+    float a[4];
+    float u[4];
+    float v[4];
+} RrtLight;
+
+enum { RRT_LIGHT_QUAD = 0, RRT_LIGHT_SPHERE = 1 };
+
 /* Book-2 scene data beyond the flat sphere/material ABI. NULL = none.
  * sphere_motion: n_spheres x 4 floats, (center2 - center1).xyz of Sphere::new_moving
  * (the_next_week/sphere.rs:24-40; the sphere's center at ray time t is center1 + t*motion;
@@ -143,6 +158,9 @@ typedef struct RrtSceneExt {
     uint32_t n_media;
     uint32_t n_boundary_quads;
     const RrtQuad *boundary_quads;
+    const RrtLight *lights; /* book 3 (RRT_FLAG_BOOK3): the MIS light list */
+    uint32_t n_lights;
+    uint32_t _pad;
 } RrtSceneExt;
 
 /* Image texture, RGB8 row-major (rtw_image.rs:57-67 `to_rgb8().into_raw()`). Borrowed. */
@@ -173,6 +191,12 @@ typedef struct RrtOverrides {
 #define RRT_FLAG_RAY_TIME 0x1u
 /* Suppress the stderr progress lines (cuda/mod.rs:426-431 style). */
 #define RRT_FLAG_QUIET 0x2u
+/* Book-3 integrator (the_rest_of_your_life/camera.rs:96-254): stratified camera samples
+ * (samples_per_pixel must be a square, sqrt_spp^2; sample s = s_j * sqrt_spp + s_i), one-sided
+ * DiffuseLight, Lambertian / Isotropic scatter by the mixture pdf 0.5 * lights + 0.5 * material
+ * (cosine / sphere pdf) over RrtSceneExt.lights, Russian roulette folded into the weight.
+ * Requires RRT_FLAG_RAY_TIME (the book-3 camera draws a time per ray). */
+#define RRT_FLAG_BOOK3 0x4u
 
 /* ---- error codes ------------------------------------------------------------------ */
 #define RRT_OK 0
@@ -315,7 +339,7 @@ int32_t rrt_build_in_one_weekend_scene(const RrtOverrides *ov, uint64_t seed, in
  * needed. uses_texture0 = 1 when a material samples texture 0, the earth image the caller
  * supplies. The camera carries book 2's background (bg_mode 1); render with RRT_FLAG_RAY_TIME
  * and an RrtSceneExt over these arrays. */
-typedef struct RrtNextWeekScene {
+typedef struct RrtBookScene {
     RrtCamera camera;
     RrtSphere *spheres;
     float *sphere_motion; /* sphere_cap x 4 floats, may be NULL */
@@ -324,17 +348,26 @@ typedef struct RrtNextWeekScene {
     RrtPerlin *perlin;
     RrtMedium *media;
     RrtQuad *boundary_quads;
+    RrtLight *lights;
     uint32_t sphere_cap, n_spheres;
     uint32_t material_cap, n_materials;
     uint32_t quad_cap, n_quads;
     uint32_t perlin_cap, n_perlin;
     uint32_t media_cap, n_media;
     uint32_t boundary_quad_cap, n_boundary_quads;
+    uint32_t light_cap, n_lights;
     uint32_t uses_texture0;
-    uint32_t _pad;
-} RrtNextWeekScene;
+    uint32_t flags; /* the RRT_FLAG_* the scene renders with (RAY_TIME; BOOK3 for book 3) */
+} RrtBookScene;
 
-int32_t rrt_build_next_week_scene(int32_t scene, const RrtOverrides *ov, uint64_t seed, RrtNextWeekScene *out);
+int32_t rrt_build_next_week_scene(int32_t scene, const RrtOverrides *ov, uint64_t seed, RrtBookScene *out);
+
+/* The book-3 scene (the_rest_of_your_life/mod.rs:69-164): the Cornell box with one rotated box
+ * and a glass sphere, the light list {the light quad, the glass sphere} for MIS. The camera's
+ * samples_per_pixel is rounded down to sqrt_spp^2 (Camera::initialize, camera.rs:115-117).
+ * Render with out->flags (RRT_FLAG_RAY_TIME | RRT_FLAG_BOOK3) and an RrtSceneExt over the arrays
+ * (lights included). */
+int32_t rrt_build_rest_of_your_life_scene(const RrtOverrides *ov, uint64_t seed, RrtBookScene *out);
 
 /* Camera::initialize (in_one_weekend/camera.rs:102-150) in f64, cast to the f32 ABI as
  * gpu/mod.rs:278-298 does. lookfrom/lookat/vup are 3-vectors. */

@@ -44,6 +44,8 @@ def load() -> ctypes.CDLL:
                                        c_uint32, c_uint32, c_uint32, c_uint32, c_int, P, P, P, c_uint32]
     lib.oracle_sin_f32.restype = None
     lib.oracle_sin_f32.argtypes = [c_uint32, P, P]
+    lib.oracle_cos_f32.restype = None
+    lib.oracle_cos_f32.argtypes = [c_uint32, P, P]
     lib.oracle_log_f32.restype = None
     lib.oracle_log_f32.argtypes = [c_uint32, P, P]
     lib.oracle_medium_u.restype = None
@@ -90,15 +92,15 @@ class _Tex(ctypes.Structure):
 class _Ext(ctypes.Structure):  # RrtSceneExt (include/rrt_hip.h)
     _fields_ = [("sphere_motion", c_void_p), ("perlin", c_void_p), ("n_perlin", c_uint32), ("n_quads", c_uint32),
                 ("quads", c_void_p), ("media", c_void_p), ("n_media", c_uint32), ("n_boundary_quads", c_uint32),
-                ("boundary_quads", c_void_p)]
+                ("boundary_quads", c_void_p), ("lights", c_void_p), ("n_lights", c_uint32), ("_pad", c_uint32)]
 
 
 def _ext(scene):
     """(pointer to RrtSceneExt or None, keep-alive) from the scene's book-2 motion / Perlin / quad data."""
     motion, perlin = getattr(scene, "motion", None), getattr(scene, "perlin", None)
     quads, media = getattr(scene, "quads", None), getattr(scene, "media", None)
-    bquads = getattr(scene, "boundary_quads", None)
-    if motion is None and perlin is None and quads is None and media is None:
+    bquads, lights = getattr(scene, "boundary_quads", None), getattr(scene, "lights", None)
+    if motion is None and perlin is None and quads is None and media is None and lights is None:
         return None, []
     e, keep = _Ext(), []
     if motion is not None:
@@ -129,6 +131,12 @@ def _ext(scene):
         keep.append(bq)
         e.boundary_quads = bq.ctypes.data
         e.n_boundary_quads = len(bq)
+    if lights is not None:
+        lt = np.ascontiguousarray(lights)
+        assert lt.dtype.itemsize == 64, "RrtLight records"
+        keep.append(lt)
+        e.lights = lt.ctypes.data
+        e.n_lights = len(lt)
     keep.append(e)
     return ctypes.cast(ctypes.byref(e), c_void_p), keep
 
@@ -272,6 +280,15 @@ def acos_atan2_f32(x, y):
     a, b = c_float(0), c_float(0)
     lib.oracle_acos_atan2_f32(x, y, ctypes.byref(a), ctypes.byref(b))
     return a.value, b.value
+
+
+def cos_f32(x):
+    """The f32 Cephes cos of the kernel (rrt_cosf) at each element of x."""
+    lib = load()
+    xs = np.ascontiguousarray(x, dtype=np.float32).ravel()
+    out = np.zeros_like(xs)
+    lib.oracle_cos_f32(xs.size, _p(xs), _p(out))
+    return out
 
 
 def log_f32(x):

@@ -263,6 +263,32 @@ float cephes_logf(float x) {
     r = r + 0.693359375f * fe;
     return r;
 }
+// Cephes cosf: the kernel's rrt_cosf op for op.
+float cephes_cosf(float xx) {
+    float x = xx < 0.0f ? -xx : xx;
+    if (x > 16777215.0f) return 0.0f;
+    if (!(x == x)) return xx;
+    float sign = 1.0f;
+    int j = (int)(1.27323954473516f * x);
+    float y = (float)j;
+    if (j & 1) { j += 1; y += 1.0f; }
+    j &= 7;
+    if (j > 3) { j -= 4; sign = -sign; }
+    if (j > 1) sign = -sign;
+    if (x > 8192.0f) x = x - y * 0.7853981633974483096f;
+    else x = ((x - y * 0.78515625f) - y * 2.4187564849853515625e-4f) - y * 3.77489497744594108e-8f;
+    const float z = x * x;
+    if (j == 1 || j == 2) {
+        y = ((-1.9515295891e-4f * z + 8.3321608736e-3f) * z - 1.6666654611e-1f) * z * x;
+        y = y + x;
+    } else {
+        y = ((2.443315711809948e-5f * z - 1.388731625493765e-3f) * z + 4.166664568298827e-2f) * z * z;
+        y = y - 0.5f * z;
+        y = y + 1.0f;
+    }
+    return sign < 0.0f ? -y : y;
+}
+float cephes_sinf(float xx);
 template <class T> T t_log(T x) { if constexpr (std::is_same_v<T, float>) return cephes_logf(x); else return std::log(x); }
 
 // ---- scene in T ---------------------------------------------------------------------------------
@@ -350,6 +376,14 @@ template <class T> struct World {
     std::vector<QuadT<T>> quads;  // primitive n_spheres + j
     std::vector<MediumT<T>> media;  // primitive n_spheres + n_quads + m
     std::vector<QuadT<T>> bquads;  // media boundaries
+    struct LightT {  // book-3 MIS light (RrtLight)
+        uint32_t kind;
+        Vec3<T> center;
+        T radius;
+        QuadT<T> quad;
+        T area;
+    };
+    std::vector<LightT> lights;
     std::vector<Material<T>> mats;
     std::vector<Texture> texs;
     std::vector<PerlinT<T>> perlin;
@@ -706,6 +740,8 @@ template <class T> struct Cam {
     T radius;
     uint32_t max_depth, seed, bg_mode, flags;
     uint32_t width, height;
+    uint32_t sqrt_spp = 0;  // book 3: stratified samples
+    T recip_sqrt_spp = T(0);
 };
 
 template <class T>
@@ -724,6 +760,10 @@ void load_world(World<T> &w, Cam<T> &cam, const RrtCamera *c, const RrtSphere *s
     cam.seed = c->params_u[1];
     cam.bg_mode = c->params_u[3];
     cam.flags = flags;
+    if (flags & RRT_FLAG_BOOK3) {  // Camera::initialize (the_rest_of_your_life/camera.rs:115-117)
+        cam.sqrt_spp = (uint32_t)std::sqrt((double)std::max(c->params_f[3], 1.0f));
+        cam.recip_sqrt_spp = (T)(1.0 / (double)cam.sqrt_spp);
+    }
     cam.width = (uint32_t)c->params_f[1];
     cam.height = (uint32_t)c->params_f[2];
     const float *motion = ext ? ext->sphere_motion : nullptr;
@@ -798,6 +838,22 @@ void load_world(World<T> &w, Cam<T> &cam, const RrtCamera *c, const RrtSphere *s
             }
             w.perlin.push_back(pt);
         }
+    const uint32_t nl = ext && ext->lights ? ext->n_lights : 0u;
+    for (uint32_t l = 0; l < nl; ++l) {
+        const RrtLight &L = ext->lights[l];
+        typename World<T>::LightT lt{};
+        lt.kind = L.kind;
+        lt.center = v3(L.a);
+        lt.radius = std::max((T)L.a[3], T(0));
+        if (L.kind == RRT_LIGHT_QUAD) {
+            RrtQuad rq{};
+            for (int i = 0; i < 3; ++i) rq.q[i] = L.a[i], rq.u[i] = L.u[i], rq.v[i] = L.v[i];
+            lt.quad = make_quad<T>(rq);
+            const Vec3<double> nv = cross(mk<double>(L.u[0], L.u[1], L.u[2]), mk<double>(L.v[0], L.v[1], L.v[2]));
+            lt.area = (T)length(nv);  // quad.rs:28
+        }
+        w.lights.push_back(lt);
+    }
     const uint32_t np = n + nq + nmd;
     if (np) {
         std::vector<int32_t> objs(np);
@@ -1088,11 +1144,211 @@ Vec3<T> ray_color_twin(const World<T> &w, const Cam<T> &cam, PathRng &rng, Vec3<
     return Lp;
 }
 
+// ---- book 3 (the_rest_of_your_life): pdf.rs, onb.rs, quad.rs / sphere.rs pdf_value and random ----
+template <class T> T t_cos(T x) { if constexpr (std::is_same_v<T, float>) return cephes_cosf(x); else return std::cos(x); }
+template <class T> T t_sin3(T x) { if constexpr (std::is_same_v<T, float>) return cephes_sinf(x); else return std::sin(x); }
+
+template <class T> Vec3<T> onb_transform(Vec3<T> n, Vec3<T> a) {  // Onb::new(n).transform(a)
+    const Vec3<T> w = unit_vector(n);
+    const Vec3<T> ax = std::fabs(w[0]) > L(0.9) ? mk(T(0), T(1), T(0)) : mk(T(1), T(0), T(0));
+    const Vec3<T> v = unit_vector(cross(w, ax));
+    const Vec3<T> u = cross(w, v);
+    return a[0] * u + a[1] * v + a[2] * w;
+}
+
+// HittableList::pdf_value over the light list (hittable_list.rs:60-69)
+template <class T> T lights_pdf(const World<T> &w, Vec3<T> o, Vec3<T> d) {
+    const T inf = std::numeric_limits<T>::infinity();
+    const T weight = T(1) / (T)w.lights.size();
+    T sum = T(0);
+    for (const auto &lt : w.lights) {
+        T pdf = T(0), t;
+        if (lt.kind == RRT_LIGHT_QUAD) {  // quad.rs:93-102
+            if (World<T>::quad_hit(lt.quad, o, d, Interval<T>{L(0.001), inf}, t)) {
+                const T dist2 = t * t * length_squared(d);
+                const T cosine = std::fabs(dot(d, lt.quad.normal)) / length(d);
+                pdf = dist2 / (cosine * lt.area);
+            }
+        } else if (World<T>::sphere_root(lt.center, lt.radius, o, d, Interval<T>{L(0.001), inf}, t)) {  // sphere.rs:102-115
+            const T dist2 = length_squared(lt.center - o);
+            const T cos_max = std::sqrt(T(1) - lt.radius * lt.radius / dist2);
+            pdf = T(1) / ((T(2) * t_pi<T>()) * (T(1) - cos_max));
+        }
+        sum = sum + weight * pdf;
+    }
+    return sum;
+}
+
+// HittableList::random (hittable_list.rs:71-75) + Quad::random / Sphere::random
+template <class T> Vec3<T> lights_random(const World<T> &w, Vec3<T> o, PathRng &rng) {
+    const int idx = (int)rng.random_double_range<T>(T(0), (T)w.lights.size());
+    const auto &lt = w.lights[idx];
+    if (lt.kind == RRT_LIGHT_QUAD) {
+        const T r1 = rng.random_double<T>();
+        const Vec3<T> a = lt.quad.q + r1 * lt.quad.u;
+        const T r2 = rng.random_double<T>();
+        return (a + r2 * lt.quad.v) - o;
+    }
+    const Vec3<T> dir = lt.center - o;
+    const T d2 = length_squared(dir);
+    const T r1 = rng.random_double<T>(), r2 = rng.random_double<T>();
+    const T z = T(1) + r2 * (std::sqrt(T(1) - lt.radius * lt.radius / d2) - T(1));
+    const T phi = (T(2) * t_pi<T>()) * r1;
+    const T sxy = std::sqrt(T(1) - z * z);
+    return onb_transform(dir, mk(t_cos(phi) * sxy, t_sin3(phi) * sxy, z));
+}
+
+// The attenuation of a pdf-sampled material (Lambertian textures / Isotropic albedo).
+template <class T> Vec3<T> b3_attenuation(const World<T> &w, const Material<T> &m, const Record<T> &rec) {
+    if (m.kind == RRT_MAT_TEXTURED_LAMBERTIAN) return texture_value(w, m.tex, rec.outward);
+    if (m.kind == RRT_MAT_CHECKER_LAMBERTIAN) return checker_even(m.w, rec.p) ? m.albedo : m.odd;
+    if (m.kind == RRT_MAT_NOISE_LAMBERTIAN) {
+        const T g = noise_value(w.perlin[m.tex], m.w, rec.p);
+        return mk(g, g, g);
+    }
+    return m.albedo;
+}
+
+// Mixture sample + pdf + scattering pdf of a Lambertian / Isotropic hit (camera.rs:226-248).
+// Returns false when pdf_value <= 0 (the path ends with `emitted`).
+template <class T>
+bool b3_sample(const World<T> &w, PathRng &rng, const Record<T> &rec, bool iso, Vec3<T> &dir, T &pdf, T &spdf) {
+    const T inv4pi = T(1) / (T(4) * t_pi<T>());
+    if (rng.random_double<T>() < L(0.5)) {
+        dir = lights_random(w, rec.p, rng);
+    } else if (iso) {
+        dir = random_unit_vector<T>(rng);
+    } else {  // random_cosine_direction (vec3.rs:212-222)
+        const T r1 = rng.random_double<T>(), r2 = rng.random_double<T>();
+        const T phi = (T(2) * t_pi<T>()) * r1;
+        const T sr2 = std::sqrt(r2);
+        dir = onb_transform(rec.normal, mk(t_cos(phi) * sr2, t_sin3(phi) * sr2, std::sqrt(T(1) - r2)));
+    }
+    T mat_pdf;
+    if (iso) {
+        mat_pdf = inv4pi;
+    } else {
+        const T cosine = dot(unit_vector(dir), unit_vector(rec.normal));
+        mat_pdf = cosine <= T(0) ? T(0) : cosine / t_pi<T>();
+    }
+    pdf = L(0.5) * lights_pdf(w, rec.p, dir) + L(0.5) * mat_pdf;
+    if (pdf <= T(0)) return false;
+    if (iso) {
+        spdf = inv4pi;
+    } else {
+        const T cosine = dot(rec.normal, unit_vector(dir));
+        spdf = cosine < T(0) ? T(0) : cosine / t_pi<T>();
+    }
+    return true;
+}
+
+// Book-3 metal (no absorption test) / dielectric scatter.
+template <class T> void b3_skip_scatter(const Material<T> &m, PathRng &rng, Vec3<T> d_in, const Record<T> &rec,
+                                        Vec3<T> &att, Vec3<T> &dir) {
+    if (m.kind == RRT_MAT_METAL) {
+        const Vec3<T> r = random_unit_vector<T>(rng);
+        dir = unit_vector(reflect(d_in, rec.normal)) + m.fuzz * r;
+        att = m.albedo;
+        return;
+    }
+    att = mk(T(1), T(1), T(1));
+    const T ri = rec.front ? T(1) / m.ref_idx : m.ref_idx;
+    const Vec3<T> ud = unit_vector(d_in);
+    const T cos_theta = rmin(-dot(ud, rec.normal), T(1));
+    const T sin_theta = std::sqrt(T(1) - cos_theta * cos_theta);
+    const bool cannot = ri * sin_theta > T(1);
+    T r0 = (T(1) - ri) / (T(1) + ri);
+    r0 = r0 * r0;
+    const T x = T(1) - cos_theta;
+    const T x2 = x * x;
+    const T x4 = x2 * x2;
+    const T refl = r0 + (T(1) - r0) * (x * x4);
+    if (cannot || refl > rng.random_double<T>()) dir = reflect(ud, rec.normal);
+    else dir = refract(ud, rec.normal, ri);
+}
+
+// BOOKS, book 3: the_rest_of_your_life/camera.rs:184-254, recursive, f64.
+template <class T>
+Vec3<T> ray_color_b3_books(const World<T> &w, const Cam<T> &cam, PathRng &rng, Vec3<T> o, Vec3<T> d, T time,
+                           int depth, Tally &tl) {
+    if (depth <= 0) return mk(T(0), T(0), T(0));
+    tl.rays++;
+    Record<T> rec;
+    if (!world_hit(w, o, d, time, rng.s ^ ((uint64_t)(cam.max_depth - depth) << 32), rec, &tl.tests))
+        return cam.background;
+    const Material<T> &m = w.mats[rec.mat];
+    if (m.kind == RRT_MAT_DIFFUSE_LIGHT) return rec.front ? m.albedo : mk(T(0), T(0), T(0));
+    const int bounces = (int)cam.max_depth - depth;
+    if (m.kind == RRT_MAT_METAL || m.kind == RRT_MAT_DIELECTRIC) {
+        Vec3<T> att, dir;
+        b3_skip_scatter(m, rng, d, rec, att, dir);
+        if (bounces >= 5) {
+            const T p = rr_probability(att);
+            if (rng.random_double<T>() > p) return mk(T(0), T(0), T(0));
+            return att * ray_color_b3_books(w, cam, rng, rec.p, dir, time, depth - 1, tl) / p;
+        }
+        return att * ray_color_b3_books(w, cam, rng, rec.p, dir, time, depth - 1, tl);
+    }
+    const Vec3<T> att = b3_attenuation(w, m, rec);
+    const T rr = bounces >= 5 ? rr_probability(att) : T(1);
+    if (rr < T(1) && rng.random_double<T>() > rr) return mk(T(0), T(0), T(0));
+    Vec3<T> dir;
+    T pdf, spdf;
+    if (!b3_sample(w, rng, rec, m.kind == RRT_MAT_ISOTROPIC, dir, pdf, spdf)) return mk(T(0), T(0), T(0));
+    const Vec3<T> sample = ray_color_b3_books(w, cam, rng, rec.p, dir, time, depth - 1, tl);
+    return ((att * spdf) * sample) / (pdf * rr);
+}
+
+// TWIN, book 3: the kernel's shade_b3 (throughput form), f32.
+template <class T>
+Vec3<T> ray_color_b3_twin(const World<T> &w, const Cam<T> &cam, PathRng &rng, Vec3<T> o, Vec3<T> d, T time, Tally &tl,
+                          const KTree *kt = nullptr) {
+    Vec3<T> Tp = mk(T(1), T(1), T(1)), Lp = mk(T(0), T(0), T(0));
+    for (uint32_t k = 0; k < cam.max_depth; ++k) {
+        tl.rays++;
+        Record<T> rec;
+        if (!world_hit(w, o, d, time, rng.s ^ ((uint64_t)k << 32), rec, &tl.tests, kt)) return Lp + Tp * cam.background;
+        const Material<T> &m = w.mats[rec.mat];
+        if (m.kind == RRT_MAT_DIFFUSE_LIGHT) return rec.front ? Lp + Tp * m.albedo : Lp;
+        Vec3<T> att, dir;
+        if (m.kind == RRT_MAT_METAL || m.kind == RRT_MAT_DIELECTRIC) {
+            b3_skip_scatter(m, rng, d, rec, att, dir);
+            if (k >= 5u) {
+                const T p = rr_probability(att);
+                if (rng.random_double<T>() > p) return Lp;
+                Tp = (Tp * att) * (T(1) / p);
+            } else {
+                Tp = Tp * att;
+            }
+        } else {
+            att = b3_attenuation(w, m, rec);
+            T rr = T(1);
+            if (k >= 5u) {
+                rr = rr_probability(att);
+                if (rr < T(1) && rng.random_double<T>() > rr) return Lp;
+            }
+            T pdf, spdf;
+            if (!b3_sample(w, rng, rec, m.kind == RRT_MAT_ISOTROPIC, dir, pdf, spdf)) return Lp;
+            Tp = Tp * ((att * spdf) * (T(1) / (pdf * rr)));
+        }
+        o = rec.p;
+        d = dir;
+    }
+    return Lp;
+}
+
 // Camera::get_ray (camera.rs:152-169, the_next_week/camera.rs:148-163)
 template <class T>
-void get_ray(const Cam<T> &cam, PathRng &rng, uint32_t i, uint32_t j, Vec3<T> &o, Vec3<T> &d, T &time) {
-    const T ox = rng.random_double<T>() - L(0.5);
-    const T oy = rng.random_double<T>() - L(0.5);
+void get_ray(const Cam<T> &cam, PathRng &rng, uint32_t i, uint32_t j, uint32_t s, Vec3<T> &o, Vec3<T> &d, T &time) {
+    T ox, oy;
+    if (cam.flags & RRT_FLAG_BOOK3) {  // sample_square_stratified (the_rest_of_your_life/camera.rs:173-177)
+        const uint32_t sj = s / cam.sqrt_spp, si = s - sj * cam.sqrt_spp;
+        ox = (((T)si + rng.random_double<T>()) * cam.recip_sqrt_spp) - L(0.5);
+        oy = (((T)sj + rng.random_double<T>()) * cam.recip_sqrt_spp) - L(0.5);
+    } else {
+        ox = rng.random_double<T>() - L(0.5);
+        oy = rng.random_double<T>() - L(0.5);
+    }
     const Vec3<T> pixel_sample = cam.p00 + ((T)i + ox) * cam.du + ((T)j + oy) * cam.dv;
     if (cam.radius <= T(0)) {
         o = cam.center;
@@ -1136,9 +1392,15 @@ int render(const RrtCamera *c, const RrtSphere *s, uint32_t n, const RrtMaterial
                         PathRng rng{splitmix64(key + sidx)};
                         Vec3<T> o, d;
                         T time;
-                        get_ray(cam, rng, i, j, o, d, time);
-                        csum = csum + ((mode & 0xff) == 1 ? ray_color_books(w, cam, rng, o, d, time, (int)cam.max_depth, tl)
-                                                          : ray_color_twin(w, cam, rng, o, d, time, tl, kt));
+                        get_ray(cam, rng, i, j, sidx, o, d, time);
+                        Vec3<T> c;
+                        if (cam.flags & RRT_FLAG_BOOK3)
+                            c = (mode & 0xff) == 1 ? ray_color_b3_books(w, cam, rng, o, d, time, (int)cam.max_depth, tl)
+                                                   : ray_color_b3_twin(w, cam, rng, o, d, time, tl, kt);
+                        else
+                            c = (mode & 0xff) == 1 ? ray_color_books(w, cam, rng, o, d, time, (int)cam.max_depth, tl)
+                                                   : ray_color_twin(w, cam, rng, o, d, time, tl, kt);
+                        csum = csum + c;
                     }
                     sum = (c0 == s0) ? csum : sum + csum;
                 }
@@ -1402,6 +1664,10 @@ void oracle_acos_atan2_f32(float x, float y, float *acos_out, float *atan2_out) 
 // value / checker parity at points p[n][3] with table `pt` (f32 != 0: twin arithmetic).
 void oracle_sin_f32(uint32_t n, const float *x, float *out) {
     for (uint32_t i = 0; i < n; ++i) out[i] = cephes_sinf(x[i]);
+}
+
+void oracle_cos_f32(uint32_t n, const float *x, float *out) {
+    for (uint32_t i = 0; i < n; ++i) out[i] = cephes_cosf(x[i]);
 }
 
 void oracle_log_f32(uint32_t n, const float *x, float *out) {

@@ -37,6 +37,7 @@ assert CAMERA_DTYPE.itemsize == 144 and SPHERE_DTYPE.itemsize == 32 and MATERIAL
 MAT_LAMBERTIAN, MAT_METAL, MAT_DIELECTRIC, MAT_TEXTURED_LAMBERTIAN, MAT_DIFFUSE_LIGHT = range(5)
 FLAG_RAY_TIME = 0x1
 FLAG_QUIET = 0x2
+FLAG_BOOK3 = 0x4
 
 # Every symbol include/rrt_hip.h declares (checked by tests/test_abi.py).
 EXPORTED_SYMBOLS = (
@@ -68,6 +69,7 @@ EXPORTED_SYMBOLS = (
     "rrt_scene_create_ex",
     "rrt_build_bvh_ex",
     "rrt_build_next_week_scene",
+    "rrt_build_rest_of_your_life_scene",
     "rrt_device_count",
 )
 
@@ -86,6 +88,9 @@ QUAD_DTYPE = np.dtype([("q", "<f4", 4), ("u", "<f4", 4), ("v", "<f4", 4), ("mate
                        ("_pad", "<u4", 3)])
 
 
+# == RrtLight (include/rrt_hip.h): book-3 MIS light, kind 0 quad (a = q, u, v) / 1 sphere (a = c, r); 64 B
+LIGHT_DTYPE = np.dtype([("kind", "<u4"), ("_pad", "<u4", 3), ("a", "<f4", 4), ("u", "<f4", 4), ("v", "<f4", 4)])
+
 # == RrtMedium (include/rrt_hip.h): boundary sphere or quad range, phase material, density; 48 B
 MEDIUM_DTYPE = np.dtype([("sphere", "<f4", 4), ("boundary_kind", "<u4"), ("first", "<u4"), ("count", "<u4"),
                          ("material_index", "<u4"), ("density", "<f4"), ("_pad", "<u4", 3)])
@@ -94,16 +99,16 @@ MEDIUM_DTYPE = np.dtype([("sphere", "<f4", 4), ("boundary_kind", "<u4"), ("first
 class RrtSceneExt(ctypes.Structure):
     _fields_ = [("sphere_motion", c_void_p), ("perlin", c_void_p), ("n_perlin", c_uint32), ("n_quads", c_uint32),
                 ("quads", c_void_p), ("media", c_void_p), ("n_media", c_uint32), ("n_boundary_quads", c_uint32),
-                ("boundary_quads", c_void_p)]
+                ("boundary_quads", c_void_p), ("lights", c_void_p), ("n_lights", c_uint32), ("_pad", c_uint32)]
 
 
-class RrtNextWeekScene(ctypes.Structure):
+class RrtBookScene(ctypes.Structure):
     _fields_ = [("camera", ctypes.c_uint8 * 144), ("spheres", c_void_p), ("sphere_motion", c_void_p),
                 ("materials", c_void_p), ("quads", c_void_p), ("perlin", c_void_p), ("media", c_void_p),
-                ("boundary_quads", c_void_p)] + [
+                ("boundary_quads", c_void_p), ("lights", c_void_p)] + [
         (f, c_uint32) for f in ("sphere_cap", "n_spheres", "material_cap", "n_materials", "quad_cap", "n_quads",
                                 "perlin_cap", "n_perlin", "media_cap", "n_media", "boundary_quad_cap",
-                                "n_boundary_quads", "uses_texture0", "_pad")]
+                                "n_boundary_quads", "light_cap", "n_lights", "uses_texture0", "flags")]
 
 
 class RrtOverrides(ctypes.Structure):
@@ -223,6 +228,7 @@ def load() -> ctypes.CDLL:
         "rrt_scene_create_ex": (c_int32, [P, P, c_uint32, P, c_uint32, P, c_uint32, P, c_uint32, c_int32, P]),
         "rrt_build_bvh_ex": (c_int32, [P, c_uint32, P, c_uint32, c_uint32, P, c_size_t, P, P]),
         "rrt_build_next_week_scene": (c_int32, [c_int32, P, c_uint64, P]),
+        "rrt_build_rest_of_your_life_scene": (c_int32, [P, c_uint64, P]),
         "rrt_device_count": (c_int32, [P]),
     }
     experiment = "RRT_LIB_PATH" in os.environ  # A/B of older builds: tolerate symbols they lack

@@ -105,6 +105,8 @@ int main(int argc, char **argv) {
     }
     const bool book1 = book == "inoneweekend" || book == "oneweekend" || book == "weekend";
     const bool book2 = book == "thenextweek" || book == "nextweek" || book == "next";  // main.rs:89
+    const bool book3 = book == "therestofyourlife" || book == "restofyourlife" || book == "rest" ||
+                       book == "restoflife";  // main.rs:90-92
     const int scene = positional.size() > 1 ? std::atoi(positional[1].c_str()) : 0;  // main.rs:55
     if (book2 && !(scene >= 1 && scene <= 8 && scene != 3)) {
         std::fprintf(stderr, "HIP backend supports the_next_week scenes 1 (bouncing_spheres), 2 (checkered_spheres), "
@@ -113,8 +115,9 @@ int main(int argc, char **argv) {
                              "use the Python API.\n");
         return 2;
     }
-    if (!book1 && !book2) {  // main.rs:59-70
-        std::fprintf(stderr, "HIP backend supports in_one_weekend and the_next_week scenes 1, 2, 4-8 only.\n");
+    if (!book1 && !book2 && !book3) {  // main.rs:59-70, 93-97
+        std::fprintf(stderr, "HIP backend supports in_one_weekend, the_next_week scenes 1, 2, 4-8 and "
+                             "the_rest_of_your_life.\n");
         return 2;
     }
 
@@ -124,6 +127,7 @@ int main(int argc, char **argv) {
     std::vector<RrtMaterial> materials;
     std::vector<RrtQuad> quads, boundary_quads;
     std::vector<RrtMedium> media;
+    std::vector<RrtLight> lights;
     std::vector<float> motion;
     std::vector<RrtPerlin> perlin;
     uint32_t flags = 0;
@@ -141,8 +145,11 @@ int main(int argc, char **argv) {
         n_mat = n;
     } else {
         const uint64_t s2 = seed_set ? seed : 0xB00C0002ull;
-        RrtNextWeekScene nw{};
-        if (rrt_build_next_week_scene(scene, &ov, s2, &nw)) {  // sizing pass
+        auto build = [&](RrtBookScene *o) {
+            return book3 ? rrt_build_rest_of_your_life_scene(&ov, s2, o) : rrt_build_next_week_scene(scene, &ov, s2, o);
+        };
+        RrtBookScene nw{};
+        if (build(&nw)) {  // sizing pass
             std::fprintf(stderr, "HIP render failed: %s\n", rrt_hip_last_error());
             return 1;
         }
@@ -153,19 +160,21 @@ int main(int argc, char **argv) {
         perlin.resize(nw.n_perlin);
         media.resize(nw.n_media);
         boundary_quads.resize(nw.n_boundary_quads);
+        lights.resize(nw.n_lights);
+        nw.lights = lights.data(), nw.light_cap = nw.n_lights;
         nw.spheres = spheres.data(), nw.sphere_cap = nw.n_spheres, nw.sphere_motion = motion.data();
         nw.materials = materials.data(), nw.material_cap = nw.n_materials;
         nw.quads = quads.data(), nw.quad_cap = nw.n_quads;
         nw.perlin = perlin.data(), nw.perlin_cap = nw.n_perlin;
         nw.media = media.data(), nw.media_cap = nw.n_media;
         nw.boundary_quads = boundary_quads.data(), nw.boundary_quad_cap = nw.n_boundary_quads;
-        if (rrt_build_next_week_scene(scene, &ov, s2, &nw)) {
+        if (build(&nw)) {
             std::fprintf(stderr, "HIP render failed: %s\n", rrt_hip_last_error());
             return 1;
         }
         cam = nw.camera;
         n = nw.n_spheres, n_mat = nw.n_materials, n_quads = nw.n_quads, n_perlin = nw.n_perlin;
-        flags = RRT_FLAG_RAY_TIME;  // book-2 camera (the_next_week/camera.rs:160)
+        flags = nw.flags;  // RAY_TIME (book-2/3 cameras), BOOK3 (MIS integrator)
     }
     RrtSceneExt ext{};
     ext.sphere_motion = motion.empty() ? nullptr : motion.data();
@@ -177,13 +186,15 @@ int main(int argc, char **argv) {
     ext.n_media = (uint32_t)media.size();
     ext.boundary_quads = boundary_quads.empty() ? nullptr : boundary_quads.data();
     ext.n_boundary_quads = (uint32_t)boundary_quads.size();
+    ext.lights = lights.empty() ? nullptr : lights.data();
+    ext.n_lights = (uint32_t)lights.size();
     const uint32_t w = (uint32_t)cam.params_f[1], h = (uint32_t)cam.params_f[2];
     const uint32_t spp = (uint32_t)(cam.params_f[3] < 1.0f ? 1.0f : cam.params_f[3]);
     const auto t0 = std::chrono::steady_clock::now();
     std::vector<float> accum;
     std::vector<uint8_t> rgb8;
     int rc;
-    if (book2 || (host_quantise && !p6)) {  // float accum -> render_io on the host (book 2: rrt_hip_render_ex)
+    if (!book1 || (host_quantise && !p6)) {  // float accum -> render_io on the host (book 2: rrt_hip_render_ex)
         accum.resize((size_t)w * h * 4);
         rc = rrt_hip_render_ex(&cam, spheres.data(), n, materials.data(), n_mat, nullptr, 0, &ext, spp, gpus, flags,
                                accum.data());

@@ -530,12 +530,15 @@ struct ExtView {
     uint32_t n_media = 0;
     const RrtQuad *bquads = nullptr;
     uint32_t n_bquads = 0;
+    const RrtLight *lights = nullptr;
+    uint32_t n_lights = 0;
     explicit ExtView(const RrtSceneExt *e) {
         if (!e) return;
         motion = e->sphere_motion;
         if (e->quads) quads = e->quads, n_quads = e->n_quads;
         if (e->media) media = e->media, n_media = e->n_media;
         if (e->boundary_quads) bquads = e->boundary_quads, n_bquads = e->n_boundary_quads;
+        if (e->lights) lights = e->lights, n_lights = e->n_lights;
     }
 };
 
@@ -606,6 +609,7 @@ struct RrtScene {
     rrt::GPerlin *d_perlin = nullptr;
     rrt::GQuad *d_quads = nullptr;
     rrt::GMedium *d_media = nullptr;
+    rrt::GLight *d_lights = nullptr;
     uint8_t *d_tex_pool = nullptr;
     rrt::GTexture *d_texs = nullptr;
     unsigned long long *d_counters = nullptr;       // 5 x u64, render launches
@@ -629,6 +633,7 @@ void free_scene(RrtScene *s) {
     (void)hipFree(s->d_perlin);
     (void)hipFree(s->d_quads);
     (void)hipFree(s->d_media);
+    (void)hipFree(s->d_lights);
     (void)hipFree(s->d_tex_pool);
     (void)hipFree(s->d_texs);
     (void)hipFree(s->d_counters);
@@ -663,7 +668,11 @@ int check_tile_shape(const RrtTile *t) {
 
 int check_tile(const RrtScene *s, const RrtTile *t) {
     if (!s) return fail(RRT_E_INVALID, "null scene");
-    return check_tile_shape(t);
+    if (int rc = check_tile_shape(t)) return rc;
+    const uint32_t sq = s->base.sqrt_spp;
+    if (sq && (uint64_t)t->sample_end > (uint64_t)sq * sq)  // book 3: s = s_j * sqrt_spp + s_i
+        return fail(RRT_E_INVALID, "RRT_FLAG_BOOK3: sample_end exceeds sqrt_spp^2 = " + std::to_string(sq * sq));
+    return RRT_OK;
 }
 
 int fill_params(RrtScene *s, const RrtTile *t, float *d_accum, rrt::KParams &p) {
@@ -761,7 +770,20 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
         return fail(RRT_E_INVALID, "moving spheres need RRT_FLAG_RAY_TIME (rays carry the camera's time draw)");
     // Book-2 scenes (moving spheres or checker / noise materials) take the kernel variant that
     // supports them; it reads a motion row per sphere (zero for static spheres).
-    bool book2 = has_motion || n_quads > 0 || n_media > 0;
+    const bool book3 = (flags & RRT_FLAG_BOOK3) != 0;
+    uint32_t sqrt_spp = 0;
+    if (book3) {
+        if (!(flags & RRT_FLAG_RAY_TIME)) return fail(RRT_E_INVALID, "RRT_FLAG_BOOK3 needs RRT_FLAG_RAY_TIME");
+        if (ex.n_lights == 0) return fail(RRT_E_INVALID, "RRT_FLAG_BOOK3 needs a non-empty RrtSceneExt.lights");
+        const uint32_t spp = (uint32_t)std::max(cam->params_f[3], 1.0f);
+        sqrt_spp = (uint32_t)std::sqrt((double)spp);
+        if (sqrt_spp * sqrt_spp != spp)
+            return fail(RRT_E_INVALID, "RRT_FLAG_BOOK3 samples_per_pixel must be a square (sqrt_spp^2, camera.rs:115-117)");
+        for (uint32_t l = 0; l < ex.n_lights; ++l)
+            if (ex.lights[l].kind > RRT_LIGHT_SPHERE)
+                return fail(RRT_E_INVALID, "light " + std::to_string(l) + ": unknown kind");
+    }
+    bool book2 = has_motion || n_quads > 0 || n_media > 0 || book3;
     for (uint32_t i = 0; i < n_materials && materials; ++i)
         book2 = book2 || materials[i].kind == RRT_MAT_CHECKER_LAMBERTIAN || materials[i].kind == RRT_MAT_NOISE_LAMBERTIAN ||
                 materials[i].kind == RRT_MAT_ISOTROPIC;
@@ -793,7 +815,8 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
     bvh_defaults(width, max_leaf);
     if (book2) width = 2;  // the book-2 kernel variants are BVH2 only
     std::vector<uint32_t> order;
-    if ((uint64_t)n_spheres + n_quads + n_media >= (1u << 24) || (uint64_t)n_quads + ex.n_bquads >= (1u << 24))
+    if ((uint64_t)n_spheres + n_quads + n_media >= (1u << 24) ||
+        (uint64_t)n_quads + ex.n_bquads + ex.n_lights >= (1u << 24))
         return fail(RRT_E_INVALID, ">= 2^24 primitives or quads");
     if (!has_motion) ex.motion = nullptr;
     const FlatBvh fb = build_bvh(spheres, n_spheres, ex, width, max_leaf, order);
@@ -817,9 +840,28 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
     // 32-B record at the primitive's index (no dependent material-index fetch).
     // Quads with their derived plane (quad.rs:21-37 in f64: n = cross(u, v), normal = n * (1/|n|),
     // D = dot(normal, q), w = n * (1/dot(n, n)); Vec3 / f64 is `(1/rhs) * v`, vec3.rs:142-148).
-    std::vector<rrt::GQuad> gquads(n_quads + (size_t)ex.n_bquads);
+    // GQuad array: the scene's quads, media boundary quads, book-3 light quads
+    std::vector<RrtQuad> light_quads;
+    std::vector<rrt::GLight> glights(book3 ? ex.n_lights : 0);
+    for (uint32_t l = 0; l < glights.size(); ++l) {
+        const RrtLight &L = ex.lights[l];
+        rrt::GLight &g = glights[l];
+        g.kind = L.kind;
+        g.sphere = make_float4(L.a[0], L.a[1], L.a[2], std::max(L.a[3], 0.0f));
+        if (L.kind == RRT_LIGHT_QUAD) {
+            RrtQuad q{};
+            for (int i = 0; i < 3; ++i) q.q[i] = L.a[i], q.u[i] = L.u[i], q.v[i] = L.v[i];
+            g.quad = n_quads + ex.n_bquads + (uint32_t)light_quads.size();
+            const D3 n = cross(d3(L.u[0], L.u[1], L.u[2]), d3(L.v[0], L.v[1], L.v[2]));
+            g.area = (float)std::sqrt(n.x * n.x + n.y * n.y + n.z * n.z);  // quad.rs:28 area = |n|
+            light_quads.push_back(q);
+        }
+    }
+    std::vector<rrt::GQuad> gquads(n_quads + (size_t)ex.n_bquads + light_quads.size());
     for (uint32_t j = 0; j < gquads.size(); ++j) {
-        const RrtQuad &qd = j < n_quads ? quads[j] : ex.bquads[j - n_quads];
+        const RrtQuad &qd = j < n_quads ? quads[j]
+                            : j < n_quads + ex.n_bquads ? ex.bquads[j - n_quads]
+                                                        : light_quads[j - n_quads - ex.n_bquads];
         const D3 q = d3(qd.q[0], qd.q[1], qd.q[2]), u = d3(qd.u[0], qd.u[1], qd.u[2]), v = d3(qd.v[0], qd.v[1], qd.v[2]);
         const D3 n = cross(u, v);
         const double nn = n.x * n.x + n.y * n.y + n.z * n.z;
@@ -902,6 +944,7 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
         if (n_perlin && (rc = upload(&s->d_perlin, perlin.data(), perlin.size(), "Perlin tables"))) break;
         if (!gquads.empty() && (rc = upload(&s->d_quads, gquads.data(), gquads.size(), "quads"))) break;
         if (n_media && (rc = upload(&s->d_media, gmedia.data(), gmedia.size(), "media"))) break;
+        if (!glights.empty() && (rc = upload(&s->d_lights, glights.data(), glights.size(), "lights"))) break;
         if ((rc = upload(&s->d_tex_pool, tex_pool.data(), tex_pool.size(), "textures"))) break;
         if ((rc = upload(&s->d_texs, texs.data(), texs.size(), "texture table"))) break;
         if (hipMalloc((void **)&s->d_counters, 8 * sizeof(unsigned long long)) != hipSuccess ||
@@ -932,6 +975,10 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
     p.n_quads = n_quads;
     p.media = s->d_media;
     p.n_media = n_media;
+    p.lights = s->d_lights;
+    p.n_lights = (uint32_t)glights.size();
+    p.sqrt_spp = sqrt_spp;
+    p.recip_sqrt_spp = sqrt_spp ? (float)(1.0 / (double)sqrt_spp) : 0.0f;  // camera.rs:117
     p.tex_pool = s->d_tex_pool;
     p.texs = s->d_texs;
     p.counters = s->d_counters;
@@ -1419,12 +1466,10 @@ int32_t rrt_build_in_one_weekend_scene(const RrtOverrides *ov, uint64_t seed, in
 // draws, in the same order, come from SmallRng(seed): random_double() = gen_range(0.0..1.0),
 // random_double_range = gen_range(min..max), random_int(min,max) = random_double_range(min,
 // max+1) as i32 (rtweekend.rs:17-30). Parity unpinned (entropy RNG).
-int32_t rrt_build_next_week_scene(int32_t scene, const RrtOverrides *ov, uint64_t seed, RrtNextWeekScene *out) {
+// Book-2 scenes 1..10 and the book-3 scene (kBook3Scene), flattened into RrtBookScene.
+static const int32_t kBook3Scene = 100;
+static int32_t build_book_scene(int32_t scene, const RrtOverrides *ov, uint64_t seed, RrtBookScene *out) {
     if (!out) return fail(RRT_E_INVALID, "null output");
-    if (scene < 1 || scene > 10)
-        return fail(RRT_E_INVALID, "book-2 scene must be 1 bouncing_spheres, 2 checkered_spheres, 3 earth, "
-                                   "4 perlin_spheres, 5 quads, 6 simple_light, 7 cornell_box, 8 cornell_smoke, "
-                                   "9 final_scene(800, 10000, 40), 10 final_scene(400, 250, 4)");
     // Camera (the_next_week/mod.rs:137-150, 177-190, 203-216, 237-250)
     double aspect_ratio = 16.0 / 9.0;
     int32_t image_width = 400, samples_per_pixel = 100, max_depth = 50;
@@ -1443,12 +1488,12 @@ int32_t rrt_build_next_week_scene(int32_t scene, const RrtOverrides *ov, uint64_
         lookfrom[0] = 26.0, lookfrom[1] = 3.0, lookfrom[2] = 6.0;
         lookat[1] = 2.0;
         background[0] = background[1] = background[2] = 0.0;
-    } else if (scene == 7 || scene == 8) {  // mod.rs:412-423, 490-501
-        aspect_ratio = 1.0, image_width = 600, samples_per_pixel = 200, vfov = 40.0;
+    } else if (scene == 7 || scene == 8 || scene == kBook3Scene) {  // mod.rs:412-423, 490-501; book 3 mod.rs:146-158
+        aspect_ratio = 1.0, image_width = 600, samples_per_pixel = scene == kBook3Scene ? 100 : 200, vfov = 40.0;
         lookfrom[0] = 278.0, lookfrom[1] = 278.0, lookfrom[2] = -800.0;
         lookat[0] = 278.0, lookat[1] = 278.0, lookat[2] = 0.0;
         background[0] = background[1] = background[2] = 0.0;
-    } else if (scene >= 9) {  // final_scene (mod.rs:570-585), main.rs:78-79 arguments
+    } else if (scene == 9 || scene == 10) {  // final_scene (mod.rs:570-585), main.rs:78-79 arguments
         aspect_ratio = 1.0, vfov = 40.0;
         image_width = scene == 9 ? 800 : 400;
         samples_per_pixel = scene == 9 ? 10000 : 250;
@@ -1469,6 +1514,7 @@ int32_t rrt_build_next_week_scene(int32_t scene, const RrtOverrides *ov, uint64_
     std::vector<RrtPerlin> tables;
     std::vector<RrtQuad> qds, bqs;
     std::vector<RrtMedium> meds;
+    std::vector<RrtLight> lights;
     uint32_t uses_texture0 = 0;
     auto bits = [](float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; };
     auto add_material = [&](uint32_t kind, float r, float g, float b, float w, float ref_idx, uint32_t p0, uint32_t p1) {
@@ -1654,6 +1700,27 @@ int32_t rrt_build_next_week_scene(int32_t scene, const RrtOverrides *ov, uint64_
         add_quad(d3(0, 0, 555), d3(555, 0, 0), d3(0, 555, 0), white, ident);
         box_medium(d3(0, 0, 0), d3(165, 330, 165), rotate_translate(15.0, d3(265, 0, 295)), 0.01, d3(0, 0, 0));
         box_medium(d3(0, 0, 0), d3(165, 165, 165), rotate_translate(-18.0, d3(130, 0, 65)), 0.01, d3(1, 1, 1));
+    } else if (scene == kBook3Scene) {  // the_rest_of_your_life/mod.rs:69-143
+        const uint32_t red = lambertian(0.65f, 0.05f, 0.05f), white = lambertian(0.73f, 0.73f, 0.73f);
+        const uint32_t green = lambertian(0.12f, 0.45f, 0.15f), light = diffuse_light(15.0f);
+        add_quad(d3(555, 0, 0), d3(0, 0, 555), d3(0, 555, 0), green, ident);
+        add_quad(d3(0, 0, 555), d3(0, 0, -555), d3(0, 555, 0), red, ident);
+        add_quad(d3(0, 555, 0), d3(555, 0, 0), d3(0, 0, 555), white, ident);
+        add_quad(d3(0, 0, 555), d3(555, 0, 0), d3(0, 0, -555), white, ident);
+        add_quad(d3(555, 0, 555), d3(-555, 0, 0), d3(0, 555, 0), white, ident);
+        add_quad(d3(213, 554, 227), d3(130, 0, 0), d3(0, 0, 105), light, ident);
+        make_box(d3(0, 0, 0), d3(165, 330, 165), white, rotate_translate(15.0, d3(265, 0, 295)));
+        add_sphere(d3(190, 90, 190), 90.0, add_material(RRT_MAT_DIELECTRIC, 1, 1, 1, 0, 1.5f, 0, 0), still);
+        RrtLight lq{};  // lights: the light quad (reversed edges) and the glass sphere
+        lq.kind = RRT_LIGHT_QUAD;
+        put4(lq.a, 343.0f, 554.0f, 332.0f, 0.0f);
+        put4(lq.u, -130.0f, 0.0f, 0.0f, 0.0f);
+        put4(lq.v, 0.0f, 0.0f, -105.0f, 0.0f);
+        lights.push_back(lq);
+        RrtLight ls{};
+        ls.kind = RRT_LIGHT_SPHERE;
+        put4(ls.a, 190.0f, 90.0f, 190.0f, 90.0f);
+        lights.push_back(ls);
     } else {  // final_scene (mod.rs:503-587)
         const uint32_t ground = lambertian(0.48f, 0.83f, 0.53f);
         for (int i = 0; i < 20; ++i)
@@ -1686,14 +1753,20 @@ int32_t rrt_build_next_week_scene(int32_t scene, const RrtOverrides *ov, uint64_
         }
     }
     const uint32_t sample_seed = rng.next_u32();
-    RrtNextWeekScene &o = *out;
+    if (scene == kBook3Scene) {  // Camera::initialize: sqrt_spp^2 stratified samples (camera.rs:115-117)
+        const int32_t sq = (int32_t)std::sqrt((double)std::max(samples_per_pixel, 1));
+        samples_per_pixel = sq * sq;
+    }
+    RrtBookScene &o = *out;
     o.n_spheres = (uint32_t)sph.size();
     o.n_materials = (uint32_t)mat.size();
     o.n_quads = (uint32_t)qds.size();
     o.n_perlin = (uint32_t)tables.size();
     o.n_media = (uint32_t)meds.size();
     o.n_boundary_quads = (uint32_t)bqs.size();
+    o.n_lights = (uint32_t)lights.size();
     o.uses_texture0 = uses_texture0;
+    o.flags = RRT_FLAG_RAY_TIME | (scene == kBook3Scene ? RRT_FLAG_BOOK3 : 0u);
     int rc = rrt_make_camera(aspect_ratio, image_width, samples_per_pixel, max_depth, vfov, lookfrom, lookat, vup,
                              defocus_angle, focus_dist, has_bg ? background : nullptr, sample_seed,
                              (uint32_t)sph.size(), &o.camera);
@@ -1709,11 +1782,24 @@ int32_t rrt_build_next_week_scene(int32_t scene, const RrtOverrides *ov, uint64_
     if ((rc = put(o.spheres, o.sphere_cap, sph, "sphere")) || (rc = put(o.materials, o.material_cap, mat, "material")) ||
         (rc = put(o.quads, o.quad_cap, qds, "quad")) || (rc = put(o.perlin, o.perlin_cap, tables, "perlin")) ||
         (rc = put(o.media, o.media_cap, meds, "media")) ||
-        (rc = put(o.boundary_quads, o.boundary_quad_cap, bqs, "boundary_quad")))
+        (rc = put(o.boundary_quads, o.boundary_quad_cap, bqs, "boundary_quad")) ||
+        (rc = put(o.lights, o.light_cap, lights, "light")))
         return rc;
     if (o.sphere_motion && o.sphere_cap >= sph.size() && !mot.empty())
         std::memcpy(o.sphere_motion, mot.data(), mot.size() * sizeof(float));
     return RRT_OK;
+}
+
+int32_t rrt_build_next_week_scene(int32_t scene, const RrtOverrides *ov, uint64_t seed, RrtBookScene *out) {
+    if (scene < 1 || scene > 10)
+        return fail(RRT_E_INVALID, "book-2 scene must be 1 bouncing_spheres, 2 checkered_spheres, 3 earth, "
+                                   "4 perlin_spheres, 5 quads, 6 simple_light, 7 cornell_box, 8 cornell_smoke, "
+                                   "9 final_scene(800, 10000, 40), 10 final_scene(400, 250, 4)");
+    return build_book_scene(scene, ov, seed, out);
+}
+
+int32_t rrt_build_rest_of_your_life_scene(const RrtOverrides *ov, uint64_t seed, RrtBookScene *out) {
+    return build_book_scene(kBook3Scene, ov, seed, out);
 }
 
 // ---- render_io.rs:3-31 -------------------------------------------------------------------

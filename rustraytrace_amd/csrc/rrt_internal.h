@@ -69,6 +69,16 @@ struct alignas(16) GMedium {
     float neg_inv_density;
 };
 
+// Book-3 MIS light: sphere (center xyz, radius w) or quad (index into KParams.quads, its area
+// |u x v| in f64 rounded to f32). 32 B.
+struct alignas(16) GLight {
+    float4 sphere;
+    uint32_t kind;  // 0 quad, 1 sphere
+    uint32_t quad;
+    float area;
+    uint32_t _pad;
+};
+
 struct GTexture {
     int32_t offset;  // byte offset into the texture pool
     int32_t width;
@@ -86,6 +96,7 @@ struct KParams {
     const GQuad *quads;          // quads, then media boundary quads; a quad's leaf-order primitive record is
                                  // (0, 0, 0, -(1 + index)), a medium's (0, 0, 0, -(1 + n_quads + index))
     const GMedium *media;
+    const GLight *lights;        // book 3: the MIS light list
     const uint8_t *tex_pool;
     const GTexture *texs;
     float4 *accum;               // tile-local rows * width
@@ -122,6 +133,9 @@ struct KParams {
     uint32_t n_perlin;
     uint32_t n_quads;       // the scene's quads (boundary quads follow them)
     uint32_t n_media;
+    uint32_t n_lights;
+    uint32_t sqrt_spp;      // book 3: stratified camera samples (sqrt_spp^2 per pixel)
+    float recip_sqrt_spp;   // 1/sqrt_spp in f64, rounded
     uint32_t stack_depth;   // entries needed (BVH depth + 1)
     uint32_t scene_in_lds;  // stage nodes + spheres + their materials in LDS per block
     uint32_t trav_frac;     // leave the traversal loop when <= live*trav_frac/256 lanes still traverse

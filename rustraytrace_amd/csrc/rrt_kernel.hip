@@ -235,7 +235,7 @@ __device__ __forceinline__ float div_by_a(float n, const RayK &rk) {
 // center at the ray's time, center1 + time * (center2 - center1) (the_next_week/sphere.rs:44:
 // Ray::at; static book-2 spheres carry a zero motion).
 // kBook2: 0 = book-1 scenes, 1 = book 2 (motion, procedural textures), 2 = book 2 with quads,
-// 3 = book 2 with quads and media
+// 3 = book 2 with quads and media, 4 = book 3 (all of book 2 + the MIS integrator)
 template <int kBook2>
 struct Prims {
     const float4 *cr;
@@ -246,7 +246,7 @@ struct Prims {
     uint32_t n_quads;
     uint64_t seg;  // the path's RNG state at this segment ^ (bounce << 32): key of the media draws
     static constexpr bool kHasQuads = kBook2 >= 2;
-    static constexpr bool kHasMedia = kBook2 == 3;
+    static constexpr bool kHasMedia = kBook2 >= 3;
     __device__ __forceinline__ float4 at(int i) const {
         float4 c = cr[i];
         if constexpr (kBook2) {
@@ -620,9 +620,17 @@ struct PathState {
 };
 
 // Camera::get_ray (camera.rs:152-180) for global pixel (x, y) and the path's RNG.
-__device__ __forceinline__ void camera_ray(const KParams &P, uint32_t x, uint32_t y, PathState &ps) {
-    const float ox = rnd(ps.rng) - 0.5f;
-    const float oy = rnd(ps.rng) - 0.5f;
+template <bool kStrat>
+__device__ __forceinline__ void camera_ray(const KParams &P, uint32_t x, uint32_t y, uint32_t s, PathState &ps) {
+    float ox, oy;
+    if constexpr (kStrat) {  // sample_square_stratified (the_rest_of_your_life/camera.rs:173-177)
+        const uint32_t sj = s / P.sqrt_spp, si = s - sj * P.sqrt_spp;
+        ox = (((float)si + rnd(ps.rng)) * P.recip_sqrt_spp) - 0.5f;
+        oy = (((float)sj + rnd(ps.rng)) * P.recip_sqrt_spp) - 0.5f;
+    } else {
+        ox = rnd(ps.rng) - 0.5f;
+        oy = rnd(ps.rng) - 0.5f;
+    }
     const float fi = (float)x + ox;
     const float fj = (float)y + oy;
     const V3 sample = v3(P.p00[0] + P.du[0] * fi + P.dv[0] * fj,
@@ -680,6 +688,32 @@ __device__ __forceinline__ float rrt_sinf(float xx) {
     } else {
         y = ((-1.9515295891e-4f * z + 8.3321608736e-3f) * z - 1.6666654611e-1f) * z * x;
         y = y + x;
+    }
+    return sign < 0.0f ? -y : y;
+}
+
+// Cephes cosf: rrt_sinf's reduction, the octant's sign and polynomial for cos.
+__device__ __forceinline__ float rrt_cosf(float xx) {
+    float x = xx < 0.0f ? -xx : xx;
+    if (x > 16777215.0f) return 0.0f;
+    if (!(x == x)) return xx;
+    float sign = 1.0f;
+    int j = (int)(1.27323954473516f * x);
+    float y = (float)j;
+    if (j & 1) { j += 1; y += 1.0f; }
+    j &= 7;
+    if (j > 3) { j -= 4; sign = -sign; }
+    if (j > 1) sign = -sign;
+    if (x > 8192.0f) x = x - y * 0.7853981633974483096f;
+    else x = ((x - y * 0.78515625f) - y * 2.4187564849853515625e-4f) - y * 3.77489497744594108e-8f;
+    const float z = x * x;
+    if (j == 1 || j == 2) {
+        y = ((-1.9515295891e-4f * z + 8.3321608736e-3f) * z - 1.6666654611e-1f) * z * x;
+        y = y + x;
+    } else {
+        y = ((2.443315711809948e-5f * z - 1.388731625493765e-3f) * z + 4.166664568298827e-2f) * z * z;
+        y = y - 0.5f * z;
+        y = y + 1.0f;
     }
     return sign < 0.0f ? -y : y;
 }
@@ -865,6 +899,210 @@ __device__ __forceinline__ bool shade(const KParams &P, const PR &prims, const G
     return false;
 }
 
+// ---- book 3 (the_rest_of_your_life): pdfs, light sampling, the MIS shading step ---------------
+// Onb::new(n).transform(a) (onb.rs:8-33): w = unit(n), a helper axis, v = unit(w x axis), u = w x v.
+__device__ __forceinline__ V3 onb_transform(V3 n, V3 a) {
+    const V3 w = unit(n);
+    const V3 ax = (__builtin_fabsf(w.x) > 0.9f) ? v3(0.0f, 1.0f, 0.0f) : v3(1.0f, 0.0f, 0.0f);
+    const V3 v = unit(cross(w, ax));
+    const V3 u = cross(w, v);
+    return v3(a.x * u.x + a.y * v.x + a.z * w.x, a.x * u.y + a.y * v.y + a.z * w.y, a.x * u.z + a.y * v.z + a.z * w.z);
+}
+
+// Sphere::hit's root over (tmin, inf) for a static sphere (IEEE division: the light-pdf path).
+__device__ __forceinline__ bool sphere_root(float4 c, V3 o, V3 d, float tmin) {
+    const V3 oc = v3(c.x - o.x, c.y - o.y, c.z - o.z);
+    const float a = dot(d, d);
+    const float h = dot(d, oc);
+    const float cc = dot(oc, oc) - c.w * c.w;
+    const float disc = h * h - a * cc;
+    if (disc < 0.0f) return false;
+    const float sq = __builtin_sqrtf(disc);
+    const float inf = __builtin_inff();
+    float root = (h - sq) / a;
+    if (!(tmin < root && root < inf)) {
+        root = (h + sq) / a;
+        if (!(tmin < root && root < inf)) return false;
+    }
+    return true;
+}
+
+// HittableList::pdf_value over the light list (hittable_list.rs:60-69): sum of (1/n) * pdf_i,
+// Quad::pdf_value (quad.rs:93-102), Sphere::pdf_value (sphere.rs:102-115).
+__device__ __forceinline__ float lights_pdf(const KParams &P, V3 o, V3 d) {
+    const float weight = 1.0f / (float)P.n_lights;
+    float sum = 0.0f;
+    for (uint32_t l = 0; l < P.n_lights; ++l) {
+        const GLight L = P.lights[l];
+        float pdf = 0.0f;
+        if (L.kind == 0u) {
+            const GQuad g = P.quads[L.quad];
+            float t;
+            if (quad_hit(g, o, d, 0.001f, __builtin_inff(), t)) {
+                const float len2 = dot(d, d);
+                const float dist2 = t * t * len2;
+                const float cosine = __builtin_fabsf(dot(d, v3(g.n.x, g.n.y, g.n.z))) / __builtin_sqrtf(len2);
+                pdf = dist2 / (cosine * L.area);
+            }
+        } else if (sphere_root(L.sphere, o, d, 0.001f)) {
+            const V3 oc = v3(L.sphere.x - o.x, L.sphere.y - o.y, L.sphere.z - o.z);
+            const float cos_max = __builtin_sqrtf(1.0f - L.sphere.w * L.sphere.w / dot(oc, oc));
+            pdf = 1.0f / ((2.0f * kPi) * (1.0f - cos_max));
+        }
+        sum = sum + weight * pdf;
+    }
+    return sum;
+}
+
+// HittableList::random (hittable_list.rs:71-75): random_int(0, n-1), then Quad::random
+// (quad.rs:104-107) or Sphere::random + random_to_sphere (sphere.rs:55-66, 117-122).
+__device__ __forceinline__ V3 lights_random(const KParams &P, V3 o, uint64_t &rng) {
+    const int idx = (int)rnd_range(rng, 0.0f, (float)P.n_lights);
+    const GLight L = P.lights[idx];
+    if (L.kind == 0u) {
+        const GQuad g = P.quads[L.quad];
+        const float r1 = rnd(rng);
+        const V3 a = v3(g.q.x + r1 * g.u.x, g.q.y + r1 * g.u.y, g.q.z + r1 * g.u.z);
+        const float r2 = rnd(rng);
+        const V3 p = v3(a.x + r2 * g.v.x, a.y + r2 * g.v.y, a.z + r2 * g.v.z);
+        return sub(p, o);
+    }
+    const V3 dir = v3(L.sphere.x - o.x, L.sphere.y - o.y, L.sphere.z - o.z);
+    const float d2 = dot(dir, dir);
+    const float r1 = rnd(rng), r2 = rnd(rng);
+    const float z = 1.0f + r2 * (__builtin_sqrtf(1.0f - L.sphere.w * L.sphere.w / d2) - 1.0f);
+    const float phi = (2.0f * kPi) * r1;
+    const float sxy = __builtin_sqrtf(1.0f - z * z);
+    return onb_transform(dir, v3(rrt_cosf(phi) * sxy, rrt_sinf(phi) * sxy, z));
+}
+
+// the_rest_of_your_life/camera.rs:184-254 in throughput form. Metal / dielectric keep the
+// book-2 scatter (skip_pdf); Lambertian (cosine pdf) and Isotropic (sphere pdf) sample the
+// mixture 0.5 * lights + 0.5 * material and weight by scattering_pdf / (pdf * rr).
+template <typename C, class PR>
+__device__ __forceinline__ bool shade_b3(const KParams &P, const PR &prims, const GMaterial *mtl, PathState &ps,
+                                         float t, int prim, V3 &sum, C &cnt) {
+    if (prim < 0) {
+        sum = add(sum, mul(ps.T, v3(P.background[0], P.background[1], P.background[2])));
+        return true;
+    }
+    const float4 cr = prims.at(prim);
+    const V3 p = v3(ps.o.x + ps.d.x * t, ps.o.y + ps.d.y * t, ps.o.z + ps.d.z * t);
+    V3 outward;
+    if (cr.w < 0.0f) {
+        const int j = (int)(-cr.w) - 1;
+        if (j >= (int)prims.n_quads) {
+            outward = v3(1.0f, 0.0f, 0.0f);
+        } else {
+            const float4 qn = prims.qd[j].n;
+            outward = v3(qn.x, qn.y, qn.z);
+        }
+    } else {
+        const float inv_r = 1.0f / cr.w;
+        outward = v3((p.x - cr.x) * inv_r, (p.y - cr.y) * inv_r, (p.z - cr.z) * inv_r);
+    }
+    const bool front = (cr.w < 0.0f && (int)(-cr.w) - 1 >= (int)prims.n_quads) ? true : dot(ps.d, outward) < 0.0f;
+    const V3 nrm = front ? outward : v3(-outward.x, -outward.y, -outward.z);
+    const GMaterial m = mtl[prim];
+    const int kind = m.b.x;
+    if (kind == 4) {  // DiffuseLight: one-sided (material.rs:155-160), scatter None
+        if (front) sum = add(sum, mul(ps.T, v3(m.a.x, m.a.y, m.a.z)));
+        return true;
+    }
+    V3 att, dir;
+    if (kind == 1 || kind == 2) {  // skip_pdf: the book-2 metal / dielectric scatter + RR
+        if (kind == 1) {
+            const V3 r = random_unit_vector(ps.rng, cnt);
+            const V3 refl = unit(reflect(ps.d, nrm));
+            dir = add(refl, muls(r, m.a.w));
+            att = v3(m.a.x, m.a.y, m.a.z);
+            // book 3 has no absorption test: the skip_pdf ray is followed whatever its direction
+        } else {
+            const float eta = __int_as_float(m.b.y);
+            const float ri = front ? (1.0f / eta) : eta;
+            const V3 ud = unit(ps.d);
+            float c = -dot(ud, nrm);
+            c = (c < 1.0f) ? c : 1.0f;
+            const float sn = __builtin_sqrtf(1.0f - c * c);
+            const bool cannot = ri * sn > 1.0f;
+            if (cannot || reflectance(c, ri) > rnd(ps.rng)) dir = reflect(ud, nrm);
+            else dir = refract(ud, nrm, ri);
+            att = v3(1.0f, 1.0f, 1.0f);
+        }
+        if (ps.k >= 5u) {
+            float pr = att.x;
+            if (att.y > pr) pr = att.y;
+            if (att.z > pr) pr = att.z;
+            if (pr < 0.05f) pr = 0.05f;
+            if (pr > 0.95f) pr = 0.95f;
+            if (rnd(ps.rng) > pr) return true;
+            ps.T = muls(mul(ps.T, att), 1.0f / pr);
+        } else {
+            ps.T = mul(ps.T, att);
+        }
+        ps.o = p;
+        ps.d = dir;
+        ps.k++;
+        return false;
+    }
+    // pdf path: the material's attenuation (texture value at the hit)
+    if (kind == 3) {
+        const float theta = rrt_acosf(-outward.y);
+        const float phi = rrt_atan2f(-outward.z, outward.x) + kPi;
+        att = texel(P, m.b.z, phi / (2.0f * kPi), theta / kPi);
+    } else if (kind == 5) {
+        att = checker_even(m.a.w, p) ? v3(m.a.x, m.a.y, m.a.z)
+                                     : v3(__int_as_float(m.b.y), __int_as_float(m.b.z), __int_as_float(m.b.w));
+    } else if (kind == 6) {
+        const float g = noise_value(P.perlin + m.b.z, m.a.w, p);
+        att = v3(g, g, g);
+    } else {
+        att = v3(m.a.x, m.a.y, m.a.z);
+    }
+    float rr = 1.0f;
+    if (ps.k >= 5u) {
+        rr = att.x;
+        if (att.y > rr) rr = att.y;
+        if (att.z > rr) rr = att.z;
+        if (rr < 0.05f) rr = 0.05f;
+        if (rr > 0.95f) rr = 0.95f;
+        if (rr < 1.0f && rnd(ps.rng) > rr) return true;
+    }
+    const bool iso = kind == 7;
+    const float inv4pi = 1.0f / (4.0f * kPi);
+    if (rnd(ps.rng) < 0.5f) {  // MixturePdf::generate (pdf.rs:92-98): p0 = lights
+        dir = lights_random(P, p, ps.rng);
+    } else if (iso) {  // SpherePdf::generate
+        dir = random_unit_vector(ps.rng, cnt);
+    } else {  // CosinePdf::generate: Onb(normal).transform(random_cosine_direction()) (vec3.rs:212-222)
+        const float r1 = rnd(ps.rng), r2 = rnd(ps.rng);
+        const float phi = (2.0f * kPi) * r1;
+        const float sr2 = __builtin_sqrtf(r2);
+        dir = onb_transform(nrm, v3(rrt_cosf(phi) * sr2, rrt_sinf(phi) * sr2, __builtin_sqrtf(1.0f - r2)));
+    }
+    float mat_pdf;
+    if (iso) {
+        mat_pdf = inv4pi;
+    } else {  // CosinePdf::value (pdf.rs:36-44)
+        const float cosine = dot(unit(dir), unit(nrm));
+        mat_pdf = cosine <= 0.0f ? 0.0f : cosine / kPi;
+    }
+    const float pdf = 0.5f * lights_pdf(P, p, dir) + 0.5f * mat_pdf;
+    if (pdf <= 0.0f) return true;
+    float spdf;
+    if (iso) {
+        spdf = inv4pi;
+    } else {  // Lambertian::scattering_pdf (material.rs:56-63)
+        const float cosine = dot(nrm, unit(dir));
+        spdf = cosine < 0.0f ? 0.0f : cosine / kPi;
+    }
+    ps.T = mul(ps.T, muls(muls(att, spdf), 1.0f / (pdf * rr)));
+    ps.o = p;
+    ps.d = dir;
+    ps.k++;
+    return false;
+}
+
 __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
@@ -961,7 +1199,7 @@ __device__ __forceinline__ void render_body(const KParams &P) {
                         s_hi = min(s + P.chunk, P.sample_end);
                         sum = v3(0.0f, 0.0f, 0.0f);
                         ps.rng = path_rng(P, x, y, s);
-                        camera_ray(P, x, y, ps);
+                        camera_ray<kBook2 == 4>(P, x, y, s, ps);
                         need_ray = true;
                         has = true;
                     }
@@ -1043,7 +1281,15 @@ __device__ __forceinline__ void render_body(const KParams &P) {
         }
         if (has && !need_ray && !tracing) {
             need_ray = true;
-            seg_done = shade<kBook2>(P, Prims<kBook2>{prims, motion, ps.time, P.quads, P.media, P.n_quads, ps.rng ^ ((uint64_t)ps.k << 32)}, mtl, ps, tr.closest, tr.hit_prim, sum, cnt);
+            const Prims<kBook2> spr{prims, motion, ps.time, P.quads, P.media, P.n_quads, ps.rng ^ ((uint64_t)ps.k << 32)};
+#ifdef RRT_TRACE_X
+            if ((xy & 0xffffu) == RRT_TRACE_X && (xy >> 16) == RRT_TRACE_Y && s == RRT_TRACE_S)
+                printf("K k=%u o=(%a %a %a) d=(%a %a %a) t=%a prim=%d T=(%a %a %a) rng=%llx\n", ps.k, ps.o.x, ps.o.y,
+                       ps.o.z, ps.d.x, ps.d.y, ps.d.z, tr.closest, tr.hit_prim, ps.T.x, ps.T.y, ps.T.z,
+                       (unsigned long long)ps.rng);
+#endif
+            if constexpr (kBook2 == 4) seg_done = shade_b3(P, spr, mtl, ps, tr.closest, tr.hit_prim, sum, cnt);
+            else seg_done = shade<kBook2>(P, spr, mtl, ps, tr.closest, tr.hit_prim, sum, cnt);
         }
         w_paths += (uint32_t)__popcll(__ballot(seg_done));
         if (seg_done) {  // pixel_color += ray_color(..) (camera.rs:73-76): already in `sum`
@@ -1051,7 +1297,7 @@ __device__ __forceinline__ void render_body(const KParams &P) {
             const uint32_t x = xy & 0xffffu, y = xy >> 16;
             if (s < s_hi) {
                 ps.rng = path_rng(P, x, y, s);
-                camera_ray(P, x, y, ps);
+                camera_ray<kBook2 == 4>(P, x, y, s, ps);
             } else {  // unit complete: the chunk's sum, in sample order
                 // chunk index and tile-local row, re-derived from (y, s_hi) once per unit
                 const uint32_t chunk = (s_hi - 1u - P.sample_begin) / P.chunk;
@@ -1198,13 +1444,14 @@ hipError_t launch_width(const KParams &p, bool count, hipStream_t stream) {
         // a 5-wave bound (96 VGPRs, 1-3 spills) measured 0-8% slower too.
         return p.scene_in_lds ? launch_variant<true, uint16_t, kWide, kBook2>(p, count, stream)
                               : launch_variant<false, uint16_t, kWide, kBook2>(p, count, stream);
+    } else {
+        if (!kWide && p.scene_in_lds && p.min_waves >= 6)
+            return launch_variant<true, uint16_t, kWide, kBook2, kWavesPerSimd>(p, count, stream);
+        if (!kWide && !p.scene_in_lds && p.global_waves >= 6)
+            return launch_variant<false, uint16_t, kWide, kBook2, kWavesPerSimd>(p, count, stream);
+        return p.scene_in_lds ? launch_variant<true, uint16_t, kWide, kBook2>(p, count, stream)
+                              : launch_variant<false, uint16_t, kWide, kBook2>(p, count, stream);
     }
-    if (!kWide && p.scene_in_lds && p.min_waves >= 6)
-        return launch_variant<true, uint16_t, kWide, kBook2, kWavesPerSimd>(p, count, stream);
-    if (!kWide && !p.scene_in_lds && p.global_waves >= 6)
-        return launch_variant<false, uint16_t, kWide, kBook2, kWavesPerSimd>(p, count, stream);
-    return p.scene_in_lds ? launch_variant<true, uint16_t, kWide, kBook2>(p, count, stream)
-                          : launch_variant<false, uint16_t, kWide, kBook2>(p, count, stream);
 }
 
 }  // namespace
@@ -1216,6 +1463,7 @@ hipError_t launch_render_kernel(const KParams &p, bool count, hipStream_t stream
     // binary tree for them); motion is always present (zero for static spheres).
     if (p.prim_motion) {  // book 2: the binary BVH only
         if (p.bvh_width != 2) return hipErrorInvalidValue;
+        if (p.flags & 0x4u) return launch_width<false, 4>(p, count, stream);  // RRT_FLAG_BOOK3
         if (p.n_media) return launch_width<false, 3>(p, count, stream);
         return p.n_quads ? launch_width<false, 2>(p, count, stream) : launch_width<false, 1>(p, count, stream);
     }

@@ -34,8 +34,8 @@ def _textures(scene: SceneData):
 def scene_ext(scene: SceneData):
     """(RrtSceneExt or None, keep-alive list) for the book-2 data of `scene` (motion, Perlin, quads)."""
     quads, media = getattr(scene, "quads", None), getattr(scene, "media", None)
-    bquads = getattr(scene, "boundary_quads", None)
-    if scene.motion is None and scene.perlin is None and quads is None and media is None:
+    bquads, lights = getattr(scene, "boundary_quads", None), getattr(scene, "lights", None)
+    if scene.motion is None and scene.perlin is None and quads is None and media is None and lights is None:
         return None, []
     ext = _lib.RrtSceneExt()
     keep = []
@@ -64,6 +64,11 @@ def scene_ext(scene: SceneData):
         keep.append(bq)
         ext.boundary_quads = bq.ctypes.data
         ext.n_boundary_quads = len(bq)
+    if lights is not None:
+        lt = np.ascontiguousarray(lights, dtype=_lib.LIGHT_DTYPE)
+        keep.append(lt)
+        ext.lights = lt.ctypes.data
+        ext.n_lights = len(lt)
     return ext, keep
 
 

@@ -50,6 +50,7 @@ class SceneData:
     quads: Optional[np.ndarray] = None  # QUAD_DTYPE quads (primitives n_spheres + j), or None
     media: Optional[np.ndarray] = None  # MEDIUM_DTYPE constant-density media, or None
     boundary_quads: Optional[np.ndarray] = None  # QUAD_DTYPE boundaries of quad-bounded media
+    lights: Optional[np.ndarray] = None  # LIGHT_DTYPE book-3 MIS light list (FLAG_BOOK3)
 
     @property
     def width(self) -> int:
@@ -163,9 +164,24 @@ def next_week_scene(scene: int, overrides: Optional[dict] = None, seed: int = NE
     with its motion rows, quads and media (instanced geometry baked to world space) and Perlin
     tables. Book-2 camera: background colour, a time draw per camera ray."""
     lib = _lib.load()
+    return _book_scene(lambda ov, nw: lib.rrt_build_next_week_scene(int(scene), _lib.ptr(ov), seed, ctypes.byref(nw)),
+                       overrides, NEXT_WEEK_SCENES[scene] if scene in NEXT_WEEK_SCENES else str(scene))
+
+
+def rest_of_your_life_scene(overrides: Optional[dict] = None, seed: int = NEXT_WEEK_SEED) -> SceneData:
+    """The book-3 scene (the_rest_of_your_life/mod.rs:69-164): Cornell box, a rotated box and a
+    glass sphere, with the MIS light list {light quad, glass sphere}; stratified sampling rounds
+    samples_per_pixel down to a square. Renders with FLAG_RAY_TIME | FLAG_BOOK3."""
+    lib = _lib.load()
+    return _book_scene(lambda ov, nw: lib.rrt_build_rest_of_your_life_scene(_lib.ptr(ov), seed, ctypes.byref(nw)),
+                       overrides, "rest_of_your_life")
+
+
+def _book_scene(build, overrides, name) -> SceneData:
+    """Two-pass RrtBookScene build (sizes, then arrays) into a SceneData."""
     ov = _lib.make_overrides(**(overrides or {}))
-    nw = _lib.RrtNextWeekScene()
-    _lib.check(lib.rrt_build_next_week_scene(int(scene), _lib.ptr(ov), seed, ctypes.byref(nw)))  # sizes
+    nw = _lib.RrtBookScene()
+    _lib.check(build(ov, nw))  # sizes
     spheres = _empty(_lib.SPHERE_DTYPE, nw.n_spheres)
     motion = np.zeros((nw.n_spheres, 4), dtype=np.float32)
     mats = _empty(_lib.MATERIAL_DTYPE, nw.n_materials)
@@ -173,19 +189,21 @@ def next_week_scene(scene: int, overrides: Optional[dict] = None, seed: int = NE
     perlin = np.zeros(nw.n_perlin, dtype=_lib.PERLIN_DTYPE)
     media = np.zeros(nw.n_media, dtype=_lib.MEDIUM_DTYPE)
     bquads = np.zeros(nw.n_boundary_quads, dtype=_lib.QUAD_DTYPE)
+    lights = np.zeros(nw.n_lights, dtype=_lib.LIGHT_DTYPE)
     for field, arr in (("spheres", spheres), ("materials", mats), ("quads", quads), ("perlin", perlin),
-                       ("media", media), ("boundary_quads", bquads)):
+                       ("media", media), ("boundary_quads", bquads), ("lights", lights)):
         setattr(nw, field, arr.ctypes.data)
     nw.sphere_motion = motion.ctypes.data
     nw.sphere_cap, nw.material_cap, nw.quad_cap = nw.n_spheres, nw.n_materials, nw.n_quads
     nw.perlin_cap, nw.media_cap, nw.boundary_quad_cap = nw.n_perlin, nw.n_media, nw.n_boundary_quads
-    _lib.check(lib.rrt_build_next_week_scene(int(scene), _lib.ptr(ov), seed, ctypes.byref(nw)))
+    nw.light_cap = nw.n_lights
+    _lib.check(build(ov, nw))
     cam = np.frombuffer(bytes(nw.camera), dtype=_lib.CAMERA_DTYPE).copy()
     textures = [earth_texture()] if nw.uses_texture0 else []
-    return SceneData(cam, spheres, mats, textures=textures, flags=_lib.FLAG_RAY_TIME, name=NEXT_WEEK_SCENES[scene],
+    return SceneData(cam, spheres, mats, textures=textures, flags=int(nw.flags), name=name,
                      motion=motion if np.any(motion[:, :3]) else None, perlin=perlin if len(perlin) else None,
                      quads=quads if len(quads) else None, media=media if len(media) else None,
-                     boundary_quads=bquads if len(bquads) else None)
+                     boundary_quads=bquads if len(bquads) else None, lights=lights if len(lights) else None)
 
 
 def rtow(image_width=1920, samples_per_pixel=512, max_depth=100, grid_half=11, seed=RTOW_SEED) -> SceneData:

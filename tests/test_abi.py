@@ -131,8 +131,8 @@ def test_cli_mirrors_main_rs():
     assert r.returncode == 2 and "CPU books renderer" in r.stderr
     r = subprocess.run([cli, "--backend=hip", "the_next_week"], capture_output=True, text=True)
     assert r.returncode == 2 and "the_next_week scenes 1" in r.stderr  # final_scene (0) not supported
-    r = subprocess.run([cli, "--backend=hip", "the_rest_of_your_life"], capture_output=True, text=True)
-    assert r.returncode == 2
+    r = subprocess.run([cli, "--backend=hip", "no_such_book"], capture_output=True, text=True)
+    assert r.returncode == 2 and "the_rest_of_your_life" in r.stderr
     r = subprocess.run([cli, "--backend", "wgpu"], capture_output=True, text=True)
     assert r.returncode == 2
     if rrt.device_count() == 0:

@@ -1,0 +1,83 @@
+"""GPU parity for book 3: the_rest_of_your_life's MIS integrator through the C-ABI
+(RRT_FLAG_BOOK3 + RrtSceneExt.lights), bit-exact against the oracle's f32 twin on its own tree
+and on the kernel's tree (KBVH). The oracle's book-3 restatement is pinned in tests/test_book3.py."""
+import copy
+
+import numpy as np
+import pytest
+
+import rustraytrace_amd as rrt
+from oracle import oracle
+from rustraytrace_amd.render import build_bvh
+
+from test_gpu_parity import assert_bit_exact, gpu_tile
+
+pytestmark = pytest.mark.gpu
+
+CASES = [dict(image_width=48, samples_per_pixel=16, max_depth=10),
+         dict(image_width=64, samples_per_pixel=25, max_depth=50),
+         dict(image_width=33, samples_per_pixel=81, max_depth=6)]
+
+
+@pytest.mark.parametrize("kw", CASES, ids=[f"{k['image_width']}x{k['samples_per_pixel']}d{k['max_depth']}" for k in CASES])
+def test_book3_one_shot_matches_oracle(kw):
+    sc = rrt.rest_of_your_life_scene(kw)
+    gpu = rrt.render(sc)
+    nodes, order, info = build_bvh(sc)
+    kref, _, _ = oracle.render_kbvh(sc, nodes, order, info["width"], threads=16)
+    assert_bit_exact(gpu, kref, sc.spp)
+    assert np.all(gpu[..., 3] == sc.spp) and np.isfinite(gpu).all()
+    # the oracle's own tree: the box faces share edges, and an exact t-tie there goes to the first
+    # quad tested, so a few paths may turn differently (tests/test_gpu_book2.py); all other pixels
+    # are bit-identical
+    ref, _, _ = oracle.render(sc, oracle.TWIN, threads=16)
+    same = np.all(gpu.astype(np.float64) == ref, axis=-1)
+    assert same.mean() > 0.995
+
+
+def test_book3_device_tiles_and_ray_counts():
+    sc = rrt.rest_of_your_life_scene(dict(image_width=40, samples_per_pixel=36, max_depth=12))
+    gpu, idx, ctr, work = gpu_tile(sc, count=True)
+    nodes, order, info = build_bvh(sc)
+    ref, rays, _ = oracle.render_kbvh(sc, nodes, order, info["width"], threads=16)
+    assert_bit_exact(gpu, ref, sc.spp)
+    assert ctr["rays"] == rays and ctr["paths"] == sc.width * sc.height * sc.spp
+
+
+def test_book3_larger_frame():
+    sc = rrt.rest_of_your_life_scene(dict(image_width=160, samples_per_pixel=64, max_depth=50))
+    gpu = rrt.render(sc)
+    nodes, order, info = build_bvh(sc)
+    ref, _, _ = oracle.render_kbvh(sc, nodes, order, info["width"], threads=16)
+    assert_bit_exact(gpu, ref, sc.spp)
+
+
+def test_book3_parameter_validation():
+    sc = rrt.rest_of_your_life_scene(dict(image_width=8, samples_per_pixel=4))
+    bad = copy.copy(sc)
+    bad.camera = sc.camera.copy()
+    bad.camera["params_f"][0, 3] = 5
+    with pytest.raises(rrt.RrtError, match="square"):
+        rrt.render(bad)
+    nolights = copy.copy(sc)
+    nolights.lights = None
+    with pytest.raises(rrt.RrtError, match="lights"):
+        rrt.render(nolights)
+    notime = copy.copy(sc)
+    notime.flags = rrt._lib.FLAG_BOOK3
+    with pytest.raises(rrt.RrtError, match="RAY_TIME"):
+        rrt.render(notime)
+
+
+def test_cli_rest_of_your_life_matches_python(tmp_path):
+    import os
+    import subprocess
+
+    cli = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "rustraytrace_amd", "rrt")
+    path = tmp_path / "b3.ppm"
+    r = subprocess.run([cli, "--backend", "hip", "the_rest_of_your_life", "--image_width", "40",
+                        "--samples_per_pixel", "16", "--max_depth", "8", "-o", str(path)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    sc = rrt.rest_of_your_life_scene(dict(image_width=40, samples_per_pixel=16, max_depth=8))
+    acc = rrt.render(sc)
+    assert path.read_bytes() == rrt.format_ppm_from_accum(sc.width, sc.height, acc, sc.spp)

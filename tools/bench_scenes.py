@@ -33,6 +33,7 @@ def scenes(spp_scale):
     yield "NW7 cornell_box 1080x1080", rrt.next_week_scene(7, dict(sq, samples_per_pixel=s(256)))
     yield "NW8 cornell_smoke 1080x1080", rrt.next_week_scene(8, dict(sq, samples_per_pixel=s(256)))
     yield "NW9 final_scene 1080x1080 d40", rrt.next_week_scene(9, dict(image_width=1080, samples_per_pixel=s(256)))
+    yield "B3 rest_of_your_life 1080x1080", rrt.rest_of_your_life_scene(dict(sq, samples_per_pixel=s(256)))
 
 
 def main():
