@@ -369,6 +369,50 @@ int32_t rrt_build_next_week_scene(int32_t scene, const RrtOverrides *ov, uint64_
  * (lights included). */
 int32_t rrt_build_rest_of_your_life_scene(const RrtOverrides *ov, uint64_t seed, RrtBookScene *out);
 
+/* == A node of the books' object graph (the_next_week/hittable.rs:172-180 HittableObject), for
+ * rrt_flatten_scene. 112 B; the payload is f64 like the books' Vec3, rounded to f32 once, after
+ * the transforms. Children of a LIST / BVH node are children[first .. first + count);
+ * TRANSLATE, ROTATE_Y and CONSTANT_MEDIUM take exactly one child (count 1).
+ *   SPHERE          a = center1.xyz, radius; b.xyz = center2 - center1 (Sphere::new_moving; 0 = static)
+ *   QUAD            a.xyz = q, b.xyz = u, c.xyz = v
+ *   LIST, BVH       (no payload; a BVH node is flattened like a list: the backend builds its own tree)
+ *   TRANSLATE       a.xyz = offset (hittable.rs:65-97)
+ *   ROTATE_Y        a[0] = angle in degrees (hittable.rs:99-170)
+ *   CONSTANT_MEDIUM a[0] = density; material = its Isotropic phase material; the child subtree is
+ *                   the boundary: one sphere, or quads only (constant_medium.rs)
+ * material: the RrtMaterial index of a SPHERE / QUAD / CONSTANT_MEDIUM. */
+typedef struct RrtSceneNode {
+    uint32_t kind;
+    uint32_t material;
+    uint32_t first;
+    uint32_t count;
+    double a[4];
+    double b[4];
+    double c[4];
+} RrtSceneNode;
+
+enum {
+    RRT_NODE_SPHERE = 0,
+    RRT_NODE_QUAD = 1,
+    RRT_NODE_LIST = 2,
+    RRT_NODE_BVH = 3,
+    RRT_NODE_TRANSLATE = 4,
+    RRT_NODE_ROTATE_Y = 5,
+    RRT_NODE_CONSTANT_MEDIUM = 6
+};
+
+/* Flatten the object graph under `root` into the ABI's flat arrays: spheres with
+ * motion rows, quads, media and their boundary quads, with every Translate / RotateY composed
+ * and applied to the geometry in f64 (points rotate and translate, edge and motion vectors
+ * rotate) — geometrically the reference's per-ray instance transforms, once per build instead of
+ * twice per ray and instance. Graph sharing (one Arc under several parents) is flattened once
+ * per path, as the reference would hit it once per path. Writes into out's sphere / motion /
+ * quad / media / boundary-quad arrays under their caps (caps 0 = size only); camera, materials,
+ * Perlin tables and lights are the caller's and left untouched. Errors: a cycle or depth > 64,
+ * a child index out of range, a medium boundary mixing spheres and quads or holding a medium. */
+int32_t rrt_flatten_scene(const RrtSceneNode *nodes, uint32_t n_nodes, const uint32_t *children,
+                          uint32_t n_children, uint32_t root, RrtBookScene *out);
+
 /* Camera::initialize (in_one_weekend/camera.rs:102-150) in f64, cast to the f32 ABI as
  * gpu/mod.rs:278-298 does. lookfrom/lookat/vup are 3-vectors. */
 int32_t rrt_make_camera(double aspect_ratio, int32_t image_width, int32_t samples_per_pixel,

@@ -4,7 +4,7 @@ The product is librrt_hip.so (rustraytrace_amd/csrc: gfx950 megakernel + host ru
 C-ABI declared in include/rrt_hip.h). This package is the Python host over that C-ABI:
 scene builders, render entries, PPM output. It never renders on the CPU.
 """
-from . import _lib
+from . import _lib, world
 from ._lib import RrtError, load
 from .render import (
     DeviceScene,

@@ -70,6 +70,7 @@ EXPORTED_SYMBOLS = (
     "rrt_build_bvh_ex",
     "rrt_build_next_week_scene",
     "rrt_build_rest_of_your_life_scene",
+    "rrt_flatten_scene",
     "rrt_device_count",
 )
 
@@ -109,6 +110,12 @@ class RrtBookScene(ctypes.Structure):
         (f, c_uint32) for f in ("sphere_cap", "n_spheres", "material_cap", "n_materials", "quad_cap", "n_quads",
                                 "perlin_cap", "n_perlin", "media_cap", "n_media", "boundary_quad_cap",
                                 "n_boundary_quads", "light_cap", "n_lights", "uses_texture0", "flags")]
+
+
+# == RrtSceneNode (include/rrt_hip.h): one node of the books' object graph, f64 payload; 112 B
+NODE_DTYPE = np.dtype([("kind", "<u4"), ("material", "<u4"), ("first", "<u4"), ("count", "<u4"),
+                       ("a", "<f8", 4), ("b", "<f8", 4), ("c", "<f8", 4)])
+NODE_SPHERE, NODE_QUAD, NODE_LIST, NODE_BVH, NODE_TRANSLATE, NODE_ROTATE_Y, NODE_CONSTANT_MEDIUM = range(7)
 
 
 class RrtOverrides(ctypes.Structure):
@@ -229,6 +236,7 @@ def load() -> ctypes.CDLL:
         "rrt_build_bvh_ex": (c_int32, [P, c_uint32, P, c_uint32, c_uint32, P, c_size_t, P, P]),
         "rrt_build_next_week_scene": (c_int32, [c_int32, P, c_uint64, P]),
         "rrt_build_rest_of_your_life_scene": (c_int32, [P, c_uint64, P]),
+        "rrt_flatten_scene": (c_int32, [P, c_uint32, P, c_uint32, c_uint32, P]),
         "rrt_device_count": (c_int32, [P]),
     }
     experiment = "RRT_LIB_PATH" in os.environ  # A/B of older builds: tolerate symbols they lack

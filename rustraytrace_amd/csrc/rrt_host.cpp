@@ -1802,6 +1802,153 @@ int32_t rrt_build_rest_of_your_life_scene(const RrtOverrides *ov, uint64_t seed,
     return build_book_scene(kBook3Scene, ov, seed, out);
 }
 
+}  // extern "C"
+
+// ---- the object-graph flattener -------------------------------------------
+namespace {
+
+// RotateY then Translate as one affine map of the xz plane (hittable.rs:65-170): a point p goes
+// to (c x + s z, y, -s x + c z) + off, a vector rotates only.
+struct FXform {
+    double c = 1.0, s = 0.0;
+    D3 off = d3(0.0, 0.0, 0.0);
+    D3 vec(D3 v) const { return d3(c * v.x + s * v.z, v.y, -s * v.x + c * v.z); }
+    D3 point(D3 p) const { return vec(p) + off; }
+};
+// outer after inner
+FXform compose(const FXform &outer, const FXform &inner) {
+    FXform r;
+    r.c = outer.c * inner.c - outer.s * inner.s;
+    r.s = outer.s * inner.c + outer.c * inner.s;
+    r.off = outer.vec(inner.off) + outer.off;
+    return r;
+}
+
+struct Flattener {
+    const RrtSceneNode *nodes;
+    uint32_t n_nodes;
+    const uint32_t *children;
+    uint32_t n_children;
+    std::vector<RrtSphere> sph;
+    std::vector<float> mot;
+    std::vector<RrtQuad> qds, bqs;
+    std::vector<RrtMedium> meds;
+    std::string err;
+
+    bool walk(uint32_t id, const FXform &xf, int depth, bool in_medium) {
+        if (depth > 64) return err = "object graph deeper than 64 (a cycle?)", false;
+        if (id >= n_nodes) return err = "node index " + std::to_string(id) + " out of range", false;
+        const RrtSceneNode &n = nodes[id];
+        auto child = [&](uint32_t k) -> int64_t {
+            if ((uint64_t)n.first + k >= n_children) return -1;
+            return children[n.first + k];
+        };
+        switch (n.kind) {
+            case RRT_NODE_SPHERE: {
+                const D3 c = xf.point(d3(n.a[0], n.a[1], n.a[2]));
+                const D3 m = xf.vec(d3(n.b[0], n.b[1], n.b[2]));
+                RrtSphere sp{};
+                put4(sp.center_radius, (float)c.x, (float)c.y, (float)c.z, (float)n.a[3]);
+                sp.material_index = n.material;
+                sph.push_back(sp);
+                mot.insert(mot.end(), {(float)m.x, (float)m.y, (float)m.z, 0.0f});
+                return true;
+            }
+            case RRT_NODE_QUAD: {
+                const D3 q = xf.point(d3(n.a[0], n.a[1], n.a[2]));
+                const D3 u = xf.vec(d3(n.b[0], n.b[1], n.b[2])), v = xf.vec(d3(n.c[0], n.c[1], n.c[2]));
+                RrtQuad r{};
+                put4(r.q, (float)q.x, (float)q.y, (float)q.z, 0.0f);
+                put4(r.u, (float)u.x, (float)u.y, (float)u.z, 0.0f);
+                put4(r.v, (float)v.x, (float)v.y, (float)v.z, 0.0f);
+                r.material_index = n.material;
+                qds.push_back(r);
+                return true;
+            }
+            case RRT_NODE_LIST:
+            case RRT_NODE_BVH:
+                for (uint32_t k = 0; k < n.count; ++k) {
+                    const int64_t c = child(k);
+                    if (c < 0) return err = "node " + std::to_string(id) + ": children out of range", false;
+                    if (!walk((uint32_t)c, xf, depth + 1, in_medium)) return false;
+                }
+                return true;
+            case RRT_NODE_TRANSLATE:
+            case RRT_NODE_ROTATE_Y: {
+                const int64_t c = n.count == 1 ? child(0) : -1;
+                if (c < 0) return err = "node " + std::to_string(id) + ": a transform takes one child", false;
+                FXform t;
+                if (n.kind == RRT_NODE_TRANSLATE) {
+                    t.off = d3(n.a[0], n.a[1], n.a[2]);
+                } else {  // RotateY::new (hittable.rs:100-103)
+                    const double rad = degrees_to_radians(n.a[0]);
+                    t.s = std::sin(rad);
+                    t.c = std::cos(rad);
+                }
+                return walk((uint32_t)c, compose(xf, t), depth + 1, in_medium);
+            }
+            case RRT_NODE_CONSTANT_MEDIUM: {
+                if (in_medium) return err = "node " + std::to_string(id) + ": a medium inside a medium boundary", false;
+                const int64_t c = n.count == 1 ? child(0) : -1;
+                if (c < 0) return err = "node " + std::to_string(id) + ": a medium takes one boundary child", false;
+                Flattener sub{nodes, n_nodes, children, n_children, {}, {}, {}, {}, {}, {}};
+                if (!sub.walk((uint32_t)c, xf, depth + 1, true)) return err = sub.err, false;
+                RrtMedium md{};
+                md.material_index = n.material;
+                md.density = (float)n.a[0];
+                if (sub.sph.size() == 1 && sub.qds.empty()) {
+                    if (sub.mot[0] != 0.0f || sub.mot[1] != 0.0f || sub.mot[2] != 0.0f)
+                        return err = "node " + std::to_string(id) + ": moving medium boundaries are not supported", false;
+                    md.boundary_kind = RRT_BOUNDARY_SPHERE;
+                    std::memcpy(md.sphere, sub.sph[0].center_radius, sizeof(md.sphere));
+                } else if (sub.sph.empty() && !sub.qds.empty()) {
+                    md.boundary_kind = RRT_BOUNDARY_QUADS;
+                    md.first = (uint32_t)bqs.size();
+                    md.count = (uint32_t)sub.qds.size();
+                    bqs.insert(bqs.end(), sub.qds.begin(), sub.qds.end());
+                } else {
+                    return err = "node " + std::to_string(id) + ": a medium boundary is one sphere or quads only", false;
+                }
+                meds.push_back(md);
+                return true;
+            }
+            default:
+                return err = "node " + std::to_string(id) + ": unknown kind", false;
+        }
+    }
+};
+
+}  // namespace
+
+extern "C" {
+
+int32_t rrt_flatten_scene(const RrtSceneNode *nodes, uint32_t n_nodes, const uint32_t *children, uint32_t n_children,
+                          uint32_t root, RrtBookScene *out) {
+    if (!out || (n_nodes && !nodes) || (n_children && !children)) return fail(RRT_E_INVALID, "null argument");
+    Flattener f{nodes, n_nodes, children, n_children, {}, {}, {}, {}, {}, {}};
+    if (!f.walk(root, FXform{}, 0, false)) return fail(RRT_E_INVALID, "rrt_flatten_scene: " + f.err);
+    RrtBookScene &o = *out;
+    o.n_spheres = (uint32_t)f.sph.size();
+    o.n_quads = (uint32_t)f.qds.size();
+    o.n_media = (uint32_t)f.meds.size();
+    o.n_boundary_quads = (uint32_t)f.bqs.size();
+    auto put = [&](auto *dst, uint32_t cap, const auto &src, const char *what) -> int32_t {
+        if (cap == 0) return RRT_OK;
+        if (cap < src.size() || !dst)
+            return fail(RRT_E_INVALID, std::string(what) + "_cap too small (need " + std::to_string(src.size()) + ")");
+        if (!src.empty()) std::memcpy(dst, src.data(), src.size() * sizeof(src[0]));
+        return RRT_OK;
+    };
+    int32_t rc;
+    if ((rc = put(o.spheres, o.sphere_cap, f.sph, "sphere")) || (rc = put(o.quads, o.quad_cap, f.qds, "quad")) ||
+        (rc = put(o.media, o.media_cap, f.meds, "media")) ||
+        (rc = put(o.boundary_quads, o.boundary_quad_cap, f.bqs, "boundary_quad")))
+        return rc;
+    if (o.sphere_motion && o.sphere_cap >= f.sph.size() && !f.mot.empty())
+        std::memcpy(o.sphere_motion, f.mot.data(), f.mot.size() * sizeof(float));
+    return RRT_OK;
+}
+
 // ---- render_io.rs:3-31 -------------------------------------------------------------------
 static inline uint8_t quantize_channel(float x, float scale) {
     float r = x * scale;

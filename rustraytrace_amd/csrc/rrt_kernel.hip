@@ -35,6 +35,9 @@ namespace {
 //   2: traversal wave-iterations x 64 / sum of tracing lanes per iteration / outer iterations
 //   3: leaf-loop wave-iterations x 64 / active lanes per leaf iteration / lanes taking the root branch
 //   4: shade entries x 64 / shading lanes / rejection-loop wave-iterations x 64
+#ifndef RRT_SPHERE_FMA
+#define RRT_SPHERE_FMA 0
+#endif
 #ifndef RRT_PHASE_TIMING
 #define RRT_PHASE_TIMING 0
 #endif
@@ -368,9 +371,15 @@ __device__ __forceinline__ void test_prims(const PR &prim_cr, int first, int cou
         if (kCount) cnt.spheres++;
         const float4 cr = prim_cr.at(i);
         const V3 oc = v3(cr.x - o.x, cr.y - o.y, cr.z - o.z);
+#if RRT_SPHERE_FMA
+        const float h = __builtin_fmaf(d.z, oc.z, __builtin_fmaf(d.y, oc.y, d.x * oc.x));
+        const float c = __builtin_fmaf(-cr.w, cr.w, __builtin_fmaf(oc.z, oc.z, __builtin_fmaf(oc.y, oc.y, oc.x * oc.x)));
+        const float disc = __builtin_fmaf(h, h, -(a * c));
+#else
         const float h = dot(d, oc);
         const float c = dot(oc, oc) - cr.w * cr.w;
         const float disc = h * h - a * c;
+#endif
         if (disc < 0.0f) continue;
         const float sq = __builtin_sqrtf(disc);
         float root = (h - sq) / a;
@@ -412,9 +421,15 @@ __device__ __forceinline__ void test_prims2(const PR &prim_cr, int f0, int c0, i
             }
         }
         const V3 oc = v3(cr.x - o.x, cr.y - o.y, cr.z - o.z);
+#if RRT_SPHERE_FMA
+        const float h = __builtin_fmaf(d.z, oc.z, __builtin_fmaf(d.y, oc.y, d.x * oc.x));
+        const float c = __builtin_fmaf(-cr.w, cr.w, __builtin_fmaf(oc.z, oc.z, __builtin_fmaf(oc.y, oc.y, oc.x * oc.x)));
+        const float disc = __builtin_fmaf(h, h, -(a * c));
+#else
         const float h = dot(d, oc);
         const float c = dot(oc, oc) - cr.w * cr.w;
         const float disc = h * h - a * c;
+#endif
         if (disc < 0.0f) continue;
         if constexpr (RRT_PHASE_TIMING == 3) cnt.d2 += 1;
         const float sq = __builtin_sqrtf(disc);

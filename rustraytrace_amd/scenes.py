@@ -8,9 +8,11 @@
     C3 rtow_4k         same scene, 3840x2160, 2048 spp (8-GPU tile split)
     C4 earth_light     textured earth + emissive sphere, 1920x1080, 1024 spp
     C5 stress10k       RTOW generator on a 100x100 grid (<=10,004 spheres), 1920x1080, 256 spp
-* `next_week_scene` — book-2 scenes 1-4 (the_next_week/mod.rs:83-255: bouncing_spheres with
-  moving spheres and a checker ground, checkered_spheres, earth, perlin_spheres), flattened by
-  rrt_build_next_week_scene.
+* `next_week_scene` — book-2 scenes 1-10 (the_next_week/mod.rs:68-587), flattened by
+  rrt_build_next_week_scene; `rest_of_your_life_scene` — book 3.
+* Scenes of your own: the books' object API in `rustraytrace_amd.world` (Sphere, Quad,
+  HittableList, BvhNode, Translate, RotateY, ConstantMedium, make_box, materials and textures),
+  flattened by rrt_flatten_scene.
 """
 from __future__ import annotations
 
