@@ -111,7 +111,8 @@ typedef struct RrtQuad {
  * The boundary is not a surface of the scene (add it separately if it is one). material_index
  * names the phase function (RRT_MAT_ISOTROPIC). Free-flight draw: the reference takes
  * `random_double()` from its entropy stream inside hit(), so its stream position depends on the
- * BVH walk; here the draw is u = splitmix64(path_rng ^ (bounce << 32) ^ medium) >> 40 (24 bits,
+ * BVH walk; here the draw is u = splitmix64(path_rng ^ (bounce << 32) ^ medium) >> 40 (path_rng:
+ * the first 64 bits of the path's xoshiro128+ state at the segment start; 24 bits,
  * times 2^-24) — one independent uniform per (path, segment, medium), the same whichever order a
  * BVH tests the primitives in. hit_distance = (-1/density) * ln(u) in f32 (a Cephes logf). */
 typedef struct RrtMedium {

@@ -34,7 +34,7 @@
 //          for the GPU (no FP contraction: built with -ffp-contract=off).
 // Deliberate restatement choices:
 //   * RNG: the reference's thread-local SmallRng::from_entropy (rtweekend.rs:9-11) is not
-//     reproducible; both sides use a PCG32 stream per (seed, pixel, sample) instead, and
+//     reproducible; both sides use a xoshiro128+ stream per (seed, pixel, sample) instead, and
 //     random_double() = (u32 >> 8) * 2^-24 (exact in f32 and f64).
 //   * f32 twin: 1e-160 (vec3.rs:185) underflows to 0; transcendentals of sphere UV and the
 //     noise texture's sin use the Cephes f32 polynomials the kernel uses (books mode: libm).
@@ -106,14 +106,21 @@ uint64_t splitmix64(uint64_t z) {
     z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
     return z ^ (z >> 31);
 }
-struct PathRng {
-    uint64_t s;
+struct PathRng {  // xoshiro128+ (the kernel's rng_next, rrt_kernel.hip)
+    uint32_t a, b, c, d;
+    PathRng(uint64_t z, uint64_t key)
+        : a((uint32_t)z), b((uint32_t)(z >> 32)), c((uint32_t)key), d((uint32_t)(key >> 32) | 1u) {}
+    uint64_t key() const { return (uint64_t)a | ((uint64_t)b << 32); }
     uint32_t next() {
-        const uint64_t old = s;
-        s = old * 6364136223846793005ull + 1442695040888963407ull;
-        const uint32_t xs = (uint32_t)(((old >> 18) ^ old) >> 27);
-        const uint32_t rot = (uint32_t)(old >> 59);
-        return (xs >> rot) | (xs << ((32u - rot) & 31u));
+        const uint32_t r = a + d;
+        const uint32_t t = b << 9;
+        c ^= a;
+        d ^= b;
+        b ^= c;
+        a ^= d;
+        c ^= t;
+        d = (d << 11) | (d >> 21);
+        return r;
     }
     template <class T> T random_double() { return (T)(next() >> 8) * lit<T>(0x1.0p-24, 0x1.0p-24f); }
     template <class T> T random_double_range(T lo, T hi) { return random_double<T>() * (hi - lo) + lo; }
@@ -624,6 +631,9 @@ struct KTree {
     const uint32_t *order = nullptr;  // leaf-order primitive -> original sphere index
 };
 
+// 1/d clamped to +-2^64: a zero direction component gives a huge finite slope instead of inf,
+// so (P - o) * inv keeps its sign (inf * P - inf * o would be NaN or -inf at a straddling slab)
+inline float kclamp_inv(float v) { return std::fmax(std::fmin(v, 0x1.0p64f), -0x1.0p64f); }
 struct KRay {
     float ix, iy, iz, oix, oiy, oiz;
 };
@@ -655,9 +665,9 @@ __attribute__((target_clones("fma", "default")))
 bool kbvh_hit(const World<float> &w, const KTree &kt, Vec3<float> o, Vec3<float> d, float time, Hit<float> &rec,
               uint64_t *tests, uint64_t seg) {
     KRay r;
-    r.ix = 1.0f / d[0];
-    r.iy = 1.0f / d[1];
-    r.iz = 1.0f / d[2];
+    r.ix = kclamp_inv(1.0f / d[0]);  // the kernel's ray_consts
+    r.iy = kclamp_inv(1.0f / d[1]);
+    r.iz = kclamp_inv(1.0f / d[2]);
     r.oix = o[0] * r.ix;
     r.oiy = o[1] * r.iy;
     r.oiz = o[2] * r.iz;
@@ -1104,7 +1114,7 @@ Vec3<T> ray_color_books(const World<T> &w, const Cam<T> &cam, PathRng &rng, Vec3
     if (depth <= 0) return mk(T(0), T(0), T(0));
     tl.rays++;
     Record<T> rec;
-    if (!world_hit(w, o, d, time, rng.s ^ ((uint64_t)(cam.max_depth - depth) << 32), rec, &tl.tests))
+    if (!world_hit(w, o, d, time, rng.key() ^ ((uint64_t)(cam.max_depth - depth) << 32), rec, &tl.tests))
         return miss_color(cam, d);
     const Vec3<T> em = emitted(w, rec);
     Vec3<T> att, dir;
@@ -1126,7 +1136,7 @@ Vec3<T> ray_color_twin(const World<T> &w, const Cam<T> &cam, PathRng &rng, Vec3<
     for (uint32_t k = 0; k < cam.max_depth; ++k) {
         tl.rays++;
         Record<T> rec;
-        if (!world_hit(w, o, d, time, rng.s ^ ((uint64_t)k << 32), rec, &tl.tests, kt)) return Lp + Tp * miss_color(cam, d);
+        if (!world_hit(w, o, d, time, rng.key() ^ ((uint64_t)k << 32), rec, &tl.tests, kt)) return Lp + Tp * miss_color(cam, d);
         const Material<T> &m = w.mats[rec.mat];
         if (m.kind == RRT_MAT_DIFFUSE_LIGHT) return Lp + Tp * m.albedo;
         Vec3<T> att, dir;
@@ -1274,7 +1284,7 @@ Vec3<T> ray_color_b3_books(const World<T> &w, const Cam<T> &cam, PathRng &rng, V
     if (depth <= 0) return mk(T(0), T(0), T(0));
     tl.rays++;
     Record<T> rec;
-    if (!world_hit(w, o, d, time, rng.s ^ ((uint64_t)(cam.max_depth - depth) << 32), rec, &tl.tests))
+    if (!world_hit(w, o, d, time, rng.key() ^ ((uint64_t)(cam.max_depth - depth) << 32), rec, &tl.tests))
         return cam.background;
     const Material<T> &m = w.mats[rec.mat];
     if (m.kind == RRT_MAT_DIFFUSE_LIGHT) return rec.front ? m.albedo : mk(T(0), T(0), T(0));
@@ -1307,7 +1317,7 @@ Vec3<T> ray_color_b3_twin(const World<T> &w, const Cam<T> &cam, PathRng &rng, Ve
     for (uint32_t k = 0; k < cam.max_depth; ++k) {
         tl.rays++;
         Record<T> rec;
-        if (!world_hit(w, o, d, time, rng.s ^ ((uint64_t)k << 32), rec, &tl.tests, kt)) return Lp + Tp * cam.background;
+        if (!world_hit(w, o, d, time, rng.key() ^ ((uint64_t)k << 32), rec, &tl.tests, kt)) return Lp + Tp * cam.background;
         const Material<T> &m = w.mats[rec.mat];
         if (m.kind == RRT_MAT_DIFFUSE_LIGHT) return rec.front ? Lp + Tp * m.albedo : Lp;
         Vec3<T> att, dir;
@@ -1389,7 +1399,7 @@ int render(const RrtCamera *c, const RrtSphere *s, uint32_t n, const RrtMaterial
                 for (uint32_t c0 = s0; c0 < s1; c0 += step) {
                     Vec3<T> csum = mk(T(0), T(0), T(0));
                     for (uint32_t sidx = c0; sidx < std::min(s1, c0 + step); ++sidx) {
-                        PathRng rng{splitmix64(key + sidx)};
+                        PathRng rng(splitmix64(key + sidx), key);
                         Vec3<T> o, d;
                         T time;
                         get_ray(cam, rng, i, j, sidx, o, d, time);
@@ -1651,7 +1661,8 @@ void oracle_reflect_refract(int f32, const double *v, const double *n, double et
 
 // The first `count` u32 draws of path (seed, pixel, sample).
 void oracle_path_stream(uint32_t seed, uint32_t pixel, uint32_t sample, uint32_t count, uint32_t *out) {
-    PathRng rng{splitmix64(splitmix64(((uint64_t)seed << 32) ^ (uint64_t)pixel) + sample)};
+    const uint64_t key = splitmix64(((uint64_t)seed << 32) ^ (uint64_t)pixel);
+    PathRng rng(splitmix64(key + sample), key);
     for (uint32_t i = 0; i < count; ++i) out[i] = rng.next();
 }
 

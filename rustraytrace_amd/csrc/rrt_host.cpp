@@ -343,10 +343,34 @@ struct FlatBvh {
     uint32_t n_nodes = 0, n_leaves = 0, max_depth = 0, max_leaf = 0, stack_need = 0, width = 2;
 };
 
-void put_box(float *lo, float *hi, const Aabb &b) {
+// Conservative slab test in f32. The kernel's plane distance fma(P, inv, -o*inv) differs from
+// the exact (P - o)/d by at most u(2|P - o| + |o|)/|d| along axis a (u = 2^-24: the roundings
+// of 1/d, of o*inv and of the fma), and the primitive tests' own t carry a few ulps. Growing
+// each stored box face by 4u(2|P| + 3 O_a) in position space — O_a = the largest |coordinate|
+// on axis a of the scene's bounds, which holds every ray origin (hit points, and cameras inside
+// the scene's extent) — covers all of it, so a box never rejects a ray its primitives would hit
+// (a missed grazing hit at final_scene's |p| ~ 2000 showed the need). The growth is ~1e-5 of
+// a box's size at RTOW scale; traversal cost unchanged within noise.
+struct BoxSlack {
+    double o[3] = {0.0, 0.0, 0.0};
+    explicit BoxSlack(const Aabb &scene) {
+        for (int a = 0; a < 3; ++a) {
+            const double m = std::max(std::fabs(scene.ax[a].min), std::fabs(scene.ax[a].max));
+            if (std::isfinite(m) && m < 1e29) o[a] = m;
+        }
+    }
+    double grow(int a, double p) const { return 4.0 * 0x1.0p-24 * (2.0 * std::fabs(p) + 3.0 * o[a]); }
+};
+
+void put_box(float *lo, float *hi, const Aabb &b, const BoxSlack *slack) {
     for (int a = 0; a < 3; ++a) {
-        lo[a] = f32_down(b.ax[a].min);
-        hi[a] = f32_up(b.ax[a].max);
+        double mn = b.ax[a].min, mx = b.ax[a].max;
+        if (slack && mn <= mx && std::isfinite(mn) && std::isfinite(mx) && mx < 1e29) {
+            mn -= slack->grow(a, mn);
+            mx += slack->grow(a, mx);
+        }
+        lo[a] = f32_down(mn);
+        hi[a] = f32_up(mx);
     }
 }
 
@@ -361,11 +385,12 @@ Aabb never_hit_box() {
 // BVH2: the binary tree as is, root = node 0, both child boxes stored in the parent.
 FlatBvh flatten2(const Builder &bd, int32_t root) {
     FlatBvh f;
+    const BoxSlack slack(bd.bin[root].box);
     std::vector<rrt::GNode> out;
     struct Item { int32_t bin; int32_t slot; };
     auto child_ref = [&](int32_t c, float *lo, float *hi, int32_t &ref, int32_t &cnt, std::vector<Item> &todo) {
         const Builder::BNode &b = bd.bin[c];
-        put_box(lo, hi, b.leaf && b.count == 0 ? never_hit_box() : b.box);
+        put_box(lo, hi, b.leaf && b.count == 0 ? never_hit_box() : b.box, &slack);
         if (b.leaf) {
             ref = b.first;
             cnt = b.count;
@@ -386,7 +411,7 @@ FlatBvh flatten2(const Builder &bd, int32_t root) {
         float lo0[3], hi0[3], lo1[3], hi1[3];
         int32_t ref0, cnt0;
         child_ref(root, lo0, hi0, ref0, cnt0, todo);
-        put_box(lo1, hi1, never_hit_box());
+        put_box(lo1, hi1, never_hit_box(), nullptr);
         rrt::GNode &n = out[0];
         n.b0 = make_float4(lo0[0], hi0[0], lo0[1], hi0[1]);
         n.b1 = make_float4(lo0[2], hi0[2], lo1[0], hi1[0]);
@@ -426,6 +451,7 @@ FlatBvh flatten2(const Builder &bd, int32_t root) {
 // collapse). Empty slots get the never-hit box.
 FlatBvh flatten4(const Builder &bd, int32_t root) {
     FlatBvh f;
+    const BoxSlack slack(bd.bin[root].box);
     std::vector<rrt::GNode4> out;
     struct Item { int32_t bin; int32_t slot; uint32_t depth; };
     std::vector<Item> stack;
@@ -457,19 +483,19 @@ FlatBvh flatten4(const Builder &bd, int32_t root) {
         int32_t child[4], count[4];
         for (int c = 0; c < 4; ++c) {
             if (c >= (int)kids.size()) {
-                put_box(lo[c], hi[c], never_hit_box());
+                put_box(lo[c], hi[c], never_hit_box(), nullptr);
                 child[c] = 0;
                 count[c] = 0;
                 continue;
             }
             const Builder::BNode &k = bd.bin[kids[c]];
             if (k.leaf && k.count == 0) {  // empty scene: nothing to enter
-                put_box(lo[c], hi[c], never_hit_box());
+                put_box(lo[c], hi[c], never_hit_box(), nullptr);
                 child[c] = 0;
                 count[c] = 0;
                 continue;
             }
-            put_box(lo[c], hi[c], k.box);
+            put_box(lo[c], hi[c], k.box, &slack);
             if (k.leaf) {
                 child[c] = k.first;
                 count[c] = k.count;

@@ -68,33 +68,51 @@ __device__ __forceinline__ V3 unit(V3 v) {
     return muls(v, inv);
 }
 
-// ---- RNG: PCG32 (XSH-RR 64/32) per path, keyed by (seed, pixel, sample) --------------------
+// ---- RNG: xoshiro128+ per path, keyed by (seed, pixel, sample) ------------------------------
 // Counter-based in effect: the i-th draw of a path is a pure function of
 // (seed, global pixel index, sample index, i); nothing depends on lane or launch shape.
+// xoshiro128+ (Blackman & Vigna) is all full-rate 32-bit VALU (add, shift, xor, alignbit):
+// 8 instructions per draw against ~17 with three quarter-rate multiplies for the 64-bit LCG
+// of a PCG32 (+4.3 % on C2, same-box A/B). Only the top 24 bits of each output are used
+// (random_double), the bits the authors recommend for floating-point generation.
 __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
     z += 0x9e3779b97f4a7c15ull;
     z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
     z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
     return z ^ (z >> 31);
 }
-__device__ __forceinline__ uint32_t pcg_next(uint64_t &s) {
-    const uint64_t old = s;
-    s = old * 6364136223846793005ull + 1442695040888963407ull;
-    const uint32_t xs = (uint32_t)(((old >> 18) ^ old) >> 27);
-    const uint32_t rot = (uint32_t)(old >> 59);
-    return (xs >> rot) | (xs << ((32u - rot) & 31u));
+struct RngState {
+    uint32_t a, b, c, d;
+};
+__device__ __forceinline__ uint32_t rotl32(uint32_t x, int k) { return (x << k) | (x >> (32 - k)); }
+__device__ __forceinline__ uint32_t rng_next(RngState &s) {
+    const uint32_t r = s.a + s.d;
+    const uint32_t t = s.b << 9;
+    s.c ^= s.a;
+    s.d ^= s.b;
+    s.b ^= s.c;
+    s.a ^= s.d;
+    s.c ^= t;
+    s.d = rotl32(s.d, 11);
+    return r;
 }
+// state = (z, pixel key); the low bit of the last word is forced so the state is never zero
+__device__ __forceinline__ RngState rng_seed(uint64_t z, uint64_t key) {
+    return RngState{(uint32_t)z, (uint32_t)(z >> 32), (uint32_t)key, (uint32_t)(key >> 32) | 1u};
+}
+// 64 bits of the state (the media draws' key at a segment start)
+__device__ __forceinline__ uint64_t rng_key(const RngState &s) { return (uint64_t)s.a | ((uint64_t)s.b << 32); }
 // random_double(): 24-bit uniform in [0,1) (exact in f32 and f64).
-__device__ __forceinline__ float rnd(uint64_t &s) { return (float)(pcg_next(s) >> 8) * 0x1.0p-24f; }
+__device__ __forceinline__ float rnd(RngState &s) { return (float)(rng_next(s) >> 8) * 0x1.0p-24f; }
 // random_double_range(lo,hi) = u*(hi-lo) + lo  (rand 0.8 UniformFloat::sample_single order)
-__device__ __forceinline__ float rnd_range(uint64_t &s, float lo, float hi) { return rnd(s) * (hi - lo) + lo; }
+__device__ __forceinline__ float rnd_range(RngState &s, float lo, float hi) { return rnd(s) * (hi - lo) + lo; }
 
 // vec3.rs:181-189 random_unit_vector: rejection in [-1,1)^3, accept 1e-160 < |p|^2 <= 1
 // (1e-160 underflows to 0 in f32: the one intentional f32 deviation).
 // The loop only draws and tests; the normalisation runs once after it, with the wave
 // converged (inside the loop it would run in every iteration in which any lane accepts).
 template <typename C>
-__device__ __forceinline__ V3 random_unit_vector(uint64_t &s, C &cnt) {
+__device__ __forceinline__ V3 random_unit_vector(RngState &s, C &cnt) {
     float px, py, pz, lensq;
     for (;;) {
         if constexpr (RRT_PHASE_TIMING == 4) cnt.d2 += wave_slot();
@@ -175,9 +193,10 @@ __device__ __forceinline__ float rrt_atan2f(float y, float x) {
 // the reference's op for op. This is the standard GPU form: t = lo*inv - o*inv as one FMA per
 // plane, near/far via min/max, entry = max3, exit = min3. It can only differ from the
 // reference's slab in grazing cases at the last ulp, where the reference's own result already
-// depends on its BVH topology ("Parity"). A zero direction component gives
-// inv = +-inf and NaN plane distances, which min/max ignore: that axis then constrains
-// nothing (conservative: never a wrong rejection).
+// depends on its BVH topology ("Parity"); the host grows every stored box by the
+// rounding bound of this arithmetic (rrt_host.cpp BoxSlack), so the test is conservative. A
+// zero direction component gives inv = +-2^64 (ray_consts), i.e. plane distances of +-huge
+// with the sign of (P - o): the ray is inside that slab for all t, or outside it.
 __device__ __forceinline__ bool box_hit(float lx, float hx, float ly, float hy, float lz, float hz,
                                         V3 inv, V3 oi, float tmin, float tmax, float &tnear) {
     const float x0 = __builtin_fmaf(lx, inv.x, -oi.x), x1 = __builtin_fmaf(hx, inv.x, -oi.x);
@@ -207,9 +226,15 @@ struct RayK {
     float ra;  // refined reciprocal of a (0 when a is outside [2^-64, 2^64])
 };
 
+// minNum / maxNum semantics (a NaN direction gives +2^64, as in the oracle's std::fmin/fmax)
+__device__ __forceinline__ float clamp_inv(float v) { return __builtin_fmaxf(__builtin_fminf(v, 0x1.0p64f), -0x1.0p64f); }
+
 __device__ __forceinline__ RayK ray_consts(V3 o, V3 d) {
     RayK r;
-    r.inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);  // aabb.rs:58 adinv, hoisted per ray
+    // aabb.rs:58 adinv, hoisted per ray, clamped to +-2^64: a zero component then gives a huge
+    // finite slope, so fma(P, inv, -o*inv) keeps the sign of (P - o). Unclamped, inf * P - inf * o
+    // is NaN or -inf, and a slab that straddles o (lo < 0 < hi about o's sign) rejects the ray.
+    r.inv = v3(clamp_inv(1.0f / d.x), clamp_inv(1.0f / d.y), clamp_inv(1.0f / d.z));
     r.oi = v3(o.x * r.inv.x, o.y * r.inv.y, o.z * r.inv.z);
     r.a = dot(d, d);                                  // sphere.rs:27, hoisted per ray
     // The reciprocal step of the IEEE f32 division expansion (v_rcp + one Newton step), done
@@ -629,7 +654,7 @@ __device__ __forceinline__ bool trav_step4(const GNode4 *__restrict__ nodes, con
 // the sum starts at +0 and therefore never becomes -0.
 struct PathState {
     V3 o, d, T;
-    uint64_t rng;
+    RngState rng;
     uint32_t k;  // bounce index (camera ray = 0)
     float time;  // the camera ray's time draw, kept by every bounce (book 2, moving spheres)
 };
@@ -671,11 +696,12 @@ __device__ __forceinline__ void camera_ray(const KParams &P, uint32_t x, uint32_
     ps.k = 0;
 }
 
-// The path's RNG stream for sample s of global pixel (x, y): PCG32 state keyed by
-// splitmix64(splitmix64((seed << 32) ^ pixel) + s). Re-derived per sample (no per-pixel key held).
-__device__ __forceinline__ uint64_t path_rng(const KParams &P, uint32_t x, uint32_t y, uint32_t s) {
+// The path's RNG stream for sample s of global pixel (x, y): xoshiro128+ state
+// (z, key | 1 << 32) with key = splitmix64((seed << 32) ^ pixel) and z = splitmix64(key + s).
+// Re-derived per sample (no per-pixel key held).
+__device__ __forceinline__ RngState path_rng(const KParams &P, uint32_t x, uint32_t y, uint32_t s) {
     const uint64_t key = splitmix64(((uint64_t)P.seed << 32) ^ (uint64_t)(y * P.width + x));
-    return splitmix64(key + s);
+    return rng_seed(splitmix64(key + s), key);
 }
 
 // ---- book-2 procedural textures (the_next_week/texture.rs:39-77, 111-126; perlin.rs) --------
@@ -971,7 +997,7 @@ __device__ __forceinline__ float lights_pdf(const KParams &P, V3 o, V3 d) {
 
 // HittableList::random (hittable_list.rs:71-75): random_int(0, n-1), then Quad::random
 // (quad.rs:104-107) or Sphere::random + random_to_sphere (sphere.rs:55-66, 117-122).
-__device__ __forceinline__ V3 lights_random(const KParams &P, V3 o, uint64_t &rng) {
+__device__ __forceinline__ V3 lights_random(const KParams &P, V3 o, RngState &rng) {
     const int idx = (int)rnd_range(rng, 0.0f, (float)P.n_lights);
     const GLight L = P.lights[idx];
     if (L.kind == 0u) {
@@ -1249,7 +1275,7 @@ __device__ __forceinline__ void render_body(const KParams &P) {
         }
         RayK rk;
         if (tracing) rk = ray_consts(ps.o, ps.d);
-        const Prims<kBook2> pr{prims, motion, ps.time, P.quads, P.media, P.n_quads, ps.rng ^ ((uint64_t)ps.k << 32)};
+        const Prims<kBook2> pr{prims, motion, ps.time, P.quads, P.media, P.n_quads, rng_key(ps.rng) ^ ((uint64_t)ps.k << 32)};
         if constexpr (kWide) {
             for (;;) {
                 if constexpr (RRT_PHASE_TIMING == 2) {
@@ -1296,12 +1322,12 @@ __device__ __forceinline__ void render_body(const KParams &P) {
         }
         if (has && !need_ray && !tracing) {
             need_ray = true;
-            const Prims<kBook2> spr{prims, motion, ps.time, P.quads, P.media, P.n_quads, ps.rng ^ ((uint64_t)ps.k << 32)};
+            const Prims<kBook2> spr{prims, motion, ps.time, P.quads, P.media, P.n_quads, rng_key(ps.rng) ^ ((uint64_t)ps.k << 32)};
 #ifdef RRT_TRACE_X
             if ((xy & 0xffffu) == RRT_TRACE_X && (xy >> 16) == RRT_TRACE_Y && s == RRT_TRACE_S)
                 printf("K k=%u o=(%a %a %a) d=(%a %a %a) t=%a prim=%d T=(%a %a %a) rng=%llx\n", ps.k, ps.o.x, ps.o.y,
                        ps.o.z, ps.d.x, ps.d.y, ps.d.z, tr.closest, tr.hit_prim, ps.T.x, ps.T.y, ps.T.z,
-                       (unsigned long long)ps.rng);
+                       (unsigned long long)rng_key(ps.rng));
 #endif
             if constexpr (kBook2 == 4) seg_done = shade_b3(P, spr, mtl, ps, tr.closest, tr.hit_prim, sum, cnt);
             else seg_done = shade<kBook2>(P, spr, mtl, ps, tr.closest, tr.hit_prim, sum, cnt);

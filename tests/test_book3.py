@@ -6,7 +6,7 @@ unbiasedness against the book-2 integrator on the same geometry. The GPU side is
 tests/test_gpu_book3.py.
 
 Parity note: the book-3 scene has no random layout; the sample streams are the backend's
-(per-path PCG), so these are restatement checks, not reference vectors (parity unpinned, as for
+(per-path xoshiro128+), so these are restatement checks, not reference vectors (parity unpinned, as for
 books 1 and 2)."""
 import copy
 

@@ -69,3 +69,11 @@ def test_partial_tiles_and_chunk_remainders(width, spp):
     sc = rrt.rtow(image_width=width, samples_per_pixel=spp, max_depth=10)
     gpu, _ = check(sc)
     assert np.all(gpu[..., 3] == spp)
+
+
+def test_axis_parallel_rays():
+    # d.x == 0 for every camera ray, through a box that straddles x = 0 (test_oracle.py)
+    from test_oracle import axis_parallel_scene
+
+    gpu, _ = check(axis_parallel_scene())
+    assert np.all(gpu[..., :3] == 0)
