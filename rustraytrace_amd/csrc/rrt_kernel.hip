@@ -106,6 +106,9 @@ __device__ __forceinline__ uint64_t rng_key(const RngState &s) { return (uint64_
 __device__ __forceinline__ float rnd(RngState &s) { return (float)(rng_next(s) >> 8) * 0x1.0p-24f; }
 // random_double_range(lo,hi) = u*(hi-lo) + lo  (rand 0.8 UniformFloat::sample_single order)
 __device__ __forceinline__ float rnd_range(RngState &s, float lo, float hi) { return rnd(s) * (hi - lo) + lo; }
+// rnd_range(s, -1, 1) in one rounding less work: u * 2^-24 * 2 is exact (power-of-two scalings
+// of a 24-bit integer), so u * 2^-23 - 1 rounds once, at the same add — identical bits.
+__device__ __forceinline__ float rnd_pm1(RngState &s) { return (float)(rng_next(s) >> 8) * 0x1.0p-23f - 1.0f; }
 
 // vec3.rs:181-189 random_unit_vector: rejection in [-1,1)^3, accept 1e-160 < |p|^2 <= 1
 // (1e-160 underflows to 0 in f32: the one intentional f32 deviation).
@@ -116,9 +119,9 @@ __device__ __forceinline__ V3 random_unit_vector(RngState &s, C &cnt) {
     float px, py, pz, lensq;
     for (;;) {
         if constexpr (RRT_PHASE_TIMING == 4) cnt.d2 += wave_slot();
-        px = rnd_range(s, -1.0f, 1.0f);
-        py = rnd_range(s, -1.0f, 1.0f);
-        pz = rnd_range(s, -1.0f, 1.0f);
+        px = rnd_pm1(s);
+        py = rnd_pm1(s);
+        pz = rnd_pm1(s);
         lensq = px * px + py * py + pz * pz;
         if (0.0f < lensq && lensq <= 1.0f) break;
     }
@@ -680,8 +683,8 @@ __device__ __forceinline__ void camera_ray(const KParams &P, uint32_t x, uint32_
     if (P.defocus_radius > 0.0f) {
         float px, py;
         for (;;) {  // vec3.rs:172-179 random_in_unit_disk
-            px = rnd_range(ps.rng, -1.0f, 1.0f);
-            py = rnd_range(ps.rng, -1.0f, 1.0f);
+            px = rnd_pm1(ps.rng);
+            py = rnd_pm1(ps.rng);
             if (px * px + py * py < 1.0f) break;
         }
         origin = v3(P.center[0] + P.disk_u[0] * px + P.disk_v[0] * py,
