@@ -341,6 +341,9 @@ struct Builder {
 struct FlatBvh {
     std::vector<uint8_t> bytes;
     uint32_t n_nodes = 0, n_leaves = 0, max_depth = 0, max_leaf = 0, stack_need = 0, width = 2;
+    // BVH2: every node whose children are both leaves has them adjacent in primitive order
+    // (right.first == left.first + left.count), so the kernel tests the hit ones as one range
+    bool sibling_leaves_adjacent = true;
 };
 
 // Conservative slab test in f32. The kernel's plane distance fma(P, inv, -o*inv) differs from
@@ -430,6 +433,7 @@ FlatBvh flatten2(const Builder &bd, int32_t root) {
             todo.clear();
             child_ref(b.left, lo0, hi0, ref0, cnt0, todo);
             child_ref(b.right, lo1, hi1, ref1, cnt1, todo);
+            if (cnt0 > 0 && cnt1 > 0 && ref1 != ref0 + cnt0) f.sibling_leaves_adjacent = false;
             rrt::GNode &n = out[it.slot];
             n.b0 = make_float4(lo0[0], hi0[0], lo0[1], hi0[1]);
             n.b1 = make_float4(lo0[2], hi0[2], lo1[0], hi1[0]);
@@ -850,6 +854,7 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
         return fail(RRT_E_INVALID, "BVH depth " + std::to_string(fb.max_depth) + " exceeds the LDS stack");
     // postponed leaf tests pack (first primitive, count) as first | count << 28
     if (fb.max_leaf > 15) return fail(RRT_E_INVALID, "leaf size > 15");
+    if (!fb.sibling_leaves_adjacent) return fail(RRT_E_INVALID, "internal: BVH2 sibling leaves not adjacent");
     const uint32_t n_prims = n_spheres + n_quads + n_media;
 
     std::vector<rrt::GMaterial> mats(n_materials);

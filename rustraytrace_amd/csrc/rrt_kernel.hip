@@ -420,14 +420,13 @@ __device__ __forceinline__ void test_prims(const PR &prim_cr, int first, int cou
     }
 }
 
-// Leaf spheres of two ranges [f0, f0+c0) then [f1, f1+c1) in one loop.
+// Leaf primitives [first, first + count): the hit leaf children of one node visit, which are
+// adjacent in primitive order (sibling leaves split one range, rrt_host.cpp flatten2).
 template <bool kCount, class PR>
-__device__ __forceinline__ void test_prims2(const PR &prim_cr, int f0, int c0, int f1, int c1, V3 o,
-                                            V3 d, const RayK &rk, float &closest, int &hit_prim, Counters &cnt) {
+__device__ __forceinline__ void test_range(const PR &prim_cr, int first, int count, V3 o, V3 d, const RayK &rk,
+                                           float &closest, int &hit_prim, Counters &cnt) {
     const float a = rk.a;
-    const int total = c0 + c1;
-    for (int k = 0; k < total; ++k) {
-        const int i = (k < c0) ? f0 + k : f1 + (k - c0);
+    for (int i = first; i < first + count; ++i) {
         if (kCount) cnt.spheres++;
         if constexpr (RRT_PHASE_TIMING == 3) {
             cnt.d0 += wave_slot();
@@ -504,11 +503,9 @@ __device__ __forceinline__ void trav_begin(Trav &t) {
     t.sp = 0;
 }
 
-// A lane's postponed leaf tests: spheres [first0, first0+count0) then [first1, first1+count1),
-// packed first | count << 28 (leaf sizes <= 15, primitive indices < 2^28).
-struct Leaves {
-    uint32_t l0, l1;
-};
+// A lane's postponed leaf tests: primitives [first, first + count), packed first | count << 28
+// (count <= 2 x the largest leaf <= 15, primitive indices < 2^28).
+using Leaves = uint32_t;
 constexpr uint32_t kLeafFirstMask = (1u << 28) - 1u;
 
 // BVH2 node visit with postponed leaf tests: tests both child boxes against the current
@@ -525,10 +522,11 @@ __device__ __forceinline__ bool trav_node(const GNode *__restrict__ nodes, Stack
     float tn0 = 0.0f, tn1 = 0.0f;
     bool h0 = box_hit(n.b0.x, n.b0.y, n.b0.z, n.b0.w, n.b1.x, n.b1.y, rk.inv, rk.oi, 0.001f, t.closest, tn0);
     bool h1 = box_hit(n.b1.z, n.b1.w, n.b2.x, n.b2.y, n.b2.z, n.b2.w, rk.inv, rk.oi, 0.001f, t.closest, tn1);
-    const uint32_t c0 = (h0 && n.link.z > 0) ? (uint32_t)n.link.z : 0u;
-    const uint32_t c1 = (h1 && n.link.w > 0) ? (uint32_t)n.link.w : 0u;
-    lv.l0 = (uint32_t)n.link.x | (c0 << 28);
-    lv.l1 = (uint32_t)n.link.y | (c1 << 28);
+    // leaf counts are >= 0 (0 = internal child); hit leaf children form one range: the left
+    // leaf's primitives are followed by the right leaf's
+    const uint32_t c0 = h0 ? (uint32_t)n.link.z : 0u;
+    const uint32_t c1 = h1 ? (uint32_t)n.link.w : 0u;
+    lv = (c0 ? (uint32_t)n.link.x : (uint32_t)n.link.y) | ((c0 + c1) << 28);
     if (c0) h0 = false;
     if (c1) h1 = false;
     if (h0 && h1) {
@@ -549,47 +547,11 @@ __device__ __forceinline__ bool trav_node(const GNode *__restrict__ nodes, Stack
     return (c0 | c1) != 0;
 }
 
-// The postponed leaf tests of one node visit (leaf 0's spheres, then leaf 1's).
+// The postponed leaf tests of one node visit (leaf 0's primitives, then leaf 1's).
 template <bool kCount, class PR>
-__device__ __forceinline__ void trav_leaves(const PR &prims, const Leaves &lv, V3 o, V3 d,
-                                            const RayK &rk, Trav &t, Counters &cnt) {
-    test_prims2<kCount>(prims, (int)(lv.l0 & kLeafFirstMask), (int)(lv.l0 >> 28), (int)(lv.l1 & kLeafFirstMask),
-                        (int)(lv.l1 >> 28), o, d, rk, t.closest, t.hit_prim, cnt);
-}
-
-// Visits node t.node: tests both children, tests leaf spheres in place, descends into the
-// nearer internal child and pushes the farther one. Returns true when the traversal is done.
-template <bool kCount, typename Stack, class PR>
-__device__ __forceinline__ bool trav_step(const GNode *__restrict__ nodes, const PR &prims,
-                                          Stack &stack, V3 o, V3 d, const RayK &rk, Trav &t, Counters &cnt) {
-    const GNode n = nodes[t.node];
-    if (kCount) { cnt.nodes++; cnt.boxes += 2; }
-    float tn0 = 0.0f, tn1 = 0.0f;
-    bool h0 = box_hit(n.b0.x, n.b0.y, n.b0.z, n.b0.w, n.b1.x, n.b1.y, rk.inv, rk.oi, 0.001f, t.closest, tn0);
-    bool h1 = box_hit(n.b1.z, n.b1.w, n.b2.x, n.b2.y, n.b2.z, n.b2.w, rk.inv, rk.oi, 0.001f, t.closest, tn1);
-    // Leaf children: one loop over leaf 0's spheres then leaf 1's (one divergent loop, not two).
-    const int c0 = (h0 && n.link.z > 0) ? n.link.z : 0;
-    const int c1 = (h1 && n.link.w > 0) ? n.link.w : 0;
-    if (c0 + c1 > 0) {
-        test_prims2<kCount>(prims, n.link.x, c0, n.link.y, c1, o, d, rk, t.closest, t.hit_prim, cnt);
-        if (c0) h0 = false;
-        if (c1) h1 = false;
-    }
-    if (h0 && h1) {
-        const bool first1 = tn1 < tn0;
-        stack.store(t.sp, first1 ? n.link.x : n.link.y);
-        ++t.sp;
-        t.node = first1 ? n.link.y : n.link.x;
-    } else if (h0) {
-        t.node = n.link.x;
-    } else if (h1) {
-        t.node = n.link.y;
-    } else {
-        if (t.sp == 0) return true;
-        --t.sp;
-        t.node = stack.load(t.sp);
-    }
-    return false;
+__device__ __forceinline__ void trav_leaves(const PR &prims, Leaves lv, V3 o, V3 d, const RayK &rk, Trav &t,
+                                            Counters &cnt) {
+    test_range<kCount>(prims, (int)(lv & kLeafFirstMask), (int)(lv >> 28), o, d, rk, t.closest, t.hit_prim, cnt);
 }
 
 // BVH4 step: test the 4 child boxes, test leaf children's spheres in place, then descend
