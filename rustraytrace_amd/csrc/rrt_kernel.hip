@@ -459,14 +459,19 @@ __device__ __forceinline__ void test_range(const PR &prim_cr, int first, int cou
 #endif
         if (disc < 0.0f) continue;
         if constexpr (RRT_PHASE_TIMING == 3) cnt.d2 += 1;
+        // both roots, then selects: the far root is a pure function of (h, sq), so computing it
+        // whether or not the near one is accepted changes nothing, and the select form keeps the
+        // leaf loop free of exec-mask branches and phi copies
         const float sq = __builtin_sqrtf(disc);
-        float root = div_by_a(h - sq, rk);
-        if (!(0.001f < root && root < closest)) {
-            root = div_by_a(h + sq, rk);
-            if (!(0.001f < root && root < closest)) continue;
+        const float r0 = div_by_a(h - sq, rk);
+        const float r1 = div_by_a(h + sq, rk);
+        const bool ok0 = 0.001f < r0 && r0 < closest;
+        const bool ok1 = 0.001f < r1 && r1 < closest;
+        const float root = ok0 ? r0 : r1;
+        if (ok0 || ok1) {
+            closest = root;
+            hit_prim = i;
         }
-        closest = root;
-        hit_prim = i;
     }
 }
 
@@ -1269,8 +1274,9 @@ __device__ __forceinline__ void render_body(const KParams &P) {
                     if (!pend && tr.node < 0) tracing = false;
                 }
                 const uint64_t pm = __ballot(pend);
-                const bool leave = (uint32_t)__popcll(__ballot(tracing)) <= min_active;
-                if (pm != 0 && (leave || (uint32_t)__popcll(pm) > leaf_min || __ballot(tracing && !pend) == 0)) {
+                const uint64_t tm = __ballot(tracing);  // pend implies tracing
+                const bool leave = (uint32_t)__popcll(tm) <= min_active;
+                if (pm != 0 && (leave || (uint32_t)__popcll(pm) > leaf_min || (tm & ~pm) == 0)) {
                     if (pend) {
                         trav_leaves<kCount>(pr, lv, ps.o, ps.d, rk, tr, cnt);
                         pend = false;
