@@ -1250,7 +1250,6 @@ static int32_t render_frame(const RrtCamera *cam, const RrtSphere *spheres, uint
         const size_t row_bytes = rgb8_out ? (size_t)width * 3 : (size_t)width * 16;
         float *d_accum = nullptr;
         uint8_t *d_rgb8 = nullptr;
-        std::vector<uint8_t> host(n_px * (rgb8_out ? 3 : 16));
         hipError_t e = hipMalloc((void **)&d_accum, std::max<size_t>(n_px, 1) * 16);
         if (e == hipSuccess && rgb8_out) e = hipMalloc((void **)&d_rgb8, std::max<size_t>(n_px, 1) * 3);
         if (e != hipSuccess) {
@@ -1268,11 +1267,21 @@ static int32_t render_frame(const RrtCamera *cam, const RrtSphere *spheres, uint
                 rc = RRT_E_HIP;
             }
         }
-        if (!rc) {
+        if (!rc && rows) {
+            // straight into the caller's image: the tile's local bands (band_rows rows each) are
+            // contiguous on both sides, so one strided 2-D copy places every whole band (its
+            // image rows are band * n_ranks + rank) and one plain copy the partial last band
+            const uint8_t *src = rgb8_out ? (const uint8_t *)d_rgb8 : (const uint8_t *)d_accum;
+            uint8_t *dst = rgb8_out ? rgb8_out : reinterpret_cast<uint8_t *>(accum_out);
+            const size_t band_bytes = (size_t)tile.band_rows * row_bytes;
+            const uint32_t whole = rows / tile.band_rows, rest = rows % tile.band_rows;
             e = hipDeviceSynchronize();
-            if (e == hipSuccess)
-                e = hipMemcpy(host.data(), rgb8_out ? (const void *)d_rgb8 : (const void *)d_accum, host.size(),
-                              hipMemcpyDeviceToHost);
+            if (e == hipSuccess && whole)
+                e = hipMemcpy2D(dst + (size_t)tile.rank * band_bytes, band_bytes * tile.n_ranks, src, band_bytes,
+                                band_bytes, whole, hipMemcpyDeviceToHost);
+            if (e == hipSuccess && rest)
+                e = hipMemcpy(dst + ((size_t)whole * tile.n_ranks + tile.rank) * band_bytes,
+                              src + (size_t)whole * band_bytes, (size_t)rest * row_bytes, hipMemcpyDeviceToHost);
             if (e != hipSuccess) {
                 g_err = std::string("render failed: ") + hipGetErrorString(e);
                 rc = RRT_E_HIP;
@@ -1282,12 +1291,6 @@ static int32_t render_frame(const RrtCamera *cam, const RrtSphere *spheres, uint
         (void)hipFree(d_rgb8);
         rrt_scene_destroy(scene);
         if (rc) return set_err(rc);
-        uint8_t *dst = rgb8_out ? rgb8_out : reinterpret_cast<uint8_t *>(accum_out);
-        for (uint32_t lr = 0; lr < rows; ++lr) {
-            const uint32_t band = lr / tile.band_rows;
-            const uint32_t y = (band * tile.n_ranks + tile.rank) * tile.band_rows + lr % tile.band_rows;
-            std::memcpy(dst + (size_t)y * row_bytes, host.data() + (size_t)lr * row_bytes, row_bytes);
-        }
         const uint32_t d = ++done;
         if (!(flags & RRT_FLAG_QUIET)) {
             std::lock_guard<std::mutex> lk(mu);
