@@ -29,7 +29,7 @@ extern "C" {
 /* 1: book 1; 2: RrtSceneExt (motion, Perlin), kinds 5-6; 3: quads, constant-density media and
  * book-3 light lists in RrtSceneExt, kind 7, RRT_FLAG_BOOK3, rrt_build_next_week_scene /
  * rrt_build_rest_of_your_life_scene with struct outputs. */
-#define RRT_ABI_VERSION 3u
+#define RRT_ABI_VERSION 4u
 
 /* ---- scene ABI (== src/gpu/mod.rs:13-42) ------------------------------------------ */
 
@@ -301,15 +301,20 @@ typedef struct RrtBvhInfo {
     uint32_t max_leaf_size;
     uint64_t node_bytes;
     uint64_t prim_bytes;
-    uint32_t width;          /* 2: 64-B binary nodes, 4: 128-B 4-wide nodes */
+    uint32_t width;          /* 2: binary nodes, 4: 128-B 4-wide nodes */
     uint32_t max_leaf_param; /* leaf size the builder was asked for */
+    uint32_t node_stride;    /* bytes per node: 80 (BVH2 staged in LDS: sign-ordered planes), 64 (BVH2 read
+                                from global memory), 128 (BVH4); layouts in DESIGN.md */
+    uint32_t _pad;
 } RrtBvhInfo;
 int32_t rrt_scene_bvh_info(const RrtScene *scene, RrtBvhInfo *out);
 
 /* Host-only: the BVH rrt_scene_create would build for these spheres (width / max_leaf 0 =
- * the defaults), as the device node array (64-B BVH2 or 128-B BVH4 nodes, layout in
- * DESIGN.md) and the leaf-order permutation of the spheres. Call with nodes_cap 0 to size
- * (info->node_bytes). Lets a checker walk exactly the tree the kernel walks. */
+ * the defaults; max_leaf <= 7 for width 2, <= 15 for width 4), as the device node array (80-B or
+ * 64-B BVH2 nodes — info->node_stride, the layout scene creation picks — or 128-B BVH4 nodes,
+ * layouts in DESIGN.md) and the leaf-order permutation of the spheres.
+ * Call with nodes_cap 0 to size (info->node_bytes). Lets a checker walk exactly the tree the
+ * kernel walks. */
 int32_t rrt_build_bvh(const RrtSphere *spheres, uint32_t n_spheres, uint32_t width, uint32_t max_leaf,
                       void *nodes_out, size_t nodes_cap, uint32_t *prim_order_out, RrtBvhInfo *info);
 /* The same over the book-2 scene (ext may be NULL): a moving sphere's box spans both ends of its

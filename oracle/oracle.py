@@ -169,9 +169,13 @@ def render(scene, mode=TWIN, rows=None, samples=None, threads=1, chunk=DEFAULT_C
     return accum, rays.value, tests.value
 
 
-def render_kbvh(scene, nodes, order, width, rows=None, samples=None, threads=1, chunk=DEFAULT_CHUNK):
+def render_kbvh(scene, nodes, order, layout, rows=None, samples=None, threads=1, chunk=DEFAULT_CHUNK):
     """TWIN arithmetic, closest hits by walking the kernel's own BVH in the kernel's order
-    (nodes/order from rustraytrace_amd.render.build_bvh). Same return as render()."""
+    (nodes/order/info from rustraytrace_amd.render.build_bvh; `layout` = that info dict, or the
+    node stride in bytes: 80 / 64 BVH2, 128 BVH4). Same return as render()."""
+    stride = int(layout["node_stride"]) if isinstance(layout, dict) else int(layout)
+    if stride not in (64, 80, 128):
+        raise ValueError(f"render_kbvh: node stride {stride} (pass build_bvh's info dict)")
     lib = load()
     W, H = int(scene.camera["params_f"][0, 1]), int(scene.camera["params_f"][0, 2])
     spp = max(int(scene.camera["params_f"][0, 3]), 1)
@@ -185,12 +189,12 @@ def render_kbvh(scene, nodes, order, width, rows=None, samples=None, threads=1, 
         tex[i].height, tex[i].width = t.shape[0], t.shape[1]
     nodes = np.ascontiguousarray(nodes, dtype=np.uint8)
     order = np.ascontiguousarray(order, dtype=np.uint32)
-    n_nodes = nodes.size // (64 if width == 2 else 128)
+    n_nodes = nodes.size // stride
     rays, tests = c_uint64(0), c_uint64(0)
     ext, keep_ext = _ext(scene)
     rc = lib.oracle_render_kbvh(_p(scene.camera), _p(scene.spheres), len(scene.spheres), _p(scene.materials),
                                 len(scene.materials), ctypes.cast(tex, c_void_p) if keep else None, len(keep), ext,
-                                int(scene.flags), _p(nodes), n_nodes, int(width), _p(order), y0, y1, s0, s1,
+                                int(scene.flags), _p(nodes), n_nodes, stride, _p(order), y0, y1, s0, s1,
                                 int(threads), _p(accum), ctypes.byref(rays), ctypes.byref(tests), int(chunk))
     del keep_ext
     if rc != 0:

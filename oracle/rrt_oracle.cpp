@@ -626,6 +626,7 @@ template <class T> struct World {
 // where the closest-hit winner depends on BVH topology (near-ties and grazing rays).
 struct KTree {
     uint32_t width = 0;
+    uint32_t stride = 0;  // bytes per node: 80 or 64 (BVH2), 128 (BVH4)
     const uint8_t *nodes = nullptr;
     uint32_t n_nodes = 0;
     const uint32_t *order = nullptr;  // leaf-order primitive -> original sphere index
@@ -688,12 +689,26 @@ bool kbvh_hit(const World<float> &w, const KTree &kt, Vec3<float> o, Vec3<float>
     int32_t node = 0;
     for (;;) {
         if (kt.width == 2) {
-            const float *f = reinterpret_cast<const float *>(kt.nodes + (size_t)node * 64);
-            const int32_t *l = reinterpret_cast<const int32_t *>(kt.nodes + (size_t)node * 64 + 48);
+            // BVH2 nodes (rrt_internal.h), links = node index, or first | count << 28:
+            //   80 B (LDS): per child lo, hi, lo for x, y, z (9 floats), then the two links; the
+            //        kernel reads each axis' (entry, exit) pair by the sign of 1/d, which takes
+            //        the same decisions as min/max over (lo, hi) here;
+            //   64 B (global): c0 lo.x hi.x lo.y hi.y lo.z hi.z, c1 the same, links, 2 unused.
+            const uint8_t *nb = kt.nodes + (size_t)node * kt.stride;
+            const float *f = reinterpret_cast<const float *>(nb);
+            const bool ordered = kt.stride == 80;
+            const uint32_t *lk = reinterpret_cast<const uint32_t *>(nb + (ordered ? 72 : 48));
+            const int32_t l[4] = {(int32_t)(lk[0] & 0x0fffffffu), (int32_t)(lk[1] & 0x0fffffffu), (int32_t)(lk[0] >> 28),
+                                  (int32_t)(lk[1] >> 28)};
             float tn0 = 0.0f, tn1 = 0.0f;
             bool h0, h1;
-            KBOX(f[0], f[1], f[2], f[3], f[4], f[5], r, kTmin, closest, tn0, h0);
-            KBOX(f[6], f[7], f[8], f[9], f[10], f[11], r, kTmin, closest, tn1, h1);
+            if (ordered) {
+                KBOX(f[0], f[1], f[3], f[4], f[6], f[7], r, kTmin, closest, tn0, h0);
+                KBOX(f[9], f[10], f[12], f[13], f[15], f[16], r, kTmin, closest, tn1, h1);
+            } else {
+                KBOX(f[0], f[1], f[2], f[3], f[4], f[5], r, kTmin, closest, tn0, h0);
+                KBOX(f[6], f[7], f[8], f[9], f[10], f[11], r, kTmin, closest, tn1, h1);
+            }
             if (h0 && l[2] > 0) { leaf(l[0], l[2]); h0 = false; }
             if (h1 && l[3] > 0) { leaf(l[1], l[3]); h1 = false; }
             if (h0 && h1) {
@@ -1484,15 +1499,17 @@ int oracle_render(const RrtCamera *cam, const RrtSphere *s, uint32_t n, const Rr
 }
 
 // mode 2 = KBVH: TWIN arithmetic, but closest hits found by walking the kernel's BVH
-// (rrt_build_bvh output: `nodes` of n_nodes x 64 B (width 2) or 128 B (width 4), `order`).
+// (rrt_build_bvh output: `nodes` of n_nodes x node_stride B (80 or 64: BVH2, 128: BVH4), `order`).
 int oracle_render_kbvh(const RrtCamera *cam, const RrtSphere *s, uint32_t n, const RrtMaterial *m, uint32_t nm,
                        const RrtTexture *tex, uint32_t ntex, const RrtSceneExt *ext, uint32_t flags, const void *nodes,
                        uint32_t n_nodes,
                        uint32_t width, const uint32_t *order, uint32_t y0, uint32_t y1, uint32_t s0, uint32_t s1,
                        int threads, double *accum, uint64_t *rays, uint64_t *sphere_tests, uint32_t chunk) {
-    if (!cam || !accum || !nodes || (width != 2 && width != 4)) return -1;
+    // `width` is the node stride in bytes: 80 / 64 (BVH2 layouts), 128 (BVH4)
+    if (!cam || !accum || !nodes || (width != 64 && width != 80 && width != 128)) return -1;
     KTree kt;
-    kt.width = width;
+    kt.width = width == 128 ? 4 : 2;
+    kt.stride = width;
     kt.nodes = static_cast<const uint8_t *>(nodes);
     kt.n_nodes = n_nodes;
     kt.order = order;

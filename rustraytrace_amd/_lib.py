@@ -167,10 +167,12 @@ class RrtBvhInfo(ctypes.Structure):
         ("prim_bytes", c_uint64),
         ("width", c_uint32),
         ("max_leaf_param", c_uint32),
+        ("node_stride", c_uint32),
+        ("_pad", c_uint32),
     ]
 
     def as_dict(self):
-        return {k: int(getattr(self, k)) for k, _ in self._fields_}
+        return {k: int(getattr(self, k)) for k, _ in self._fields_ if not k.startswith("_")}
 
 
 class RrtError(RuntimeError):

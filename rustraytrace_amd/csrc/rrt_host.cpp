@@ -341,6 +341,7 @@ struct Builder {
 struct FlatBvh {
     std::vector<uint8_t> bytes;
     uint32_t n_nodes = 0, n_leaves = 0, max_depth = 0, max_leaf = 0, stack_need = 0, width = 2;
+    uint32_t stride = 0;  // bytes per node: 80 (BVH2, sign-ordered, LDS), 64 (BVH2, global), 128 (BVH4)
     // BVH2: every node whose children are both leaves has them adjacent in primitive order
     // (right.first == left.first + left.count), so the kernel tests the hit ones as one range
     bool sibling_leaves_adjacent = true;
@@ -385,11 +386,34 @@ Aabb never_hit_box() {
     return b;
 }
 
-// BVH2: the binary tree as is, root = node 0, both child boxes stored in the parent.
+void put_node2(rrt::GNode &n, const float *lo0, const float *hi0, const float *lo1, const float *hi1, int32_t ref0,
+               int32_t cnt0, int32_t ref1, int32_t cnt1) {
+    const float *lo[2] = {lo0, lo1}, *hi[2] = {hi0, hi1};
+    for (int c = 0; c < 2; ++c)
+        for (int a = 0; a < 3; ++a) {
+            n.box[c][3 * a] = lo[c][a];
+            n.box[c][3 * a + 1] = hi[c][a];
+            n.box[c][3 * a + 2] = lo[c][a];
+        }
+    n.link[0] = (uint32_t)ref0 | ((uint32_t)cnt0 << rrt::kLinkCountShift);
+    n.link[1] = (uint32_t)ref1 | ((uint32_t)cnt1 << rrt::kLinkCountShift);
+}
+void put_node2(rrt::GNodeG &n, const float *lo0, const float *hi0, const float *lo1, const float *hi1, int32_t ref0,
+               int32_t cnt0, int32_t ref1, int32_t cnt1) {
+    n.b0 = make_float4(lo0[0], hi0[0], lo0[1], hi0[1]);
+    n.b1 = make_float4(lo0[2], hi0[2], lo1[0], hi1[0]);
+    n.b2 = make_float4(lo1[1], hi1[1], lo1[2], hi1[2]);
+    n.link = make_uint4((uint32_t)ref0 | ((uint32_t)cnt0 << rrt::kLinkCountShift),
+                        (uint32_t)ref1 | ((uint32_t)cnt1 << rrt::kLinkCountShift), 0u, 0u);
+}
+
+// BVH2: the binary tree as is, root = node 0, both child boxes stored in the parent; Node =
+// rrt::GNode (80 B, sign-ordered planes, LDS) or rrt::GNodeG (64 B, global memory).
+template <class Node>
 FlatBvh flatten2(const Builder &bd, int32_t root) {
     FlatBvh f;
     const BoxSlack slack(bd.bin[root].box);
-    std::vector<rrt::GNode> out;
+    std::vector<Node> out;
     struct Item { int32_t bin; int32_t slot; };
     auto child_ref = [&](int32_t c, float *lo, float *hi, int32_t &ref, int32_t &cnt, std::vector<Item> &todo) {
         const Builder::BNode &b = bd.bin[c];
@@ -402,12 +426,12 @@ FlatBvh flatten2(const Builder &bd, int32_t root) {
         } else {
             ref = (int32_t)out.size();
             cnt = 0;
-            out.push_back(rrt::GNode{});
+            out.push_back(Node{});
             todo.push_back(Item{c, ref});
         }
     };
     std::vector<std::pair<Item, uint32_t>> stack;  // (item, depth)
-    out.push_back(rrt::GNode{});
+    out.push_back(Node{});
     std::vector<Item> todo;
     const Builder::BNode &r = bd.bin[root];
     if (r.leaf) {  // whole scene in one leaf: child 0 = the leaf, child 1 = never hit
@@ -415,11 +439,7 @@ FlatBvh flatten2(const Builder &bd, int32_t root) {
         int32_t ref0, cnt0;
         child_ref(root, lo0, hi0, ref0, cnt0, todo);
         put_box(lo1, hi1, never_hit_box(), nullptr);
-        rrt::GNode &n = out[0];
-        n.b0 = make_float4(lo0[0], hi0[0], lo0[1], hi0[1]);
-        n.b1 = make_float4(lo0[2], hi0[2], lo1[0], hi1[0]);
-        n.b2 = make_float4(lo1[1], hi1[1], lo1[2], hi1[2]);
-        n.link = make_int4(ref0, 0, cnt0, 0);
+        put_node2(out[0], lo0, hi0, lo1, hi1, ref0, cnt0, 0, 0);
         f.max_depth = 1;
     } else {
         stack.push_back({Item{root, 0}, 0});
@@ -434,18 +454,15 @@ FlatBvh flatten2(const Builder &bd, int32_t root) {
             child_ref(b.left, lo0, hi0, ref0, cnt0, todo);
             child_ref(b.right, lo1, hi1, ref1, cnt1, todo);
             if (cnt0 > 0 && cnt1 > 0 && ref1 != ref0 + cnt0) f.sibling_leaves_adjacent = false;
-            rrt::GNode &n = out[it.slot];
-            n.b0 = make_float4(lo0[0], hi0[0], lo0[1], hi0[1]);
-            n.b1 = make_float4(lo0[2], hi0[2], lo1[0], hi1[0]);
-            n.b2 = make_float4(lo1[1], hi1[1], lo1[2], hi1[2]);
-            n.link = make_int4(ref0, ref1, cnt0, cnt1);
+            put_node2(out[it.slot], lo0, hi0, lo1, hi1, ref0, cnt0, ref1, cnt1);
             for (auto &t : todo) stack.push_back({t, depth + 1});
         }
     }
     f.n_nodes = (uint32_t)out.size();
     f.stack_need = f.max_depth + 1;
     f.width = 2;
-    f.bytes.resize(out.size() * sizeof(rrt::GNode));
+    f.stride = (uint32_t)sizeof(Node);
+    f.bytes.resize(out.size() * sizeof(Node));
     std::memcpy(f.bytes.data(), out.data(), f.bytes.size());
     return f;
 }
@@ -525,6 +542,7 @@ FlatBvh flatten4(const Builder &bd, int32_t root) {
     f.n_nodes = (uint32_t)out.size();
     f.stack_need = 3 * f.max_depth + 1;  // <= 3 pushes per level
     f.width = 4;
+    f.stride = (uint32_t)sizeof(rrt::GNode4);
     f.bytes.resize(out.size() * sizeof(rrt::GNode4));
     std::memcpy(f.bytes.data(), out.data(), f.bytes.size());
     return f;
@@ -537,6 +555,7 @@ void bvh_defaults(uint32_t &width, uint32_t &max_leaf) {
     if (const char *e = std::getenv("RRT_MAX_LEAF")) max_leaf = (uint32_t)std::min(15, std::max(1, std::atoi(e)));
     width = 2;
     if (const char *e = std::getenv("RRT_BVH_WIDTH")) width = std::atoi(e) == 4 ? 4 : 2;
+    if (width == 2) max_leaf = std::min(max_leaf, rrt::kMaxLeafPrims);
 }
 
 // Quad::set_bounding_box (quad.rs:43-47): the box of the four corners, padded.
@@ -577,8 +596,18 @@ struct ExtView {
 // constant_medium.rs bounding_box), SAH build, flatten. Primitives: spheres, then quads
 // (n_spheres + j), then media (n_spheres + n_quads + m). order[i] = original index of the i-th
 // primitive in leaf order. The medium ranges are validated by the caller.
+// Whether nodes + primitive records (+ motion for book-2 kernels) are staged in LDS per block
+// (RRT_SCENE_IN_LDS=0 forces global memory).
+bool scene_lds_fit(size_t node_bytes, size_t n_prims, bool book2) {
+    if (const char *e = std::getenv("RRT_SCENE_IN_LDS"))
+        if (std::atoi(e) == 0) return false;
+    return node_bytes + n_prims * (rrt::kPrimBytes + (book2 ? rrt::kMotionBytes : 0)) <= rrt::kLdsSceneBudget;
+}
+
+// BVH2 node layout: the sign-ordered 80-B nodes when `lds_fit(bytes of those nodes)` says the
+// scene will be staged in LDS, else the 64-B global-memory nodes.
 FlatBvh build_bvh(const RrtSphere *spheres, uint32_t n_spheres, const ExtView &ex, uint32_t width,
-                  uint32_t max_leaf, std::vector<uint32_t> &order) {
+                  uint32_t max_leaf, std::vector<uint32_t> &order, const std::function<bool(size_t)> &lds_fit) {
     const float *motion = ex.motion;
     const uint32_t n_quads = ex.n_quads;
     std::vector<Aabb> boxes(n_spheres + (size_t)n_quads + ex.n_media);
@@ -618,10 +647,13 @@ FlatBvh build_bvh(const RrtSphere *spheres, uint32_t n_spheres, const ExtView &e
         empty.box = never_hit_box();
         empty.leaf = true;
         bld.bin.push_back(empty);
-        fb = width == 4 ? flatten4(bld, 0) : flatten2(bld, 0);
+    }
+    const int32_t root = n_prims == 0 ? 0 : bld.build(0, n_prims);
+    if (width == 4) {
+        fb = flatten4(bld, root);
     } else {
-        const int32_t root = bld.build(0, n_prims);
-        fb = width == 4 ? flatten4(bld, root) : flatten2(bld, root);
+        fb = flatten2<rrt::GNode>(bld, root);
+        if (!lds_fit(fb.bytes.size())) fb = flatten2<rrt::GNodeG>(bld, root);
     }
     order = bld.objs;
     return fb;
@@ -849,11 +881,13 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
         (uint64_t)n_quads + ex.n_bquads + ex.n_lights >= (1u << 24))
         return fail(RRT_E_INVALID, ">= 2^24 primitives or quads");
     if (!has_motion) ex.motion = nullptr;
-    const FlatBvh fb = build_bvh(spheres, n_spheres, ex, width, max_leaf, order);
+    const size_t n_prims_all = (size_t)n_spheres + n_quads + n_media;
+    const FlatBvh fb = build_bvh(spheres, n_spheres, ex, width, max_leaf, order,
+                                 [&](size_t nb) { return scene_lds_fit(nb, n_prims_all, book2); });
     if (fb.stack_need > (uint32_t)rrt::kMaxStackDepth)
         return fail(RRT_E_INVALID, "BVH depth " + std::to_string(fb.max_depth) + " exceeds the LDS stack");
     // postponed leaf tests pack (first primitive, count) as first | count << 28
-    if (fb.max_leaf > 15) return fail(RRT_E_INVALID, "leaf size > 15");
+    if (fb.max_leaf > (fb.width == 2 ? rrt::kMaxLeafPrims : 15u)) return fail(RRT_E_INVALID, "leaf size too large");
     if (!fb.sibling_leaves_adjacent) return fail(RRT_E_INVALID, "internal: BVH2 sibling leaves not adjacent");
     const uint32_t n_prims = n_spheres + n_quads + n_media;
 
@@ -1034,10 +1068,9 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
     p.n_prims = n_prims;
     p.stack_depth = fb.stack_need;
     p.bvh_width = fb.width;
-    const size_t scene_bytes =
-        fb.bytes.size() + (size_t)n_prims * (rrt::kPrimBytes + (book2 ? rrt::kMotionBytes : 0));
-    p.scene_in_lds = scene_bytes <= rrt::kLdsSceneBudget;
-    if (const char *e = std::getenv("RRT_SCENE_IN_LDS")) p.scene_in_lds = p.scene_in_lds && std::atoi(e) != 0;
+    // BVH2: the node layout already encodes the choice (80-B sign-ordered nodes are the LDS ones)
+    p.scene_in_lds = fb.width == 2 ? fb.stride == (uint32_t)sizeof(rrt::GNode)
+                                   : scene_lds_fit(fb.bytes.size(), n_prims, book2);
     p.trav_frac = 32;
     p.leaf_frac = 32;
     p.min_waves = 6;
@@ -1059,6 +1092,7 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
     bi.max_depth = fb.max_depth;
     bi.max_leaf_size = fb.max_leaf;
     bi.node_bytes = fb.bytes.size();
+    bi.node_stride = fb.stride;
     bi.width = fb.width;
     bi.max_leaf_param = max_leaf;
     bi.prim_bytes = (uint64_t)n_prims * (rrt::kPrimBytes + (book2 ? rrt::kMotionBytes : 0)) +
@@ -1102,9 +1136,15 @@ int32_t rrt_build_bvh_ex(const RrtSphere *spheres, uint32_t n_spheres, const Rrt
     bvh_defaults(dw, dl);
     if (width == 0) width = dw;
     if (max_leaf == 0) max_leaf = dl;
-    if ((width != 2 && width != 4) || max_leaf > 15) return fail(RRT_E_INVALID, "width must be 2 or 4, max_leaf <= 15");
+    if ((width != 2 && width != 4) || max_leaf > (width == 2 ? rrt::kMaxLeafPrims : 15u))
+        return fail(RRT_E_INVALID, "width must be 2 or 4, max_leaf <= 7 (width 2) or 15 (width 4)");
     std::vector<uint32_t> order;
-    const FlatBvh fb = build_bvh(spheres, n_spheres, ex, width, max_leaf, order);
+    // the layout scene creation would pick (its book-2 test also counts book-2 materials; either
+    // layout holds the same tree and boxes, so a checker walks the same decisions)
+    const bool book2 = ex.motion || ex.n_quads || ex.n_media;
+    const size_t n_prims_all = (size_t)n_spheres + ex.n_quads + ex.n_media;
+    const FlatBvh fb = build_bvh(spheres, n_spheres, ex, width, max_leaf, order,
+                                 [&](size_t nb) { return scene_lds_fit(nb, n_prims_all, book2); });
     if (info) {
         *info = RrtBvhInfo{};
         info->n_nodes = fb.n_nodes;
@@ -1112,7 +1152,7 @@ int32_t rrt_build_bvh_ex(const RrtSphere *spheres, uint32_t n_spheres, const Rrt
         info->max_depth = fb.max_depth;
         info->max_leaf_size = fb.max_leaf;
         info->node_bytes = fb.bytes.size();
-        const bool book2 = ex.motion || ex.n_quads || ex.n_media;
+        info->node_stride = fb.stride;
         info->prim_bytes = (uint64_t)order.size() * (rrt::kPrimBytes + (book2 ? rrt::kMotionBytes : 0)) +
                            ((uint64_t)ex.n_quads + ex.n_bquads) * sizeof(rrt::GQuad) +
                            (uint64_t)ex.n_media * sizeof(rrt::GMedium);

@@ -7,21 +7,34 @@
 
 namespace rrt {
 
-// BVH2 node, 64 B, both children's boxes stored in the parent so one node fetch
-// (4 x dwordx4) tests both children. Boxes are f32, rounded outward from the f64
-// SAH build (bvh.rs:21-156 criterion) so they conservatively contain the spheres.
+// BVH2 node, 80 B, both children's boxes stored in the parent so one node visit reads one
+// record. Boxes are f32 rounded outward (and grown by the slab test's rounding bound, rrt_host.cpp
+// BoxSlack) from the f64 SAH build. Each axis is stored lo, hi, lo: a ray whose 1/d_a is negative
+// reads its (entry, exit) plane pair at offset 1 (hi, lo), otherwise at 0 (lo, hi), so the slab
+// test takes no min/max per axis. Links: a child node index (count 0), or for a leaf its first
+// primitive | count << 28 — which is also the postponed-leaf record the kernel keeps.
+struct alignas(16) GNode {
+    float box[2][9];    // child c, axis a: lo, hi, lo at [c][3a .. 3a+2] (f32, rounded outward)
+    uint32_t link[2];   // child c: node index (internal), or first primitive | count << 28 (leaf)
+};
+static_assert(sizeof(GNode) == 80, "GNode must be 80 B");
+// The same node in 64 B, for scenes read from global memory (beyond the LDS budget): an 80-B
+// node straddles 128-B cache lines and costs a fifth load (C5 -23 %), so there both children's
+// boxes are packed lo, hi per axis and the slab test takes min/max.
 //   b0 = c0.lo.x c0.hi.x c0.lo.y c0.hi.y
 //   b1 = c0.lo.z c0.hi.z c1.lo.x c1.hi.x
 //   b2 = c1.lo.y c1.hi.y c1.lo.z c1.hi.z
-//   link.x/.y = child ref (internal: node index; leaf: first primitive)
-//   link.z/.w = child primitive count (0 = internal node)
-struct alignas(16) GNode {
+//   link.x/.y = child link (as GNode::link), link.z/.w unused (0)
+struct alignas(16) GNodeG {
     float4 b0;
     float4 b1;
     float4 b2;
-    int4 link;
+    uint4 link;
 };
-static_assert(sizeof(GNode) == 64, "GNode must be 64 B");
+static_assert(sizeof(GNodeG) == 64, "GNodeG must be 64 B");
+constexpr uint32_t kLinkCountShift = 28;
+constexpr uint32_t kLinkFirstMask = (1u << kLinkCountShift) - 1u;
+constexpr uint32_t kMaxLeafPrims = 7;  // two leaf children's counts share one 4-bit field
 
 // BVH4 node, 128 B: the boxes of 4 children as SoA float4s (child c in component c), the
 // child refs and primitive counts (0 = internal node). Collapsed from the binary SAH tree.

@@ -213,6 +213,21 @@ __device__ __forceinline__ bool box_hit(float lx, float hx, float ly, float hy, 
     return nr < fr;
 }
 
+// box_hit on planes given in (entry, exit) order per axis (GNode's lo, hi, lo layout read at
+// the ray's sign offsets): fma is monotonic in P for a fixed multiplier, so the entry plane's
+// distance is exactly min(t_lo, t_hi) and the exit plane's exactly the max — the same values
+// and decisions as box_hit, without its six min/max.
+__device__ __forceinline__ bool box_hit_ordered(float nx, float fx, float ny, float fy, float nz, float fz, V3 inv,
+                                                V3 oi, float tmin, float tmax, float &tnear) {
+    const float x0 = __builtin_fmaf(nx, inv.x, -oi.x), x1 = __builtin_fmaf(fx, inv.x, -oi.x);
+    const float y0 = __builtin_fmaf(ny, inv.y, -oi.y), y1 = __builtin_fmaf(fy, inv.y, -oi.y);
+    const float z0 = __builtin_fmaf(nz, inv.z, -oi.z), z1 = __builtin_fmaf(fz, inv.z, -oi.z);
+    const float nr = __builtin_fmaxf(__builtin_fmaxf(x0, y0), __builtin_fmaxf(z0, tmin));
+    const float fr = __builtin_fminf(__builtin_fminf(x1, y1), __builtin_fminf(z1, tmax));
+    tnear = nr;
+    return nr < fr;
+}
+
 // Per-lane work counts of the instrumented (counting) kernel variant (+ debug statistics).
 struct Counters {
     uint32_t nodes, boxes, spheres;
@@ -227,6 +242,9 @@ struct RayK {
     V3 oi;     // o * inv
     float a;
     float ra;  // refined reciprocal of a (0 when a is outside [2^-64, 2^64])
+    // byte offsets of the ray's (entry, exit) plane pair of each axis in a GNode child box:
+    // 12a + 4 when 1/d_a < 0 (hi, lo), else 12a (lo, hi)
+    uint32_t ox, oy, oz;
 };
 
 // minNum / maxNum semantics (a NaN direction gives +2^64, as in the oracle's std::fmin/fmax)
@@ -239,6 +257,9 @@ __device__ __forceinline__ RayK ray_consts(V3 o, V3 d) {
     // is NaN or -inf, and a slab that straddles o (lo < 0 < hi about o's sign) rejects the ray.
     r.inv = v3(clamp_inv(1.0f / d.x), clamp_inv(1.0f / d.y), clamp_inv(1.0f / d.z));
     r.oi = v3(o.x * r.inv.x, o.y * r.inv.y, o.z * r.inv.z);
+    r.ox = r.inv.x < 0.0f ? 4u : 0u;
+    r.oy = r.inv.y < 0.0f ? 16u : 12u;
+    r.oz = r.inv.z < 0.0f ? 28u : 24u;
     r.a = dot(d, d);                                  // sphere.rs:27, hoisted per ray
     // The reciprocal step of the IEEE f32 division expansion (v_rcp + one Newton step), done
     // once per ray instead of in every root division (div_by_a).
@@ -509,9 +530,8 @@ __device__ __forceinline__ void trav_begin(Trav &t) {
 }
 
 // A lane's postponed leaf tests: primitives [first, first + count), packed first | count << 28
-// (count <= 2 x the largest leaf <= 15, primitive indices < 2^28).
+// like a GNode leaf link (count <= 2 x kMaxLeafPrims = 14, primitive indices < 2^28).
 using Leaves = uint32_t;
-constexpr uint32_t kLeafFirstMask = (1u << 28) - 1u;
 
 // BVH2 node visit with postponed leaf tests: tests both child boxes against the current
 // closest hit, records leaf children in `lv` (tested later, before this lane's next node
@@ -519,30 +539,52 @@ constexpr uint32_t kLeafFirstMask = (1u << 28) - 1u;
 // when nothing is left to visit. The next node depends only on these box results, so
 // testing the leaves later keeps every ray's sequence of operations unchanged. Returns
 // true when leaf tests are pending.
-template <bool kCount, typename Stack>
-__device__ __forceinline__ bool trav_node(const GNode *__restrict__ nodes, Stack &stack, const RayK &rk, Trav &t,
+template <bool kCount, typename Node, typename Stack>
+__device__ __forceinline__ bool trav_node(const Node *__restrict__ nodes, Stack &stack, const RayK &rk, Trav &t,
                                           Leaves &lv, Counters &cnt) {
-    const GNode n = nodes[t.node];
     if (kCount) { cnt.nodes++; cnt.boxes += 2; }
     float tn0 = 0.0f, tn1 = 0.0f;
-    bool h0 = box_hit(n.b0.x, n.b0.y, n.b0.z, n.b0.w, n.b1.x, n.b1.y, rk.inv, rk.oi, 0.001f, t.closest, tn0);
-    bool h1 = box_hit(n.b1.z, n.b1.w, n.b2.x, n.b2.y, n.b2.z, n.b2.w, rk.inv, rk.oi, 0.001f, t.closest, tn1);
-    // leaf counts are >= 0 (0 = internal child); hit leaf children form one range: the left
-    // leaf's primitives are followed by the right leaf's
-    const uint32_t c0 = h0 ? (uint32_t)n.link.z : 0u;
-    const uint32_t c1 = h1 ? (uint32_t)n.link.w : 0u;
-    lv = (c0 ? (uint32_t)n.link.x : (uint32_t)n.link.y) | ((c0 + c1) << 28);
+    bool h0, h1;
+    uint32_t l0, l1;
+    if constexpr (std::is_same<Node, GNode>::value) {
+        // node * 80 as a 24-bit multiply (full rate; node indices < 2^24)
+        const GNode &n = *reinterpret_cast<const GNode *>(reinterpret_cast<const char *>(nodes) +
+                                                           __umul24((uint32_t)t.node, (uint32_t)sizeof(GNode)));
+        // LDS: each plane pair read at the ray's sign offset (ds_read2_b32), no min/max
+        const char *bx = reinterpret_cast<const char *>(&n.box[0][0]);
+        auto plane = [&](uint32_t byte_off) { return *reinterpret_cast<const float *>(bx + byte_off); };
+        h0 = box_hit_ordered(plane(rk.ox), plane(rk.ox + 4), plane(rk.oy), plane(rk.oy + 4), plane(rk.oz),
+                             plane(rk.oz + 4), rk.inv, rk.oi, 0.001f, t.closest, tn0);
+        h1 = box_hit_ordered(plane(rk.ox + 36), plane(rk.ox + 40), plane(rk.oy + 36), plane(rk.oy + 40),
+                             plane(rk.oz + 36), plane(rk.oz + 40), rk.inv, rk.oi, 0.001f, t.closest, tn1);
+        l0 = n.link[0];
+        l1 = n.link[1];
+    } else {
+        // global memory (scenes beyond the LDS budget): the 64-B node in four 16-B loads and the
+        // min/max slab (per-lane dword gathers cost more there than the min/max)
+        const GNodeG n = nodes[t.node];
+        h0 = box_hit(n.b0.x, n.b0.y, n.b0.z, n.b0.w, n.b1.x, n.b1.y, rk.inv, rk.oi, 0.001f, t.closest, tn0);
+        h1 = box_hit(n.b1.z, n.b1.w, n.b2.x, n.b2.y, n.b2.z, n.b2.w, rk.inv, rk.oi, 0.001f, t.closest, tn1);
+        l0 = n.link.x;
+        l1 = n.link.y;
+    }
+    // Leaf children (count in the link's top bits, 0 = internal) are postponed; the hit ones
+    // form one range: sibling leaves are adjacent in primitive order, so l0's first primitive
+    // continues into l1's.
+    const uint32_t c0 = h0 ? (l0 >> kLinkCountShift) : 0u;
+    const uint32_t c1 = h1 ? (l1 >> kLinkCountShift) : 0u;
+    lv = c0 ? l0 + (c1 << kLinkCountShift) : l1;
     if (c0) h0 = false;
     if (c1) h1 = false;
     if (h0 && h1) {
         const bool first1 = tn1 < tn0;
-        stack.store(t.sp, first1 ? n.link.x : n.link.y);
+        stack.store(t.sp, first1 ? (int)l0 : (int)l1);
         ++t.sp;
-        t.node = first1 ? n.link.y : n.link.x;
+        t.node = first1 ? (int)l1 : (int)l0;
     } else if (h0) {
-        t.node = n.link.x;
+        t.node = (int)l0;
     } else if (h1) {
-        t.node = n.link.y;
+        t.node = (int)l1;
     } else if (t.sp == 0) {
         t.node = -1;
     } else {
@@ -556,7 +598,8 @@ __device__ __forceinline__ bool trav_node(const GNode *__restrict__ nodes, Stack
 template <bool kCount, class PR>
 __device__ __forceinline__ void trav_leaves(const PR &prims, Leaves lv, V3 o, V3 d, const RayK &rk, Trav &t,
                                             Counters &cnt) {
-    test_range<kCount>(prims, (int)(lv & kLeafFirstMask), (int)(lv >> 28), o, d, rk, t.closest, t.hit_prim, cnt);
+    test_range<kCount>(prims, (int)(lv & kLinkFirstMask), (int)(lv >> kLinkCountShift), o, d, rk, t.closest, t.hit_prim,
+                       cnt);
 }
 
 // BVH4 step: test the 4 child boxes, test leaf children's spheres in place, then descend
@@ -1125,7 +1168,8 @@ __device__ __forceinline__ void render_body(const KParams &P) {
     extern __shared__ uint4 lds_dyn[];
     // LDS layout: [traversal stack: stack_depth x kBlock x StackT, 16-B aligned][nodes][primitives]
     StackT *lds_stack = reinterpret_cast<StackT *>(lds_dyn);
-    using Node = typename std::conditional<kWide, GNode4, GNode>::type;
+    // BVH2 nodes: sign-ordered 80-B GNode when staged in LDS, 64-B GNodeG in global memory
+    using Node = typename std::conditional<kWide, GNode4, typename std::conditional<kLds, GNode, GNodeG>::type>::type;
     const Node *nodes = reinterpret_cast<const Node *>(P.nodes);
     const float4 *prims = P.prim_cr;
     const GMaterial *mtl = P.prim_mtl;
@@ -1423,7 +1467,7 @@ hipError_t launch_variant(const KParams &p, bool count, hipStream_t stream) {
     if (p.n_units == 0) return hipSuccess;
     size_t lds = ((size_t)p.stack_depth * kBlock * sizeof(StackT) + 15u) / 16u * 16u;
     if (kLds)
-        lds += (size_t)p.n_nodes * (kWide ? sizeof(GNode4) : sizeof(GNode)) +
+        lds += (size_t)p.n_nodes * (kWide ? sizeof(GNode4) : sizeof(GNode)) +  // LDS BVH2 = GNode
                (size_t)p.n_prims * (kPrimBytes + (kBook2 ? kMotionBytes : 0));
     auto kernel = count ? rrt_render<kLds, true, StackT, kWide, kWaves, kBook2>
                         : rrt_render<kLds, false, StackT, kWide, kWaves, kBook2>;

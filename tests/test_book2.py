@@ -13,7 +13,7 @@ import pytest
 
 import rustraytrace_amd as rrt
 from oracle import oracle
-from rustraytrace_amd.render import build_bvh
+from rustraytrace_amd.render import build_bvh, decode_bvh2
 
 
 # ---- f32 sin (Cephes sinf, the kernel's rrt_sinf) ---------------------------------------------
@@ -123,18 +123,17 @@ def test_moving_sphere_boxes_span_both_ends():
     sc = rrt.next_week_scene(1)
     nodes, order, info = build_bvh(sc)
     assert info["width"] == 2
-    f = nodes.view(np.float32).reshape(-1, 16)
-    links = nodes.view(np.int32).reshape(-1, 16)[:, 12:16]
+    lo, hi, first_of, count_of = decode_bvh2(nodes, info["node_stride"])
     cr = sc.spheres["center_radius"][order]
     mo = sc.motion[order]
     checked = 0
-    for n in range(len(f)):
-        for child, (lo, hi) in enumerate([((0, 2, 4), (1, 3, 5)), ((6, 8, 10), (7, 9, 11))]):
-            cnt = links[n, 2 + child]
+    for n in range(len(lo)):
+        for child in range(2):
+            cnt = count_of[n, child]
             if cnt <= 0:
                 continue
-            first = links[n, child]
-            blo, bhi = f[n, list(lo)], f[n, list(hi)]
+            first = first_of[n, child]
+            blo, bhi = lo[n, child], hi[n, child]
             for i in range(first, first + cnt):
                 for t in (0.0, 0.5, 0.999):
                     c = cr[i, :3] + np.float32(t) * mo[i, :3]
@@ -165,7 +164,7 @@ def test_book2_kbvh_agrees_with_books_tree(scene):
     sc = rrt.next_week_scene(scene, dict(image_width=48, samples_per_pixel=4, max_depth=10))
     a, ra, _ = oracle.render(sc, oracle.TWIN, threads=4)
     nodes, order, info = build_bvh(sc)
-    b, rb, _ = oracle.render_kbvh(sc, nodes, order, 2, threads=4)
+    b, rb, _ = oracle.render_kbvh(sc, nodes, order, info, threads=4)
     # quads: exact t-ties at shared edges go to the first quad tested, which can turn a
     # zero-contribution path differently in the two trees (tests/test_gpu_book2.py)
     assert np.array_equal(a, b) and (ra == rb or sc.quads is not None)
@@ -292,16 +291,15 @@ def test_quad_bvh_boxes_contain_quads():
     sc = rrt.next_week_scene(7)
     nodes, order, info = build_bvh(sc)
     assert info["width"] == 2 and len(order) == 18 and sorted(order.tolist()) == list(range(18))
-    f = nodes.view(np.float32).reshape(-1, 16)
-    links = nodes.view(np.int32).reshape(-1, 16)[:, 12:16]
+    lo, hi, first_of, count_of = decode_bvh2(nodes, info["node_stride"])
     checked = 0
-    for n in range(len(f)):
-        for child, (lo, hi) in enumerate([((0, 2, 4), (1, 3, 5)), ((6, 8, 10), (7, 9, 11))]):
-            cnt = links[n, 2 + child]
+    for n in range(len(lo)):
+        for child in range(2):
+            cnt = count_of[n, child]
             if cnt <= 0:
                 continue
-            first = links[n, child]
-            blo, bhi = f[n, list(lo)], f[n, list(hi)]
+            first = first_of[n, child]
+            blo, bhi = lo[n, child], hi[n, child]
             for i in range(first, first + cnt):
                 qd = sc.quads[order[i]]
                 q, u, v = (qd[k][:3] for k in ("q", "u", "v"))

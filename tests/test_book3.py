@@ -56,7 +56,7 @@ def test_book3_kbvh_agrees_with_books_tree():
     a, ra, _ = oracle.render(sc, oracle.TWIN, threads=8)
     nodes, order, info = build_bvh(sc)
     assert info["width"] == 2
-    b, rb, _ = oracle.render_kbvh(sc, nodes, order, 2, threads=8)
+    b, rb, _ = oracle.render_kbvh(sc, nodes, order, info, threads=8)
     assert np.array_equal(a, b)  # ray counts may differ at exact quad-edge ties (test_book2.py)
 
 

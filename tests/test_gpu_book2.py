@@ -34,7 +34,7 @@ def test_book2_one_shot_matches_oracle(scene, kw):
     ref, rays, _ = oracle.render(sc, oracle.TWIN)
     assert_bit_exact(gpu, ref, sc.spp)
     nodes, order, info = build_bvh(sc)
-    kref, krays, _ = oracle.render_kbvh(sc, nodes, order, info["width"])
+    kref, krays, _ = oracle.render_kbvh(sc, nodes, order, info)
     assert_bit_exact(gpu, kref, sc.spp)
     assert np.all(gpu[..., 3] == sc.spp)
     # Quads meet at shared edges (box faces, walls) and lie on each other (a box's bottom on the
@@ -49,7 +49,7 @@ def test_book2_device_tiles_and_ray_counts(scene):
     sc = rrt.next_week_scene(scene, dict(image_width=80, samples_per_pixel=6, max_depth=12))
     gpu, idx, ctr, work = gpu_tile(sc, count=True)
     nodes, order, info = build_bvh(sc)
-    ref, rays, _ = oracle.render_kbvh(sc, nodes, order, info["width"])
+    ref, rays, _ = oracle.render_kbvh(sc, nodes, order, info)
     assert_bit_exact(gpu, ref, sc.spp)
     assert ctr["rays"] == rays and work["rays"] == rays
     assert ctr["paths"] == sc.width * sc.height * sc.spp
@@ -60,7 +60,7 @@ def test_bouncing_spheres_larger_frame_kbvh():
     sc = rrt.next_week_scene(1, dict(image_width=320, samples_per_pixel=16, max_depth=50))
     gpu = rrt.render(sc)
     nodes, order, info = build_bvh(sc)
-    ref, _, _ = oracle.render_kbvh(sc, nodes, order, info["width"], threads=16)
+    ref, _, _ = oracle.render_kbvh(sc, nodes, order, info, threads=16)
     assert_bit_exact(gpu, ref, sc.spp)
 
 
@@ -69,7 +69,7 @@ def test_cornell_box_larger_frame_kbvh():
     sc = rrt.next_week_scene(7, dict(image_width=200, samples_per_pixel=16, max_depth=50))
     gpu = rrt.render(sc)
     nodes, order, info = build_bvh(sc)
-    ref, _, _ = oracle.render_kbvh(sc, nodes, order, info["width"], threads=16)
+    ref, _, _ = oracle.render_kbvh(sc, nodes, order, info, threads=16)
     assert_bit_exact(gpu, ref, sc.spp)
 
 
@@ -81,7 +81,7 @@ def test_cornell_smoke_and_final_scene_larger_frames_kbvh():
         sc = rrt.next_week_scene(scene, kw)
         gpu = rrt.render(sc)
         nodes, order, info = build_bvh(sc)
-        ref, _, _ = oracle.render_kbvh(sc, nodes, order, info["width"], threads=16)
+        ref, _, _ = oracle.render_kbvh(sc, nodes, order, info, threads=16)
         assert_bit_exact(gpu, ref, sc.spp)
 
 

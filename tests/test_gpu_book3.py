@@ -24,7 +24,7 @@ def test_book3_one_shot_matches_oracle(kw):
     sc = rrt.rest_of_your_life_scene(kw)
     gpu = rrt.render(sc)
     nodes, order, info = build_bvh(sc)
-    kref, _, _ = oracle.render_kbvh(sc, nodes, order, info["width"], threads=16)
+    kref, _, _ = oracle.render_kbvh(sc, nodes, order, info, threads=16)
     assert_bit_exact(gpu, kref, sc.spp)
     assert np.all(gpu[..., 3] == sc.spp) and np.isfinite(gpu).all()
     # the oracle's own tree: the box faces share edges, and an exact t-tie there goes to the first
@@ -39,7 +39,7 @@ def test_book3_device_tiles_and_ray_counts():
     sc = rrt.rest_of_your_life_scene(dict(image_width=40, samples_per_pixel=36, max_depth=12))
     gpu, idx, ctr, work = gpu_tile(sc, count=True)
     nodes, order, info = build_bvh(sc)
-    ref, rays, _ = oracle.render_kbvh(sc, nodes, order, info["width"], threads=16)
+    ref, rays, _ = oracle.render_kbvh(sc, nodes, order, info, threads=16)
     assert_bit_exact(gpu, ref, sc.spp)
     assert ctr["rays"] == rays and ctr["paths"] == sc.width * sc.height * sc.spp
 
@@ -48,7 +48,7 @@ def test_book3_larger_frame():
     sc = rrt.rest_of_your_life_scene(dict(image_width=160, samples_per_pixel=64, max_depth=50))
     gpu = rrt.render(sc)
     nodes, order, info = build_bvh(sc)
-    ref, _, _ = oracle.render_kbvh(sc, nodes, order, info["width"], threads=16)
+    ref, _, _ = oracle.render_kbvh(sc, nodes, order, info, threads=16)
     assert_bit_exact(gpu, ref, sc.spp)
 
 

@@ -28,7 +28,7 @@ def scene_of(spheres, materials, width=61, spp=5, depth=8, **cam):
 def check(sc):
     gpu = rrt.render(sc)
     nodes, order, info = build_bvh(sc)
-    ref, rays, _ = oracle.render_kbvh(sc, nodes, order, info["width"])
+    ref, rays, _ = oracle.render_kbvh(sc, nodes, order, info)
     assert_bit_exact(gpu, ref, sc.spp)
     return gpu, ref
 

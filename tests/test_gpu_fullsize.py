@@ -55,7 +55,7 @@ def test_full_frame_properties_and_rows(cfg, rows):
     assert ctr["rays"] >= ctr["paths"]
     nodes, order, info = build_bvh(scene)
     for y in rows:
-        ref, _, _ = oracle.render_kbvh(scene, nodes, order, info["width"], rows=(y, y + 1), threads=THREADS)
+        ref, _, _ = oracle.render_kbvh(scene, nodes, order, info, rows=(y, y + 1), threads=THREADS)
         assert np.array_equal(a[y:y + 1].astype(np.float64), ref), f"{cfg} row {y} differs from the oracle"
     ds.close()
 
@@ -67,7 +67,7 @@ def test_c2_whole_frame_bit_exact(spp):
     scene = rrt.config_scene("C2", samples_per_pixel=spp)
     ds, tile, a, b, ctr = _render_full(scene)
     nodes, order, info = build_bvh(scene)
-    ref, rays, _ = oracle.render_kbvh(scene, nodes, order, info["width"], threads=THREADS)
+    ref, rays, _ = oracle.render_kbvh(scene, nodes, order, info, threads=THREADS)
     diff = np.abs(a.astype(np.float64) - ref)
     assert (diff[..., :3] / spp).max() <= 1e-4  # north-star tolerance
     assert diff.max() == 0.0, f"{int((diff > 0).any(-1).sum())} pixels differ"
@@ -104,7 +104,7 @@ def test_c3_tiles_match_oracle_rows():
         assert np.array_equal(a, b)
         y = int(idx[0])
         nodes, order, info = build_bvh(scene)
-        ref, _, _ = oracle.render_kbvh(scene, nodes, order, info["width"], rows=(y, y + 1), threads=THREADS)
+        ref, _, _ = oracle.render_kbvh(scene, nodes, order, info, rows=(y, y + 1), threads=THREADS)
         assert np.array_equal(a[0:1].astype(np.float64), ref)
         ds.close()
 

@@ -66,7 +66,7 @@ def test_one_shot_matches_oracle(cfg, kw):
     ref, rays, _ = oracle.render(scene, oracle.TWIN)  # independent books-structured tree
     assert_bit_exact(gpu, ref, scene.spp)
     nodes, order, info = build_bvh(scene)
-    kref, krays, _ = oracle.render_kbvh(scene, nodes, order, info["width"])  # the kernel's own tree
+    kref, krays, _ = oracle.render_kbvh(scene, nodes, order, info)  # the kernel's own tree
     assert_bit_exact(gpu, kref, scene.spp)
     assert krays == rays
     assert np.all(gpu[..., 3] == scene.spp)

@@ -33,6 +33,6 @@ def test_api_scene_renders_bit_exact():
     sc = W.build(w, cam, seed=99)
     gpu = rrt.render(sc)
     nodes, order, info = build_bvh(sc)
-    ref, _, _ = oracle.render_kbvh(sc, nodes, order, info["width"], threads=16)
+    ref, _, _ = oracle.render_kbvh(sc, nodes, order, info, threads=16)
     assert_bit_exact(gpu, ref, sc.spp)
     assert np.all(gpu[..., 3] == sc.spp) and gpu[..., :3].mean() > 0

@@ -319,7 +319,7 @@ def test_kbvh_mode_agrees_with_books_tree(cfg, kw, width):
     a, ra, _ = oracle.render(sc, oracle.TWIN, threads=4)
     nodes, order, info = build_bvh(sc, width=width)
     assert info["width"] == width and sorted(order.tolist()) == list(range(len(sc.spheres)))
-    b, rb, _ = oracle.render_kbvh(sc, nodes, order, width, threads=4)
+    b, rb, _ = oracle.render_kbvh(sc, nodes, order, info, threads=4)
     assert np.array_equal(a, b) and ra == rb
 
 
@@ -348,5 +348,22 @@ def test_axis_parallel_rays_hit_through_straddling_boxes():
     sc = axis_parallel_scene()
     twin, _, _ = oracle.render(sc, oracle.TWIN)
     nodes, order, info = build_bvh(sc)
-    kb, _, _ = oracle.render_kbvh(sc, nodes, order, info["width"])
+    kb, _, _ = oracle.render_kbvh(sc, nodes, order, info)
     assert np.all(twin[..., :3] == 0) and np.array_equal(twin, kb)
+
+
+def test_bvh2_node_layouts_hold_the_same_tree(monkeypatch):
+    """RTOW fits the LDS budget: 80-B sign-ordered nodes; C5's 10k spheres do not: 64-B nodes.
+    Forcing global memory on RTOW gives the 64-B layout of the same tree (same boxes, links)."""
+    from rustraytrace_amd.render import build_bvh, decode_bvh2
+
+    sc = rrt.rtow(image_width=32, samples_per_pixel=2)
+    nodes, order, info = build_bvh(sc)
+    assert info["node_stride"] == 80 and nodes.size == 80 * info["n_nodes"]
+    c5 = rrt.config_scene("C5", image_width=32, samples_per_pixel=2)
+    assert build_bvh(c5)[2]["node_stride"] == 64
+    monkeypatch.setenv("RRT_SCENE_IN_LDS", "0")
+    nodes_g, order_g, info_g = build_bvh(sc)
+    assert info_g["node_stride"] == 64 and np.array_equal(order, order_g)
+    for x, y in zip(decode_bvh2(nodes, 80), decode_bvh2(nodes_g, 64)):
+        assert np.array_equal(x, y)

@@ -23,7 +23,7 @@ def main():
     sc = eval(sys.argv[1], {"rrt": rrt, "np": np})
     nodes, order, info = build_bvh(sc)
     gpu = rrt.render(sc)
-    ref, _, _ = oracle.render_kbvh(sc, nodes, order, info["width"], threads=16)
+    ref, _, _ = oracle.render_kbvh(sc, nodes, order, info, threads=16)
     bad = np.argwhere(np.any(gpu.astype(np.float64) != ref, axis=-1))
     print("differing pixels:", len(bad), bad[:8].tolist())
     if not len(bad):
@@ -31,7 +31,7 @@ def main():
     y, x = bad[0]
     for s in range(sc.spp):
         g, _, _, _ = gpu_tile(sc, s0=s, s1=s + 1)
-        r, _, _ = oracle.render_kbvh(sc, nodes, order, info["width"], rows=(int(y), int(y) + 1), samples=(s, s + 1))
+        r, _, _ = oracle.render_kbvh(sc, nodes, order, info, rows=(int(y), int(y) + 1), samples=(s, s + 1))
         if not np.array_equal(g[y, x].astype(np.float64), r[0, x]):
             print(f"pixel x={x} y={y} sample {s}: gpu {g[y, x].tolist()} oracle {r[0, x].tolist()}")
             if len(sys.argv) > 2:
