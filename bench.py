@@ -30,7 +30,7 @@ PEAK_F32_VALU_TFLOPS = 157.3
 FLOP_PER_SPHERE_TEST = 23  # sphere.rs:26-31
 FLOP_PER_BOX_TEST = 12  # aabb.rs:56-82 with hoisted reciprocal
 BYTES_PER_SPHERE_TEST = 16
-BYTES_PER_NODE_VISIT = 64  # GNode: both child boxes + links
+BYTES_PER_NODE_VISIT = 56  # per BVH2 node visit: two child boxes (2 x 24 B) + two links (2 x 4 B)
 
 
 def parse():
