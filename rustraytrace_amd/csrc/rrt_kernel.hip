@@ -711,9 +711,13 @@ __device__ __forceinline__ void camera_ray(const KParams &P, uint32_t x, uint32_
 
 // The path's RNG stream for sample s of global pixel (x, y): xoshiro128+ state
 // (z, key | 1 << 32) with key = splitmix64((seed << 32) ^ pixel) and z = splitmix64(key + s).
-// Re-derived per sample (no per-pixel key held).
+// The key is computed once per work unit (pixel, sample chunk) and held (+0.6 % on C2).
+__device__ __forceinline__ uint64_t pixel_key(const KParams &P, uint32_t x, uint32_t y) {
+    return splitmix64(((uint64_t)P.seed << 32) ^ (uint64_t)(y * P.width + x));
+}
+__device__ __forceinline__ RngState path_rng_k(uint64_t key, uint32_t s) { return rng_seed(splitmix64(key + s), key); }
 __device__ __forceinline__ RngState path_rng(const KParams &P, uint32_t x, uint32_t y, uint32_t s) {
-    const uint64_t key = splitmix64(((uint64_t)P.seed << 32) ^ (uint64_t)(y * P.width + x));
+    const uint64_t key = pixel_key(P, x, y);
     return rng_seed(splitmix64(key + s), key);
 }
 
@@ -1210,6 +1214,7 @@ __device__ __forceinline__ void render_body(const KParams &P) {
     bool q_open = true;   // wave-uniform: the queue may still hold units
     // lane's unit: global pixel (x | y << 16), next sample s, end of its sample chunk s_hi
     uint32_t xy = 0, s = 0, s_hi = 0;
+    uint64_t pkey = 0;  // the unit's pixel key (one splitmix64 per unit instead of per path)
     V3 sum = v3(0.0f, 0.0f, 0.0f);
     PathState ps;
     Trav tr;
@@ -1253,7 +1258,8 @@ __device__ __forceinline__ void render_body(const KParams &P) {
                         s = P.sample_begin + chunk * P.chunk;
                         s_hi = min(s + P.chunk, P.sample_end);
                         sum = v3(0.0f, 0.0f, 0.0f);
-                        ps.rng = path_rng(P, x, y, s);
+                        pkey = pixel_key(P, x, y);
+                        ps.rng = path_rng_k(pkey, s);
                         camera_ray<kBook2 == 4>(P, x, y, s, ps);
                         need_ray = true;
                         has = true;
@@ -1352,7 +1358,7 @@ __device__ __forceinline__ void render_body(const KParams &P) {
             ++s;
             const uint32_t x = xy & 0xffffu, y = xy >> 16;
             if (s < s_hi) {
-                ps.rng = path_rng(P, x, y, s);
+                ps.rng = path_rng_k(pkey, s);
                 camera_ray<kBook2 == 4>(P, x, y, s, ps);
             } else {  // unit complete: the chunk's sum, in sample order
                 // chunk index and tile-local row, re-derived from (y, s_hi) once per unit
