@@ -132,11 +132,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # RCCL ("nccl") between one process per GPU. RRT_BENCH_BACKEND=gloo is a rehearsal mode for
+    # ranks sharing a GPU (device = local rank mod device count; host copies for the gather).
+    backend = os.environ.get("RRT_BENCH_BACKEND", "nccl")
+    device = local % max(1, torch.cuda.device_count()) if backend == "gloo" else local
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device(f"cuda:{local}"))
-    device = local
+        torch.cuda.set_device(device)
+        kw = {"device_id": torch.device(f"cuda:{device}")} if backend == "nccl" else {}
+        dist.init_process_group(backend, rank=rank, world_size=world, **kw)
     torch.cuda.set_device(device)
 
     kw = {}
@@ -153,14 +157,22 @@ def main():
 
     total = torch.empty_like(accum) if rank == 0 else None
 
+    def gather():  # the one exchange: partial accums -> rank 0, summed in rank order
+        if backend == "gloo":
+            res = gather_sample_ranges(accum.cpu(), dist)
+            if res is not None:
+                total.copy_(res)
+        else:
+            gather_sample_ranges(accum, dist, out=total)
+
     def step(i=None):
         if i is not None:
             k_start[i].record(stream)
         ds.render_tile_async(tile, accum.data_ptr(), stream.cuda_stream)
         if i is not None:
             k_end[i].record(stream)
-        if world > 1:  # the one exchange: partial accums -> rank 0, summed in rank order
-            gather_sample_ranges(accum, dist, out=total)
+        if world > 1:
+            gather()
 
     k_start = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     k_end = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
@@ -185,16 +197,17 @@ def main():
         dist.barrier()
         torch.cuda.synchronize()
         t = time.perf_counter()
-        gather_sample_ranges(accum, dist, out=total)
+        gather()
         torch.cuda.synchronize()
         gather_ms = (time.perf_counter() - t) * 1e3
     ctr = ds.counters()
     rays = ctr["rays"]
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{device}")
+        red_dev = f"cuda:{device}" if backend == "nccl" else "cpu"
+        t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        r = torch.tensor([rays], dtype=torch.int64, device=f"cuda:{device}")
+        r = torch.tensor([rays], dtype=torch.int64, device=red_dev)
         dist.all_reduce(r, op=dist.ReduceOp.SUM)
         rays = int(r.item())
 
