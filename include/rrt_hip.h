@@ -28,7 +28,8 @@ extern "C" {
 
 /* 1: book 1; 2: RrtSceneExt (motion, Perlin), kinds 5-6; 3: quads, constant-density media and
  * book-3 light lists in RrtSceneExt, kind 7, RRT_FLAG_BOOK3, rrt_build_next_week_scene /
- * rrt_build_rest_of_your_life_scene with struct outputs. */
+ * rrt_build_rest_of_your_life_scene with struct outputs; 4: RrtBvhInfo.node_stride (80-B LDS /
+ * 64-B global BVH2 nodes), xoshiro128+ path streams, tail-split accumulation chunks. */
 #define RRT_ABI_VERSION 4u
 
 /* ---- scene ABI (== src/gpu/mod.rs:13-42) ------------------------------------------ */
@@ -232,9 +233,12 @@ int32_t rrt_hip_render_ex(const RrtCamera *cam,
 const char *rrt_hip_last_error(void);
 uint32_t rrt_hip_abi_version(void);
 
-/* Summation order of the accum: a pixel's RGB = sum over consecutive chunks of K samples
- * (K = rrt_accum_chunk(), counted from the tile's sample_begin) of each chunk's in-order
- * sample sum, chunks added in order: ((c0 + c1) + c2) + ... Needed to reproduce it bit for bit. */
+/* Summation order of the accum: a pixel's RGB = sum over consecutive chunks of its S samples
+ * (counted from the tile's sample_begin) of each chunk's in-order sample sum, chunks added in
+ * order: ((c0 + c1) + c2) + ... With K = rrt_accum_chunk() and k = max(1, K / 8): the first
+ * nb = (S - 1) / K chunks hold K samples each (nb = 0 when S <= K), the remaining S - nb*K
+ * samples form chunks of k (the last one possibly shorter) — small units at the end of the
+ * work queue keep the persistent grid's tail short. Needed to reproduce it bit for bit. */
 uint32_t rrt_accum_chunk(void);
 
 /* ---- device-resident API (bench / multi-rank hosts) --------------------------------- */

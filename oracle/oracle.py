@@ -15,8 +15,9 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "build", "librrt_oracle.so")
 TWIN, BOOKS = 0, 1
-# Accum summation chunk of the HIP backend (include/rrt_hip.h rrt_accum_chunk): samples are
-# summed in order within chunks of this many, chunk sums added in order.
+# Accum summation chunk K of the HIP backend (include/rrt_hip.h rrt_accum_chunk): (S-1)/K chunks
+# of K samples, then chunks of max(1, K/8) for the tail; samples summed in order within a chunk,
+# chunk sums added in order.
 DEFAULT_CHUNK = 64
 
 _LIB = None

@@ -1407,11 +1407,16 @@ int render(const RrtCamera *c, const RrtSphere *s, uint32_t n, const RrtMaterial
                 const uint32_t pixel = j * cam.width + i;
                 const uint64_t key = splitmix64(((uint64_t)cam.seed << 32) ^ (uint64_t)pixel);
                 const uint64_t rays_before = tl.rays;
-                // accum order of the kernel (rrt_accum_chunk): in-order sums over chunks of
-                // `chunk` samples from s0, chunk sums added in order
+                // accum order of the kernel (rrt_accum_chunk, include/rrt_hip.h): in-order sums
+                // over chunks from s0 — (S-1)/K chunks of K samples, then chunks of max(1, K/8)
+                // for the rest (chunk 0 = one chunk) — chunk sums added in order
                 Vec3<T> sum = mk(T(0), T(0), T(0));
-                const uint32_t step = chunk ? chunk : (s1 - s0 ? s1 - s0 : 1);
-                for (uint32_t c0 = s0; c0 < s1; c0 += step) {
+                const uint32_t S = s1 - s0;
+                const uint32_t big = chunk ? chunk : (S ? S : 1);
+                const uint32_t small = chunk ? std::max(1u, chunk / 8u) : big;
+                const uint32_t nb = (chunk && S > big) ? (S - 1u) / big : 0u;
+                for (uint32_t c0 = s0; c0 < s1;) {
+                    const uint32_t step = (c0 - s0) < nb * big ? big : small;
                     Vec3<T> csum = mk(T(0), T(0), T(0));
                     for (uint32_t sidx = c0; sidx < std::min(s1, c0 + step); ++sidx) {
                         PathRng rng(splitmix64(key + sidx), key);
@@ -1428,6 +1433,7 @@ int render(const RrtCamera *c, const RrtSphere *s, uint32_t n, const RrtMaterial
                         csum = csum + c;
                     }
                     sum = (c0 == s0) ? csum : sum + csum;
+                    c0 += step;
                 }
                 double *px = accum + ((size_t)(j - y0) * cam.width + i) * 4;
                 px[0] = (double)sum.x();

@@ -749,10 +749,14 @@ int fill_params(RrtScene *s, const RrtTile *t, float *d_accum, rrt::KParams &p) 
     p.tiles_x = (p.width + 7u) / 8u;
     p.n_work_tiles = p.tiles_x * ((p.tile_rows + 7u) / 8u);
     const uint32_t S = t->sample_end - t->sample_begin;
-    p.n_chunks = (S + p.chunk - 1) / p.chunk;
+    p.chunk_small = std::max(1u, p.chunk / 8u);
+    p.n_big = S > p.chunk ? (S - 1u) / p.chunk : 0u;
+    const uint32_t tail = S - p.n_big * p.chunk;
+    p.n_chunks = S ? p.n_big + (tail + p.chunk_small - 1u) / p.chunk_small : 0u;
     const uint64_t units = (uint64_t)p.n_work_tiles * p.n_chunks * 64u;
     if (units > 0xFFFFFFFFull) return fail(RRT_E_INVALID, "tile too large: more than 2^32 work units");
     p.n_units = (uint32_t)units;
+    p.n_big_units = p.n_work_tiles * p.n_big * 64u;
     p.unit_counter = s->d_unit_counter;
     if (p.n_chunks > 1) {  // partial sums [pixel][chunk]; grow on demand
         const size_t need = (size_t)p.tile_rows * p.width * p.n_chunks;

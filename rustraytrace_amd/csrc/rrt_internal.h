@@ -157,9 +157,13 @@ struct KParams {
     uint32_t min_waves;     // launch-bounds occupancy request (waves per SIMD)
     uint32_t global_waves;  // the same for scenes read from L2 (not staged in LDS); < 6 = no bound
 
-    // persistent work queue: units = (pixel, chunk of `chunk` samples), tile-major
-    uint32_t chunk;           // samples per unit
-    uint32_t n_chunks;        // ceil((sample_end - sample_begin) / chunk)
+    // persistent work queue: units = (pixel, sample chunk), the n_big chunks of `chunk` samples
+    // of every tile first (tile-major), then the tail chunks of `chunk_small` (rrt_accum_chunk)
+    uint32_t chunk;           // samples per big chunk
+    uint32_t chunk_small;     // samples per tail chunk: max(1, chunk / 8)
+    uint32_t n_big;           // big chunks per pixel: (S - 1) / chunk (0 when S <= chunk)
+    uint32_t n_chunks;        // n_big + ceil((S - n_big * chunk) / chunk_small)
+    uint32_t n_big_units;     // n_work_tiles * n_big * 64
     uint32_t n_units;         // n_work_tiles * n_chunks * 64
     uint32_t n_cus;           // compute units of the device (grid sizing)
     uint32_t *unit_counter;   // device queue head (zeroed per launch)

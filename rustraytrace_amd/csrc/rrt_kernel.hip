@@ -1161,6 +1161,11 @@ __device__ __forceinline__ bool shade_b3(const KParams &P, const PR &prims, cons
     return false;
 }
 
+// First sample (relative to sample_begin) of chunk c of a pixel (rrt_accum_chunk's schedule).
+__device__ __forceinline__ uint32_t chunk_first(const KParams &P, uint32_t c) {
+    return c < P.n_big ? c * P.chunk : P.n_big * P.chunk + (c - P.n_big) * P.chunk_small;
+}
+
 __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
@@ -1246,8 +1251,16 @@ __device__ __forceinline__ void render_body(const KParams &P) {
                 {
                     const uint32_t lit = u & 63u;
                     const uint32_t tc = u >> 6;
-                    const uint32_t t = tc / P.n_chunks;
-                    const uint32_t chunk = tc - t * P.n_chunks;
+                    // big chunks of every tile first, then the tail chunks (small units last)
+                    uint32_t t, chunk;
+                    if (u < P.n_big_units) {
+                        t = tc / P.n_big;
+                        chunk = tc - t * P.n_big;
+                    } else {
+                        const uint32_t ns = P.n_chunks - P.n_big, tc2 = tc - (P.n_big_units >> 6);
+                        t = tc2 / ns;
+                        chunk = P.n_big + (tc2 - t * ns);
+                    }
                     const uint32_t x = (t % P.tiles_x) * 8u + (lit & 7u);
                     const uint32_t ly = (t / P.tiles_x) * 8u + (lit >> 3);
                     if (x < P.width && ly < P.tile_rows) {
@@ -1255,8 +1268,8 @@ __device__ __forceinline__ void render_body(const KParams &P) {
                         const uint32_t band = ly / P.band_rows;
                         const uint32_t y = (band * P.n_ranks + P.rank) * P.band_rows + ly % P.band_rows;
                         xy = x | (y << 16);
-                        s = P.sample_begin + chunk * P.chunk;
-                        s_hi = min(s + P.chunk, P.sample_end);
+                        s = P.sample_begin + chunk_first(P, chunk);
+                        s_hi = min(s + (chunk < P.n_big ? P.chunk : P.chunk_small), P.sample_end);
                         sum = v3(0.0f, 0.0f, 0.0f);
                         pkey = pixel_key(P, x, y);
                         ps.rng = path_rng_k(pkey, s);
@@ -1362,11 +1375,13 @@ __device__ __forceinline__ void render_body(const KParams &P) {
                 camera_ray<kBook2 == 4>(P, x, y, s, ps);
             } else {  // unit complete: the chunk's sum, in sample order
                 // chunk index and tile-local row, re-derived from (y, s_hi) once per unit
-                const uint32_t chunk = (s_hi - 1u - P.sample_begin) / P.chunk;
+                const uint32_t rel = s_hi - 1u - P.sample_begin;
+                const uint32_t nbs = P.n_big * P.chunk;
+                const uint32_t chunk = rel < nbs ? rel / P.chunk : P.n_big + (rel - nbs) / P.chunk_small;
                 const uint32_t gb = y / P.band_rows;
                 const uint32_t ly = ((gb - P.rank) / P.n_ranks) * P.band_rows + (y - gb * P.band_rows);
                 const size_t px = (size_t)ly * P.width + x;
-                const float4 out = make_float4(sum.x, sum.y, sum.z, (float)(s_hi - (P.sample_begin + chunk * P.chunk)));
+                const float4 out = make_float4(sum.x, sum.y, sum.z, (float)(s_hi - (P.sample_begin + chunk_first(P, chunk))));
                 if (P.n_chunks == 1) P.accum[px] = out;
                 else P.partial[px * P.n_chunks + chunk] = out;
                 has = false;

@@ -367,3 +367,28 @@ def test_bvh2_node_layouts_hold_the_same_tree(monkeypatch):
     assert info_g["node_stride"] == 64 and np.array_equal(order, order_g)
     for x, y in zip(decode_bvh2(nodes, 80), decode_bvh2(nodes_g, 64)):
         assert np.array_equal(x, y)
+
+
+@pytest.mark.parametrize("S,chunk", [(20, 8), (512, 64), (64, 64), (65, 64), (7, 0)])
+def test_accum_chunk_schedule(S, chunk):
+    """The TWIN accum groups samples as rrt_accum_chunk documents (include/rrt_hip.h): (S-1)/K
+    chunks of K, then chunks of max(1, K/8); in-order f32 sums per chunk, chunks added in order."""
+    sc = rrt.config_scene("C1", image_width=8, samples_per_pixel=S, max_depth=4)
+    got, _, _ = oracle.render(sc, oracle.TWIN, chunk=chunk)
+    per = [oracle.render(sc, oracle.TWIN, samples=(s, s + 1))[0][..., :3].astype(np.float32)
+           for s in range(S)]
+    K = chunk if chunk else S
+    k = max(1, chunk // 8) if chunk else S
+    nb = (S - 1) // K if chunk and S > K else 0
+    bounds, c0 = [], 0
+    while c0 < S:
+        step = K if c0 < nb * K else k
+        bounds.append((c0, min(S, c0 + step)))
+        c0 += step
+    total = None
+    for a, b in bounds:
+        cs = per[a].copy()
+        for s in range(a + 1, b):
+            cs = cs + per[s]
+        total = cs if total is None else total + cs
+    assert np.array_equal(got[..., :3].astype(np.float32), total) and np.all(got[..., 3] == S)
