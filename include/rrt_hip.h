@@ -238,7 +238,10 @@ uint32_t rrt_hip_abi_version(void);
  * order: ((c0 + c1) + c2) + ... With K = rrt_accum_chunk() and k = max(1, K / 8): the first
  * nb = (S - 1) / K chunks hold K samples each (nb = 0 when S <= K), the remaining S - nb*K
  * samples form chunks of k (the last one possibly shorter) — small units at the end of the
- * work queue keep the persistent grid's tail short. Needed to reproduce it bit for bit. */
+ * work queue keep the persistent grid's tail short. Needed to reproduce it bit for bit.
+ * The chunk partial sums live in a device buffer of at most RRT_PARTIAL_MB MiB (env, default
+ * 2048); a render with more chunks than fit runs as consecutive sample passes of whole chunks,
+ * each continuing the same fold, so the bits do not depend on the budget. */
 uint32_t rrt_accum_chunk(void);
 
 /* ---- device-resident API (bench / multi-rank hosts) --------------------------------- */
@@ -287,7 +290,10 @@ int32_t rrt_tile_row_index(uint32_t height, const RrtTile *tile, uint32_t local_
 
 /* Enqueue the render of `tile` on `stream` (a hipStream_t, NULL = default stream).
  * d_accum: device pointer to rows*W*4 floats, OVERWRITTEN with this tile's sums
- * (RGB sums over the tile's samples, w = sample count). Asynchronous. */
+ * (RGB sums over the tile's samples, w = sample count). Asynchronous.
+ * One render in flight per RrtScene: the scene owns one work-queue head and one chunk-partial
+ * buffer, so renders of the same scene must be ordered on one stream (or synchronised);
+ * concurrent renders on different streams need one RrtScene each. */
 int32_t rrt_render_tile_async(RrtScene *scene, const RrtTile *tile, float *d_accum, void *stream);
 
 /* Counters (synchronises the scene's device). */

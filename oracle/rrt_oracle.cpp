@@ -513,7 +513,11 @@ template <class T> struct World {
     }
 
     bool hit_prim(int32_t p, Vec3<T> o, Vec3<T> d, T time, Interval<T> ray_t, T &t_out, uint64_t *tests,
-                  uint64_t seg) const {
+                  uint64_t seg, int32_t skip = -1) const {
+        if (p == skip) {  // the primitive the ray is leaving (ray_color_twin): tested, never hit
+            if (tests) ++*tests;
+            return false;
+        }
         if ((size_t)p < spheres.size()) return hit_sphere(p, o, d, time, ray_t, t_out, tests);
         const size_t j = p - spheres.size();
         if (j < quads.size()) return hit_quad((int32_t)j, o, d, ray_t, t_out, tests);
@@ -601,18 +605,18 @@ template <class T> struct World {
     // HittableObject::hit dispatch + BvhNode::hit (bvh.rs:159-172), left first, right with
     // max = left.t, result = right.or(left).
     bool hit(ChildRef ref, Vec3<T> o, Vec3<T> d, T time, Interval<T> ray_t, Hit<T> &rec, uint64_t *tests,
-             uint64_t seg) const {
+             uint64_t seg, int32_t skip = -1) const {
         if (ref.is_sphere) {
             T t;
-            if (!hit_prim(ref.index, o, d, time, ray_t, t, tests, seg)) return false;
+            if (!hit_prim(ref.index, o, d, time, ray_t, t, tests, seg, skip)) return false;
             rec = Hit<T>{t, ref.index};
             return true;
         }
         const BvhNode<T> &n = nodes[ref.index];
         if (!aabb_hit(n.bbox, o, d, ray_t)) return false;
         Hit<T> hl, hr;
-        const bool l = hit(n.left, o, d, time, ray_t, hl, tests, seg);
-        const bool r = hit(n.right, o, d, time, Interval<T>{ray_t.min, l ? hl.t : ray_t.max}, hr, tests, seg);
+        const bool l = hit(n.left, o, d, time, ray_t, hl, tests, seg, skip);
+        const bool r = hit(n.right, o, d, time, Interval<T>{ray_t.min, l ? hl.t : ray_t.max}, hr, tests, seg, skip);
         if (r) { rec = hr; return true; }
         if (l) { rec = hl; return true; }
         return false;
@@ -664,7 +668,7 @@ static inline float max_num(float a, float b) { return (b != b) ? a : ((a != a) 
 // (results are identical either way: fmaf is correctly rounded in both).
 __attribute__((target_clones("fma", "default")))
 bool kbvh_hit(const World<float> &w, const KTree &kt, Vec3<float> o, Vec3<float> d, float time, Hit<float> &rec,
-              uint64_t *tests, uint64_t seg) {
+              uint64_t *tests, uint64_t seg, int32_t skip) {
     KRay r;
     r.ix = kclamp_inv(1.0f / d[0]);  // the kernel's ray_consts
     r.iy = kclamp_inv(1.0f / d[1]);
@@ -678,7 +682,7 @@ bool kbvh_hit(const World<float> &w, const KTree &kt, Vec3<float> o, Vec3<float>
     auto leaf = [&](int32_t first, int32_t count) {
         for (int32_t i = first; i < first + count; ++i) {
             float t;
-            if (w.hit_prim((int32_t)kt.order[i], o, d, time, Interval<float>{kTmin, closest}, t, tests, seg)) {
+            if (w.hit_prim((int32_t)kt.order[i], o, d, time, Interval<float>{kTmin, closest}, t, tests, seg, skip)) {
                 closest = t;
                 hit = i;
             }
@@ -767,6 +771,7 @@ template <class T> struct Cam {
     uint32_t width, height;
     uint32_t sqrt_spp = 0;  // book 3: stratified samples
     T recip_sqrt_spp = T(0);
+    bool no_exit_skip = false;  // diagnostic mode bit 0x200: f32 modes without exit_skip
 };
 
 template <class T>
@@ -891,18 +896,20 @@ template <class T> struct Record {
     Vec3<T> p, normal, outward;
     bool front;
     uint32_t mat;
+    int32_t prim;  // the hit primitive (sphere i, quad n_spheres + j, medium n_spheres + n_quads + m)
 };
 
 template <class T>
 bool world_hit(const World<T> &w, Vec3<T> o, Vec3<T> d, T time, uint64_t seg, Record<T> &rec, uint64_t *tests,
-               const KTree *kt = nullptr) {  // camera.rs:187
+               const KTree *kt = nullptr, int32_t skip = -1) {  // camera.rs:187
     Hit<T> h;
     if constexpr (std::is_same_v<T, float>) {
         if (kt) {
-            if (!kbvh_hit(w, *kt, o, d, time, h, tests, seg)) return false;
+            if (!kbvh_hit(w, *kt, o, d, time, h, tests, seg, skip)) return false;
         } else {
             if (w.root.index < 0) return false;
-            if (!w.hit(w.root, o, d, time, Interval<T>{L(0.001), std::numeric_limits<T>::infinity()}, h, tests, seg))
+            if (!w.hit(w.root, o, d, time, Interval<T>{L(0.001), std::numeric_limits<T>::infinity()}, h, tests, seg,
+                       skip))
                 return false;
         }
     } else {
@@ -911,6 +918,7 @@ bool world_hit(const World<T> &w, Vec3<T> o, Vec3<T> d, T time, uint64_t seg, Re
             return false;
     }
     rec.p = o + h.t * d;  // Ray::at
+    rec.prim = h.sphere;
     if ((size_t)h.sphere >= w.spheres.size() + w.quads.size()) {  // medium (constant_medium.rs:76-82)
         rec.outward = rec.normal = mk(T(1), T(0), T(0));
         rec.front = true;
@@ -1122,6 +1130,22 @@ struct Tally {
     uint64_t rays = 0, tests = 0;
 };
 
+// The primitive a scattered ray cannot hit again in exact arithmetic, skipped by the f32 modes'
+// (and the kernel's) next closest-hit query: the sphere it leaves outward (a sphere is convex:
+// a ray from its surface with d.n_out > 0 meets it only at t = 0), or the quad it leaves (a
+// plane is met once). In f32 the rounded hit point lies up to ~ulp(|center|) off the surface,
+// and |oc|^2 - r^2 cancels two ~|oc|^2 values (r = 1000 ground sphere: ulp 0.0625), so a
+// grazing ray would re-hit the surface it leaves past tmin = 0.001 and get trapped inside the
+// ground sphere; the f64 reference never does. -1: a medium, or a ray entering / staying
+// inside a sphere (it must meet that sphere again: refraction, internal reflection).
+template <class T> int32_t exit_skip(const World<T> &w, const Cam<T> &cam, const Record<T> &rec, Vec3<T> dir) {
+    if (cam.no_exit_skip) return -1;
+    if ((size_t)rec.prim >= w.spheres.size() + w.quads.size()) return -1;  // medium
+    if ((size_t)rec.prim >= w.spheres.size()) return rec.prim;            // quad
+    const bool same_side = dot(dir, rec.normal) > T(0);  // rec.normal faces the incoming ray
+    return same_side == rec.front ? rec.prim : -1;
+}
+
 // BOOKS: Camera::ray_color (camera.rs:182-209 / the_next_week/camera.rs:174-201), recursive.
 template <class T>
 Vec3<T> ray_color_books(const World<T> &w, const Cam<T> &cam, PathRng &rng, Vec3<T> o, Vec3<T> d, T time, int depth,
@@ -1148,10 +1172,12 @@ template <class T>
 Vec3<T> ray_color_twin(const World<T> &w, const Cam<T> &cam, PathRng &rng, Vec3<T> o, Vec3<T> d, T time, Tally &tl,
                        const KTree *kt = nullptr) {
     Vec3<T> Tp = mk(T(1), T(1), T(1)), Lp = mk(T(0), T(0), T(0));
+    int32_t skip = -1;
     for (uint32_t k = 0; k < cam.max_depth; ++k) {
         tl.rays++;
         Record<T> rec;
-        if (!world_hit(w, o, d, time, rng.key() ^ ((uint64_t)k << 32), rec, &tl.tests, kt)) return Lp + Tp * miss_color(cam, d);
+        if (!world_hit(w, o, d, time, rng.key() ^ ((uint64_t)k << 32), rec, &tl.tests, kt, skip))
+            return Lp + Tp * miss_color(cam, d);
         const Material<T> &m = w.mats[rec.mat];
         if (m.kind == RRT_MAT_DIFFUSE_LIGHT) return Lp + Tp * m.albedo;
         Vec3<T> att, dir;
@@ -1165,6 +1191,7 @@ Vec3<T> ray_color_twin(const World<T> &w, const Cam<T> &cam, PathRng &rng, Vec3<
         }
         o = rec.p;
         d = dir;
+        skip = exit_skip(w, cam, rec, dir);
     }
     return Lp;
 }
@@ -1329,10 +1356,12 @@ template <class T>
 Vec3<T> ray_color_b3_twin(const World<T> &w, const Cam<T> &cam, PathRng &rng, Vec3<T> o, Vec3<T> d, T time, Tally &tl,
                           const KTree *kt = nullptr) {
     Vec3<T> Tp = mk(T(1), T(1), T(1)), Lp = mk(T(0), T(0), T(0));
+    int32_t skip = -1;
     for (uint32_t k = 0; k < cam.max_depth; ++k) {
         tl.rays++;
         Record<T> rec;
-        if (!world_hit(w, o, d, time, rng.key() ^ ((uint64_t)k << 32), rec, &tl.tests, kt)) return Lp + Tp * cam.background;
+        if (!world_hit(w, o, d, time, rng.key() ^ ((uint64_t)k << 32), rec, &tl.tests, kt, skip))
+            return Lp + Tp * cam.background;
         const Material<T> &m = w.mats[rec.mat];
         if (m.kind == RRT_MAT_DIFFUSE_LIGHT) return rec.front ? Lp + Tp * m.albedo : Lp;
         Vec3<T> att, dir;
@@ -1358,6 +1387,7 @@ Vec3<T> ray_color_b3_twin(const World<T> &w, const Cam<T> &cam, PathRng &rng, Ve
         }
         o = rec.p;
         d = dir;
+        skip = exit_skip(w, cam, rec, dir);
     }
     return Lp;
 }
@@ -1394,6 +1424,7 @@ int render(const RrtCamera *c, const RrtSphere *s, uint32_t n, const RrtMaterial
     World<T> w;
     Cam<T> cam;
     load_world(w, cam, c, s, n, m, nm, tex, ntex, flags, ext);
+    cam.no_exit_skip = (mode & 0x200) != 0;
     if (y1 > cam.height) y1 = cam.height;
     if (y0 > y1) return -1;
     std::atomic<uint32_t> next_row{y0};

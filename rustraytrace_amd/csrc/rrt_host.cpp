@@ -737,6 +737,14 @@ int check_tile(const RrtScene *s, const RrtTile *t) {
     return RRT_OK;
 }
 
+// Bytes of chunk partials one render may hold (RRT_PARTIAL_MB, default 2048 MiB): C2 (15 x
+// 33 MB) renders in one pass, a whole C3 frame on one GPU (39 x 133 MB) in three.
+size_t partial_budget() {
+    size_t mb = 2048;
+    if (const char *e = std::getenv("RRT_PARTIAL_MB")) mb = (size_t)std::max(1, std::atoi(e));
+    return mb << 20;
+}
+
 int fill_params(RrtScene *s, const RrtTile *t, float *d_accum, rrt::KParams &p) {
     p = s->base;
     p.accum = reinterpret_cast<float4 *>(d_accum);
@@ -758,8 +766,11 @@ int fill_params(RrtScene *s, const RrtTile *t, float *d_accum, rrt::KParams &p) 
     p.n_units = (uint32_t)units;
     p.n_big_units = p.n_work_tiles * p.n_big * 64u;
     p.unit_counter = s->d_unit_counter;
-    if (p.n_chunks > 1) {  // partial sums [pixel][chunk]; grow on demand
-        const size_t need = (size_t)p.tile_rows * p.width * p.n_chunks;
+    p.pass_chunks = p.n_chunks;
+    if (p.n_chunks > 1) {  // partial sums [pass chunk][pixel], within the partial budget; grow on demand
+        const size_t n_px = std::max<size_t>((size_t)p.tile_rows * p.width, 1);
+        p.pass_chunks = (uint32_t)std::min<size_t>(p.n_chunks, std::max<size_t>(1, partial_budget() / (n_px * sizeof(float4))));
+        const size_t need = n_px * p.pass_chunks;
         if (need > s->partial_cap) {
             HIP_TRY(hipSetDevice(s->device), "hipSetDevice");
             (void)hipFree(s->d_partial);

@@ -163,11 +163,20 @@ struct KParams {
     uint32_t chunk_small;     // samples per tail chunk: max(1, chunk / 8)
     uint32_t n_big;           // big chunks per pixel: (S - 1) / chunk (0 when S <= chunk)
     uint32_t n_chunks;        // n_big + ceil((S - n_big * chunk) / chunk_small)
-    uint32_t n_big_units;     // n_work_tiles * n_big * 64
-    uint32_t n_units;         // n_work_tiles * n_chunks * 64
+    // Sample passes: the chunks are rendered pass_chunks at a time (one launch + combine per
+    // pass) so the partial buffer stays within its budget; each launch's queue holds the pass's
+    // chunks [chunk_begin, chunk_begin + pass_n): its pass_big big chunks first, then its tail
+    // chunks. The combine continues the same left fold over chunks, so passes never change bits.
+    uint32_t pass_chunks;     // chunks per pass (host: partial budget / pixels), >= 1
+    uint32_t chunk_begin;     // this launch's first chunk (set per pass by launch_render)
+    uint32_t pass_n;          // this launch's chunks
+    uint32_t pass_big;        // this launch's big chunks (they precede its tail chunks)
+    uint32_t n_big_units;     // n_work_tiles * pass_big * 64
+    uint32_t n_units;         // n_work_tiles * pass_n * 64
     uint32_t n_cus;           // compute units of the device (grid sizing)
     uint32_t *unit_counter;   // device queue head (zeroed per launch)
-    float4 *partial;          // [tile pixel][chunk] partial sums when n_chunks > 1
+    float4 *partial;          // [pass chunk][tile pixel] partial sums when n_chunks > 1: a chunk's
+                              // pixels are contiguous, so an 8x8 tile's rows fill whole 128-B lines
 };
 
 // Traversal stack entries held in LDS per lane: up to 64 (BVH depth <= 63).

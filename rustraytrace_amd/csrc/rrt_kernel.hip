@@ -414,10 +414,11 @@ __device__ __forceinline__ bool medium_hit(const PR &pr, int m, V3 o, V3 d, cons
 // Sphere::hit (sphere.rs:24-51) root selection; returns true and shrinks `closest`.
 template <bool kCount, class PR>
 __device__ __forceinline__ void test_prims(const PR &prim_cr, int first, int count, V3 o, V3 d,
-                                           float a, float &closest, int &hit_prim, Counters &cnt) {
+                                           float a, int skip, float &closest, int &hit_prim, Counters &cnt) {
     static_assert(!PR::kHasQuads, "book-2 scenes (quads, motion) use the binary BVH");
     for (int i = first; i < first + count; ++i) {
         if (kCount) cnt.spheres++;
+        if (i == skip) continue;
         const float4 cr = prim_cr.at(i);
         const V3 oc = v3(cr.x - o.x, cr.y - o.y, cr.z - o.z);
 #if RRT_SPHERE_FMA
@@ -443,9 +444,10 @@ __device__ __forceinline__ void test_prims(const PR &prim_cr, int first, int cou
 
 // Leaf primitives [first, first + count): the hit leaf children of one node visit, which are
 // adjacent in primitive order (sibling leaves split one range, rrt_host.cpp flatten2).
+// `skip` is the primitive the ray is leaving (exit_skip): tested and counted, never accepted.
 template <bool kCount, class PR>
 __device__ __forceinline__ void test_range(const PR &prim_cr, int first, int count, V3 o, V3 d, const RayK &rk,
-                                           float &closest, int &hit_prim, Counters &cnt) {
+                                           int skip, float &closest, int &hit_prim, Counters &cnt) {
     const float a = rk.a;
     for (int i = first; i < first + count; ++i) {
         if (kCount) cnt.spheres++;
@@ -461,7 +463,7 @@ __device__ __forceinline__ void test_range(const PR &prim_cr, int first, int cou
                 bool hit;
                 if (PR::kHasMedia && j >= (int)prim_cr.n_quads) hit = medium_hit(prim_cr, j - (int)prim_cr.n_quads, o, d, rk, closest, tq);
                 else hit = quad_hit(prim_cr.qd[j], o, d, 0.001f, closest, tq);
-                if (hit) {
+                if (hit && i != skip) {
                     closest = tq;
                     hit_prim = i;
                 }
@@ -489,7 +491,7 @@ __device__ __forceinline__ void test_range(const PR &prim_cr, int first, int cou
         const bool ok0 = 0.001f < r0 && r0 < closest;
         const bool ok1 = 0.001f < r1 && r1 < closest;
         const float root = ok0 ? r0 : r1;
-        if (ok0 || ok1) {
+        if ((ok0 || ok1) && i != skip) {
             closest = root;
             hit_prim = i;
         }
@@ -596,17 +598,17 @@ __device__ __forceinline__ bool trav_node(const Node *__restrict__ nodes, Stack 
 
 // The postponed leaf tests of one node visit (leaf 0's primitives, then leaf 1's).
 template <bool kCount, class PR>
-__device__ __forceinline__ void trav_leaves(const PR &prims, Leaves lv, V3 o, V3 d, const RayK &rk, Trav &t,
+__device__ __forceinline__ void trav_leaves(const PR &prims, Leaves lv, V3 o, V3 d, const RayK &rk, int skip, Trav &t,
                                             Counters &cnt) {
-    test_range<kCount>(prims, (int)(lv & kLinkFirstMask), (int)(lv >> kLinkCountShift), o, d, rk, t.closest, t.hit_prim,
-                       cnt);
+    test_range<kCount>(prims, (int)(lv & kLinkFirstMask), (int)(lv >> kLinkCountShift), o, d, rk, skip, t.closest,
+                       t.hit_prim, cnt);
 }
 
 // BVH4 step: test the 4 child boxes, test leaf children's spheres in place, then descend
 // into the nearest internal child and push the others farthest-first (5-exchange sort).
 template <bool kCount, typename Stack, class PR>
 __device__ __forceinline__ bool trav_step4(const GNode4 *__restrict__ nodes, const PR &prims,
-                                           Stack &stack, V3 o, V3 d, const RayK &rk, Trav &t, Counters &cnt) {
+                                           Stack &stack, V3 o, V3 d, const RayK &rk, int skip, Trav &t, Counters &cnt) {
     const GNode4 n = nodes[t.node];
     if (kCount) { cnt.nodes++; cnt.boxes += 4; }
     const float lox[4] = {n.lox.x, n.lox.y, n.lox.z, n.lox.w}, hix[4] = {n.hix.x, n.hix.y, n.hix.z, n.hix.w};
@@ -626,7 +628,8 @@ __device__ __forceinline__ bool trav_step4(const GNode4 *__restrict__ nodes, con
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         if (count[c] > 0) {
-            if (key[c] < __builtin_inff()) test_prims<kCount>(prims, child[c], count[c], o, d, rk.a, t.closest, t.hit_prim, cnt);
+            if (key[c] < __builtin_inff())
+                test_prims<kCount>(prims, child[c], count[c], o, d, rk.a, skip, t.closest, t.hit_prim, cnt);
             key[c] = __builtin_inff();
         }
     }
@@ -670,7 +673,23 @@ struct PathState {
     RngState rng;
     uint32_t k;  // bounce index (camera ray = 0)
     float time;  // the camera ray's time draw, kept by every bounce (book 2, moving spheres)
+    int skip;    // leaf-order primitive the current segment leaves (exit_skip), -1 none
 };
+
+// The primitive a scattered ray cannot meet again in exact arithmetic, skipped by its next
+// closest-hit query (the oracle's exit_skip, oracle/rrt_oracle.cpp): a sphere it leaves
+// outward (convex: a ray from its surface with d.n_out > 0 meets it only at t = 0), or the
+// quad it leaves (a plane is met once). In f32 the hit point lies up to ~ulp(|center|) off the
+// surface and |oc|^2 - r^2 cancels two ~|oc|^2 values (the r = 1000 ground sphere: ulp 0.0625),
+// so a grazing bounce would re-hit the surface it leaves past tmin = 0.001 and be trapped
+// inside the ground sphere: +0.71 % rays and -0.21 % radiance on C2 against the f64 books
+// path, which never does. -1 for a medium, or a ray entering / staying inside a sphere.
+// `nrm` faces the incoming ray, so d.nrm > 0 keeps the ray on the side it came from.
+__device__ __forceinline__ int exit_skip(bool is_quad, bool is_medium, bool front, V3 dir, V3 nrm, int prim) {
+    if (is_medium) return -1;
+    if (is_quad) return prim;
+    return ((dot(dir, nrm) > 0.0f) == front) ? prim : -1;
+}
 
 // Camera::get_ray (camera.rs:152-180) for global pixel (x, y) and the path's RNG.
 template <bool kStrat>
@@ -703,6 +722,7 @@ __device__ __forceinline__ void camera_ray(const KParams &P, uint32_t x, uint32_
     }
     ps.time = 0.0f;
     if (P.flags & 0x1u) ps.time = rnd(ps.rng);  // RRT_FLAG_RAY_TIME (the_next_week/camera.rs:160)
+    ps.skip = -1;
     ps.o = origin;
     ps.d = sub(sample, origin);
     ps.T = v3(1.0f, 1.0f, 1.0f);
@@ -878,11 +898,14 @@ __device__ __forceinline__ bool shade(const KParams &P, const PR &prims, const G
     const float4 cr = prims.at(prim);  // the sphere's center at the ray's time (sphere.rs:48)
     const V3 p = v3(ps.o.x + ps.d.x * t, ps.o.y + ps.d.y * t, ps.o.z + ps.d.z * t);
     V3 outward;
+    bool is_quad = false, is_medium = false;
     if (PR::kHasQuads && cr.w < 0.0f) {  // a quad's plane normal (quad.rs:79); a medium's (1, 0, 0)
         const int j = (int)(-cr.w) - 1;
         if (PR::kHasMedia && j >= (int)prims.n_quads) {
+            is_medium = true;
             outward = v3(1.0f, 0.0f, 0.0f);  // constant_medium.rs:76-82 (front_face true)
         } else {
+            is_quad = true;
             const float4 qn = prims.qd[j].n;
             outward = v3(qn.x, qn.y, qn.z);
         }
@@ -954,6 +977,7 @@ __device__ __forceinline__ bool shade(const KParams &P, const PR &prims, const G
     ps.o = p;
     ps.d = dir;
     ps.k++;
+    ps.skip = exit_skip(is_quad, is_medium, front, dir, nrm, prim);
     return false;
 }
 
@@ -1047,11 +1071,14 @@ __device__ __forceinline__ bool shade_b3(const KParams &P, const PR &prims, cons
     const float4 cr = prims.at(prim);
     const V3 p = v3(ps.o.x + ps.d.x * t, ps.o.y + ps.d.y * t, ps.o.z + ps.d.z * t);
     V3 outward;
+    bool is_quad = false, is_medium = false;
     if (cr.w < 0.0f) {
         const int j = (int)(-cr.w) - 1;
         if (j >= (int)prims.n_quads) {
+            is_medium = true;
             outward = v3(1.0f, 0.0f, 0.0f);
         } else {
+            is_quad = true;
             const float4 qn = prims.qd[j].n;
             outward = v3(qn.x, qn.y, qn.z);
         }
@@ -1101,6 +1128,7 @@ __device__ __forceinline__ bool shade_b3(const KParams &P, const PR &prims, cons
         ps.o = p;
         ps.d = dir;
         ps.k++;
+        ps.skip = exit_skip(is_quad, is_medium, front, dir, nrm, prim);
         return false;
     }
     // pdf path: the material's attenuation (texture value at the hit)
@@ -1158,6 +1186,7 @@ __device__ __forceinline__ bool shade_b3(const KParams &P, const PR &prims, cons
     ps.o = p;
     ps.d = dir;
     ps.k++;
+    ps.skip = exit_skip(is_quad, is_medium, front, dir, nrm, prim);
     return false;
 }
 
@@ -1254,12 +1283,12 @@ __device__ __forceinline__ void render_body(const KParams &P) {
                     // big chunks of every tile first, then the tail chunks (small units last)
                     uint32_t t, chunk;
                     if (u < P.n_big_units) {
-                        t = tc / P.n_big;
-                        chunk = tc - t * P.n_big;
+                        t = tc / P.pass_big;
+                        chunk = P.chunk_begin + (tc - t * P.pass_big);
                     } else {
-                        const uint32_t ns = P.n_chunks - P.n_big, tc2 = tc - (P.n_big_units >> 6);
+                        const uint32_t ns = P.pass_n - P.pass_big, tc2 = tc - (P.n_big_units >> 6);
                         t = tc2 / ns;
-                        chunk = P.n_big + (tc2 - t * ns);
+                        chunk = P.chunk_begin + P.pass_big + (tc2 - t * ns);
                     }
                     const uint32_t x = (t % P.tiles_x) * 8u + (lit & 7u);
                     const uint32_t ly = (t / P.tiles_x) * 8u + (lit >> 3);
@@ -1316,7 +1345,7 @@ __device__ __forceinline__ void render_body(const KParams &P) {
                     ph1 += (uint64_t)__popcll(__ballot(tracing));
                 }
                 if (tracing) {
-                    if (trav_step4<kCount>(nodes, pr, stack, ps.o, ps.d, rk, tr, cnt)) tracing = false;
+                    if (trav_step4<kCount>(nodes, pr, stack, ps.o, ps.d, rk, ps.skip, tr, cnt)) tracing = false;
                 }
                 if ((uint32_t)__popcll(__ballot(tracing)) <= min_active) break;
             }
@@ -1341,7 +1370,7 @@ __device__ __forceinline__ void render_body(const KParams &P) {
                 const bool leave = (uint32_t)__popcll(tm) <= min_active;
                 if (pm != 0 && (leave || (uint32_t)__popcll(pm) > leaf_min || (tm & ~pm) == 0)) {
                     if (pend) {
-                        trav_leaves<kCount>(pr, lv, ps.o, ps.d, rk, tr, cnt);
+                        trav_leaves<kCount>(pr, lv, ps.o, ps.d, rk, ps.skip, tr, cnt);
                         pend = false;
                         if (tr.node < 0) tracing = false;
                     }
@@ -1383,7 +1412,7 @@ __device__ __forceinline__ void render_body(const KParams &P) {
                 const size_t px = (size_t)ly * P.width + x;
                 const float4 out = make_float4(sum.x, sum.y, sum.z, (float)(s_hi - (P.sample_begin + chunk_first(P, chunk))));
                 if (P.n_chunks == 1) P.accum[px] = out;
-                else P.partial[px * P.n_chunks + chunk] = out;
+                else P.partial[(size_t)(chunk - P.chunk_begin) * ((size_t)P.tile_rows * P.width) + px] = out;
                 has = false;
             }
         }
@@ -1426,15 +1455,17 @@ __global__ __launch_bounds__(kBlock, kWaves) void rrt_render(KParams P) {
     render_body<kLds, kCount, StackT, kWide, kBook2>(P);
 }
 
-// accum[p] = sum over chunks c = 0..n-1 (in order) of partial[p][c].rgb; w = sample count.
+// The pass's chunk sums into accum, continuing the left fold over chunks in order: the first
+// pass starts from its chunk 0, later passes from the accum so far; w = the tile's sample count.
+// partial is [pass chunk][pixel], so each chunk row is read coalesced.
 __global__ __launch_bounds__(256) void rrt_combine_chunks(const float4 *__restrict__ partial, float4 *__restrict__ accum,
-                                                          uint32_t n_pixels, uint32_t n_chunks, float count) {
+                                                          uint32_t n_pixels, uint32_t n_chunks, uint32_t first,
+                                                          float count) {
     const uint32_t p = blockIdx.x * 256u + threadIdx.x;
     if (p >= n_pixels) return;
-    const float4 *src = partial + (size_t)p * n_chunks;
-    float4 acc = src[0];
-    for (uint32_t c = 1; c < n_chunks; ++c) {
-        const float4 v = src[c];
+    float4 acc = first ? partial[p] : accum[p];
+    for (uint32_t c = first ? 1u : 0u; c < n_chunks; ++c) {
+        const float4 v = partial[(size_t)c * n_pixels + p];
         acc.x = acc.x + v.x;
         acc.y = acc.y + v.y;
         acc.z = acc.z + v.z;
@@ -1507,7 +1538,7 @@ hipError_t launch_variant(const KParams &p, bool count, hipStream_t stream) {
     if (e != hipSuccess || p.n_chunks <= 1) return e;
     const uint32_t n_pixels = p.tile_rows * p.width;
     hipLaunchKernelGGL(rrt_combine_chunks, dim3((n_pixels + 255) / 256), dim3(256), 0, stream, p.partial, p.accum,
-                       n_pixels, p.n_chunks, (float)(p.sample_end - p.sample_begin));
+                       n_pixels, p.pass_n, p.chunk_begin == 0 ? 1u : 0u, (float)(p.sample_end - p.sample_begin));
     return hipGetLastError();
 }
 
@@ -1533,7 +1564,7 @@ hipError_t launch_width(const KParams &p, bool count, hipStream_t stream) {
 
 }  // namespace
 
-hipError_t launch_render_kernel(const KParams &p, bool count, hipStream_t stream) {
+hipError_t launch_render_pass(const KParams &p, bool count, hipStream_t stream) {
     // Variant choice: BVH width, smallest LDS stack that holds the traversal, and the scene
     // staged in LDS when the BVH + spheres fit the per-block budget (RTOW: ~20-26 KB).
     // Book-2 scenes (moving spheres, checker / noise textures): BVH2 only (the host builds a
@@ -1545,6 +1576,30 @@ hipError_t launch_render_kernel(const KParams &p, bool count, hipStream_t stream
         return p.n_quads ? launch_width<false, 2>(p, count, stream) : launch_width<false, 1>(p, count, stream);
     }
     return p.bvh_width == 4 ? launch_width<true, 0>(p, count, stream) : launch_width<false, 0>(p, count, stream);
+}
+
+// One launch (+ combine) per sample pass of at most p.pass_chunks chunks, in chunk order.
+hipError_t launch_render_kernel(const KParams &p, bool count, hipStream_t stream) {
+    if (p.n_chunks <= 1 || p.pass_chunks == 0 || p.pass_chunks >= p.n_chunks) {
+        KParams q = p;
+        q.chunk_begin = 0;
+        q.pass_n = p.n_chunks;
+        q.pass_big = p.n_big;
+        q.n_big_units = p.n_work_tiles * q.pass_big * 64u;
+        q.n_units = p.n_work_tiles * q.pass_n * 64u;
+        return launch_render_pass(q, count, stream);
+    }
+    for (uint32_t cb = 0; cb < p.n_chunks; cb += p.pass_chunks) {
+        KParams q = p;
+        q.chunk_begin = cb;
+        q.pass_n = std::min(p.pass_chunks, p.n_chunks - cb);
+        q.pass_big = cb < p.n_big ? std::min(p.n_big - cb, q.pass_n) : 0u;
+        q.n_big_units = p.n_work_tiles * q.pass_big * 64u;
+        q.n_units = p.n_work_tiles * q.pass_n * 64u;
+        const hipError_t e = launch_render_pass(q, count, stream);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 hipError_t launch_render(const KParams &p, hipStream_t stream) { return launch_render_kernel(p, false, stream); }

@@ -10,6 +10,11 @@ Each case writes <name>.npz with:
     accum          float32 (H, W, 4) TWIN accum (RGB sums, w = sample count)
     rays           closest-hit queries the oracle traced
     ppm            the render_io.rs P3 bytes (uint8 array)
+    books_accum    float64 (H, W, 4) BOOKS accum (the f64 recursive restatement)
+    books_rays     closest-hit queries of the BOOKS render
+
+Round 2 regenerated every fixture: the f32 modes (and the kernel) gained exit_skip (the
+primitive a scattered ray leaves is not tested for a hit again; oracle/rrt_oracle.cpp).
 
     python tests/golden/make_golden.py
 """
@@ -49,9 +54,11 @@ def main():
         acc32 = acc.astype(np.float32)
         assert np.array_equal(acc32.astype(np.float64), acc)
         ppm = rrt.format_ppm_from_accum(scene.width, scene.height, acc32, scene.spp)
+        bacc, brays, _ = oracle.render(scene, oracle.BOOKS, threads=8)
         np.savez_compressed(os.path.join(HERE, name + ".npz"), scene_sha256=np.array(scene_sha(scene)),
                             accum=acc32, rays=np.array(rays, dtype=np.uint64),
-                            ppm=np.frombuffer(ppm, dtype=np.uint8))
+                            ppm=np.frombuffer(ppm, dtype=np.uint8), books_accum=bacc,
+                            books_rays=np.array(brays, dtype=np.uint64))
         print(name, scene.width, scene.height, scene.spp, rays)
 
 
