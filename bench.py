@@ -1,15 +1,21 @@
-"""Benchmark: Mrays/s and wall-clock for the RTOW final scene at 1920x1080x512 spp (BASELINE.json
-configs[1] = C2) on MI355X through librrt_hip.so's device-resident C-ABI.
+"""Benchmark: Mrays/s and wall-clock for the RTOW final scene (BASELINE.json metric) on MI355X
+through librrt_hip.so's device-resident C-ABI.
 
-A step = one full C2 frame (every pixel x 512 samples, depth 100) rendered on each rank from
-scene data already resident in HBM (BVH built before timing). Ray = one closest-hit query
-(camera.rs:187), counted on the device by the kernel itself.
+A step = one full frame of the configured workload rendered from scene data already resident in
+HBM (BVH built and uploaded before timing). Ray = one closest-hit query (camera.rs:187), counted
+on the device by the kernel itself.
 
-Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): weak
-scaling. Rank r renders its own C2-sized unit of work — the full frame over samples
-[512 r, 512 (r+1)) of a 512*N spp image — and the partial accums are gathered to rank 0
-over RCCL and summed there in rank order (deterministic). value = rays of all ranks / the
-max over ranks of the timed wall-clock.
+* N = 1 (default): config C2, 1920x1080x512 spp (BASELINE.json configs[1], the metric's config),
+  the whole frame on one GPU, no gather. The line also carries a 1-GPU C3 frame (`c3_one_gpu`,
+  the strong-scaling base of the N > 1 runs), the C1 CPU-path config timed on the CPU and the
+  GPU (`c1`), the wall-clock split and the CPU baseline.
+* N > 1 (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): config C3,
+  3840x2160x2048 spp, tile-split the north star's way: 16-row bands dealt
+  round-robin (band b -> rank b mod N), every rank renders its bands over all samples, and the
+  float tiles are gathered to rank 0 over RCCL inside the timed step (`distributed.gather_rows`).
+  Strong scaling: the frame is fixed, value = all ranks' rays / the max over ranks of the timed
+  wall-clock. `--split samples` is the opt-in weak-scaling mode (every rank renders the whole
+  frame over its own sample range; partial accums summed on rank 0 in rank order).
 """
 from __future__ import annotations
 
@@ -27,10 +33,19 @@ METRIC = "Mrays/sec + wall-clock for 1920×1080×512spp RTOW final scene"
 # (MI355X_MICROARCH.md constants table; cdna_hip_programming.md "CU = 4 x SIMD-32"), so
 # 256 CU x 4 SIMD x 32 lanes x 2 FLOP x 2.4 GHz = 157.3 TFLOP/s; v_pk_fma_f32 has the same peak.
 PEAK_F32_VALU_TFLOPS = 157.3
+PEAK_HBM_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E ~8 TB/s
 FLOP_PER_SPHERE_TEST = 23  # sphere.rs:26-31
 FLOP_PER_BOX_TEST = 12  # aabb.rs:56-82 with hoisted reciprocal
 BYTES_PER_SPHERE_TEST = 16
 BYTES_PER_NODE_VISIT = 56  # per BVH2 node visit: two child boxes (2 x 24 B) + two links (2 x 4 B)
+BAND_ROWS = 16
+SCENES = {
+    "C1": "three-sphere Lambertian scene (books CPU path)",
+    "C2": "RTOW final scene (gpu/mod.rs generator, seed 0x5EED1234)",
+    "C3": "RTOW final scene (gpu/mod.rs generator, seed 0x5EED1234)",
+    "C4": "textured earth sphere (earthmap.jpg) + emissive light",
+    "C5": "10k-sphere stress scene (RTOW generator, grid_half 50)",
+}
 
 
 def parse():
@@ -38,23 +53,59 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="C2", help="workload (BASELINE config name); C2 is the metric's config")
+    ap.add_argument("--config", default=None,
+                    help="workload (BASELINE config name); default C2 (the metric's config) on 1 rank, C3 on N > 1")
+    ap.add_argument("--split", choices=["bands", "samples"], default="bands",
+                    help="bands: C3's row-band tiles, strong scaling (default); samples: whole frame per rank, "
+                         "weak scaling")
     ap.add_argument("--width", type=int, default=None)
     ap.add_argument("--spp", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-breakdown", action="store_true", help="skip the wall-clock split (one extra frame)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_C2.json"),
-                    help="per-launch HBM bytes from rocprofv3 PMC passes (written by tools/pmc_traffic.py)")
+    ap.add_argument("--no-extra", action="store_true", help="skip the 1-GPU C3 frame and the C1 timings")
+    ap.add_argument("--traffic-json", default=None,
+                    help="per-launch HBM bytes from rocprofv3 PMC passes (tools/pmc_traffic.py); "
+                         "default profiles/traffic_<config>.json")
     return ap.parse_args()
 
 
-def cpu_baseline(scene, budget_s):
-    """Oracle BOOKS mode (f64, recursive, the reference's CPU semantics) on this host's cores,
-    over a bounded sample of the same frame: every pixel of C2 at S spp, S sized to ~budget_s."""
+def host_cpus():
+    """The cores this process may run on: its affinity set, capped by a cgroup CPU quota when one
+    is set (a container's share of a large host), plus the machine's count and CPU model."""
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = os.cpu_count() or 1
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(period)))
+    except (OSError, ValueError):
+        pass
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    usable = min(affinity, quota) if quota else affinity
+    return {"threads": usable, "affinity_cpus": affinity, "cgroup_quota_cpus": quota,
+            "machine_cpus": os.cpu_count(), "cpu_model": model}
+
+
+def cpu_baseline(scene, budget_s, cpus):
+    """Oracle BOOKS mode (f64, recursive, the reference's CPU semantics; rayon over rows in the
+    reference, camera.rs:66-67) on every core this process is given, over a bounded sample of the
+    same frame: every pixel of C2 at S spp, S sized to ~budget_s."""
     from oracle import oracle
 
-    threads = min(16, os.cpu_count() or 1)
+    threads = cpus["threads"]
     t = time.perf_counter()
     _, rays1, _ = oracle.render(scene, oracle.BOOKS, samples=(0, 1), threads=threads)
     t1 = time.perf_counter() - t
@@ -71,18 +122,84 @@ def cpu_baseline(scene, budget_s):
         "unit": "Mrays/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{scene.width}x{scene.height} C2 frame at {spp_done} of {scene.spp} spp "
-                  f"(f64 books restatement, {threads} threads, {rays} rays in {secs:.2f} s; "
-                  f"extrapolated full-frame wall-clock {secs * scene.spp / spp_done:.1f} s)",
+        "host": cpus,
+        "sample": f"{scene.width}x{scene.height} {scene.name} frame at {spp_done} of {scene.spp} spp "
+                  f"(f64 books restatement, {threads} threads = every core this process is given, {rays} rays "
+                  f"in {secs:.2f} s; extrapolated full-frame wall-clock {secs * scene.spp / spp_done:.1f} s)",
     }
 
 
+def c1_timings(cpus):
+    """C1, the reference's CPU books path (configs[0]: 3-sphere Lambertian scene, 400x225, 64 spp,
+    depth 8; camera.rs:59-100): the whole frame on the CPU (f64 books restatement, all cores) and
+    on the GPU (HIP-event kernel time, scene resident)."""
+    import numpy as np
+    import torch
+
+    import rustraytrace_amd as rrt
+    from oracle import oracle
+
+    scene = rrt.config_scene("C1")
+    t = time.perf_counter()
+    _, cpu_rays, _ = oracle.render(scene, oracle.BOOKS, threads=cpus["threads"])
+    cpu_s = time.perf_counter() - t
+    ds = rrt.DeviceScene(scene)
+    tile = ds.tile(BAND_ROWS, 0, 1, 0, scene.spp)
+    buf = torch.empty((scene.height, scene.width, 4), dtype=torch.float32, device="cuda")
+    stream = torch.cuda.current_stream()
+    ds.render_tile_async(tile, buf.data_ptr(), stream.cuda_stream)  # warm
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
+    ds.reset_counters()
+    for i in range(5):
+        ev[i].record(stream)
+        ds.render_tile_async(tile, buf.data_ptr(), stream.cuda_stream)
+    ev[5].record(stream)
+    torch.cuda.synchronize()
+    gpu_ms = float(np.mean([ev[i].elapsed_time(ev[i + 1]) for i in range(5)]))
+    gpu_rays = ds.counters()["rays"] // 5
+    ds.close()
+    return {
+        "workload": f"C1 three-sphere Lambertian scene {scene.width}x{scene.height}x{scene.spp}spp depth {scene.max_depth}",
+        "cpu_frame_s": round(cpu_s, 4), "cpu_threads": cpus["threads"], "cpu_rays": cpu_rays,
+        "cpu_mrays_s": round(cpu_rays / cpu_s / 1e6, 2),
+        "gpu_frame_ms": round(gpu_ms, 4), "gpu_rays": gpu_rays, "gpu_mrays_s": round(gpu_rays / gpu_ms / 1e3, 1),
+    }
+
+
+def c3_one_gpu():
+    """One whole C3 frame (3840x2160x2048 spp) on this GPU: the 1-GPU base of the N > 1 strong
+    scaling runs (same config, same band split with one rank)."""
+    import torch
+
+    import rustraytrace_amd as rrt
+
+    scene = rrt.config_scene("C3")
+    ds = rrt.DeviceScene(scene)
+    tile = ds.tile(BAND_ROWS, 0, 1, 0, scene.spp)
+    buf = torch.empty((scene.height, scene.width, 4), dtype=torch.float32, device="cuda")
+    stream = torch.cuda.current_stream()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    a.record(stream)
+    ds.render_tile_async(tile, buf.data_ptr(), stream.cuda_stream)
+    b.record(stream)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t
+    rays = ds.counters()["rays"]
+    ds.close()
+    del buf
+    return {"workload": f"C3 {scene.width}x{scene.height}x{scene.spp}spp, 1 GPU, one frame (no warmup frame)",
+            "frame_s": round(wall, 4), "kernel_ms": round(a.elapsed_time(b), 2), "rays": rays,
+            "mrays_s": round(rays / wall / 1e6, 2)}
+
+
 def wall_clock_breakdown(scene, accum, kernel_ms):
-    """SURVEY 8(d) split of one C2 frame through the library, measured outside the timed
-    region on rank 0: host BVH build, scene creation (BVH build + H2D upload), kernel (the
-    timed loop's average), D2H of the float accum, P3 formatting (render_io.rs), and the
-    end-to-end drop-in call rrt_hip_render (scene + kernel + D2H) plus the P3 write
-    (render_io::write_ppm_from_accum to /dev/null)."""
+    """SURVEY 8(d) split of one frame through the library, measured outside the timed region on
+    rank 0: host BVH build, scene creation (BVH build + H2D upload), kernel (the timed loop's
+    average), D2H of the float accum, P3 formatting (render_io.rs), and the end-to-end drop-in
+    call rrt_hip_render (scene + kernel + D2H) plus the P3 write (render_io::write_ppm_from_accum
+    to /dev/null)."""
     import torch
 
     import rustraytrace_amd as rrt
@@ -120,6 +237,27 @@ def wall_clock_breakdown(scene, accum, kernel_ms):
     }
 
 
+def load_traffic(path, config, W, S, lib_path):
+    """HBM bytes per launch of this config from a tools/pmc_traffic.py record, or (None, None)."""
+    if not os.path.exists(path):
+        return None, None
+    try:
+        with open(path) as f:
+            tj = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    if not (tj.get("config") == config and tj.get("width") == W and tj.get("spp") == S):
+        return None, None
+    import hashlib
+
+    with open(lib_path, "rb") as f:
+        same = hashlib.sha256(f.read()).hexdigest() == tj.get("lib_sha256")
+    src = (f"{os.path.relpath(path, ROOT)}: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes, "
+           f"FETCH_SIZE x2 (gfx950 correction, MI355X_MICROARCH.md HBM section) + WRITE_SIZE, "
+           f"{'this' if same else 'an earlier'} librrt_hip.so build ({tj.get('lib_sha256', '')[:12]})")
+    return tj.get("hbm_bytes_per_launch_fetch_corrected", tj.get("hbm_bytes_per_launch")), src
+
+
 def main():
     args = parse()
     import numpy as np
@@ -127,7 +265,7 @@ def main():
     import torch.distributed as dist
 
     import rustraytrace_amd as rrt
-    from rustraytrace_amd.distributed import gather_sample_ranges
+    from rustraytrace_amd.distributed import band_rows, gather_rows, gather_sample_ranges
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -143,39 +281,48 @@ def main():
         dist.init_process_group(backend, rank=rank, world_size=world, **kw)
     torch.cuda.set_device(device)
 
+    config = args.config or ("C2" if world == 1 else "C3")
+    bands = args.split == "bands"
     kw = {}
     if args.width:
         kw["image_width"] = args.width
     if args.spp:
         kw["samples_per_pixel"] = args.spp
-    scene = rrt.config_scene(args.config, **kw)
+    scene = rrt.config_scene(config, **kw)
     W, H, S = scene.width, scene.height, scene.spp
     ds = rrt.DeviceScene(scene, device=device)
-    tile = ds.tile(band_rows=16, rank=0, n_ranks=1, sample_begin=rank * S, sample_end=(rank + 1) * S)
-    accum = torch.empty((H, W, 4), dtype=torch.float32, device=f"cuda:{device}")
+    if bands:
+        tile = ds.tile(band_rows=BAND_ROWS, rank=rank, n_ranks=world, sample_begin=0, sample_end=S)
+        rows = ds.tile_rows(tile)
+    else:
+        tile = ds.tile(band_rows=BAND_ROWS, rank=0, n_ranks=1, sample_begin=rank * S, sample_end=(rank + 1) * S)
+        rows = H
+    accum = torch.empty((max(rows, 1), W, 4), dtype=torch.float32, device=f"cuda:{device}")
     stream = torch.cuda.current_stream()
+    image = [None]  # rank 0: the gathered frame of the last step
 
-    total = torch.empty_like(accum) if rank == 0 else None
-
-    def gather():  # the one exchange: partial accums -> rank 0, summed in rank order
-        if backend == "gloo":
-            res = gather_sample_ranges(accum.cpu(), dist)
-            if res is not None:
-                total.copy_(res)
+    def gather():  # the one exchange: tiles (bands) or partial accums (samples) -> rank 0
+        src = accum[:rows] if backend == "nccl" else accum[:rows].cpu()
+        if bands:
+            image[0] = gather_rows(src, H, BAND_ROWS, dist)
         else:
-            gather_sample_ranges(accum, dist, out=total)
+            image[0] = gather_sample_ranges(src, dist)
 
     def step(i=None):
         if i is not None:
             k_start[i].record(stream)
-        ds.render_tile_async(tile, accum.data_ptr(), stream.cuda_stream)
+        if rows:
+            ds.render_tile_async(tile, accum.data_ptr(), stream.cuda_stream)
         if i is not None:
             k_end[i].record(stream)
         if world > 1:
             gather()
+            if i is not None:
+                g_end[i].record(stream)
 
     k_start = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     k_end = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    g_end = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -192,49 +339,58 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kernel_ms = [a.elapsed_time(b) for a, b in zip(k_start, k_end)]
-    gather_ms = None
-    if world > 1:  # the exchange step alone, untimed loop: partial accums -> rank 0
-        dist.barrier()
-        torch.cuda.synchronize()
-        t = time.perf_counter()
-        gather()
-        torch.cuda.synchronize()
-        gather_ms = (time.perf_counter() - t) * 1e3
+    gather_ms = [a.elapsed_time(b) for a, b in zip(k_end, g_end)] if world > 1 else None
     ctr = ds.counters()
     rays = ctr["rays"]
+    kmax = float(np.mean(kernel_ms))
     if world > 1:
         red_dev = f"cuda:{device}" if backend == "nccl" else "cpu"
-        t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
+        t = torch.tensor([elapsed, kmax], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed, kmax = float(t[0].item()), float(t[1].item())
         r = torch.tensor([rays], dtype=torch.int64, device=red_dev)
         dist.all_reduce(r, op=dist.ReduceOp.SUM)
         rays = int(r.item())
 
     if rank == 0:
-        work = ds.count_work(tile)  # instrumented twin kernel: same paths, per-frame work counts
+        work = ds.count_work(tile)  # instrumented twin kernel: same paths, per-launch work counts
         avg_kernel_s = float(np.mean(kernel_ms)) / 1e3
         flops = FLOP_PER_SPHERE_TEST * work["sphere_tests"] + FLOP_PER_BOX_TEST * work["box_tests"]
         achieved = flops / avg_kernel_s / 1e12
         alg_bytes = BYTES_PER_SPHERE_TEST * work["sphere_tests"] + BYTES_PER_NODE_VISIT * work["node_visits"]
-        traffic, traffic_src = None, None
-        if os.path.exists(args.traffic_json):
-            try:
-                with open(args.traffic_json) as f:
-                    tj = json.load(f)
-                if tj.get("config") == args.config and tj.get("width") == W and tj.get("spp") == S:
-                    traffic = tj.get("hbm_bytes_per_launch")
-                    import hashlib
-
-                    with open(rrt._lib.LIB_PATH, "rb") as f:
-                        cur = hashlib.sha256(f.read()).hexdigest()
-                    same = cur == tj.get("lib_sha256")
-                    traffic_src = (f"{os.path.relpath(args.traffic_json, ROOT)}: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
-                                   f"passes, {'this' if same else 'an earlier'} librrt_hip.so build "
-                                   f"({tj.get('lib_sha256', '')[:12]})")
-            except (OSError, ValueError):
-                traffic = None
-        rays_per_frame = work["rays"]
+        traffic_json = args.traffic_json or os.path.join(ROOT, "profiles", f"traffic_{config}.json")
+        traffic, traffic_src = (None, None)
+        if rows == H:  # the PMC record is of a whole-frame launch
+            traffic, traffic_src = load_traffic(traffic_json, config, W, S, rrt._lib.LIB_PATH)
+        if bands:
+            split = (f"{BAND_ROWS}-row bands dealt round-robin over {world} rank(s), RCCL gather of the float tiles "
+                     f"to rank 0 inside the timed step" if world > 1 else
+                     "whole frame on 1 GPU (the band split with one rank), no gather")
+        else:
+            split = (f"whole frame per rank over its own {S}-sample range, {world} rank(s), RCCL gather + rank-order "
+                     f"sum of the partial accums on rank 0" if world > 1 else "whole frame on 1 GPU, no gather")
+        if world > 1 and backend == "gloo":
+            split += " (gloo rehearsal: ranks share a GPU, host copies)"
+        roofline = {
+            "bound": "valu",
+            "achieved": round(achieved, 3),
+            "peak": PEAK_F32_VALU_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": round(achieved / PEAK_F32_VALU_TFLOPS, 4),
+            "traffic": traffic,
+            "traffic_source": traffic_src,
+            "hbm_GBps": round(traffic / avg_kernel_s / 1e9, 2) if traffic else None,
+            "hbm_frac": round(traffic / avg_kernel_s / 1e9 / PEAK_HBM_GBPS, 5) if traffic else None,
+            "hbm_note": "measured HBM bytes per launch (PMC) / average kernel time, against 8 TB/s; the scene "
+                        "is read from LDS (C2/C4) or L2 (C5), so HBM is not the bound",
+            "algorithmic_flop_per_launch": flops,
+            "algorithmic_scene_bytes_per_launch": alg_bytes,
+            "lds_l2_scene_read_GBps_algorithmic": round(alg_bytes / avg_kernel_s / 1e9, 1),
+            "note": "f32 VALU issue bound (SURVEY 8d): 23 FLOP/sphere test + 12 FLOP/box test over the "
+                    "average HIP-event kernel time; peak = wave64 v_fma_f32 at 2 cycles on SIMD-32 "
+                    "(SURVEY 8d's 78.6 assumed 16-lane SIMDs). lds_l2_scene_read_GBps_algorithmic = "
+                    "(16 B/sphere test + 56 B/node visit) / kernel time: scene reads served by LDS/L2, not HBM",
+        }
         out = {
             "metric": METRIC,
             "value": round(rays / elapsed / 1e6, 2),
@@ -244,47 +400,42 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if bands else "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic",
             "config": {
-                "workload": f"{args.config} RTOW final scene (gpu/mod.rs generator, seed 0x5EED1234), "
-                            f"{W}x{H}x{S}spp, max_depth {scene.max_depth}, {len(scene.spheres)} spheres",
+                "workload": f"{config} {SCENES.get(config, scene.name)}, {W}x{H}x{S}spp, max_depth {scene.max_depth}, "
+                            f"{len(scene.spheres)} spheres",
                 "image": [W, H],
-                "spp_per_rank": S,
+                "spp": S,
                 "max_depth": scene.max_depth,
-                "parallelism": f"frame x sample-range per rank, {world} rank(s), RCCL gather of float accums",
+                "parallelism": split,
             },
             "wall_clock_s_per_frame": round(elapsed / args.steps, 4),
-            "rays_per_frame": rays_per_frame,
-            "paths_per_frame": work["paths"],
-            "gpaths_per_s": round(work["paths"] * args.steps * world / elapsed / 1e9, 3),
+            "rays_per_step": rays // args.steps,
+            "rank0_rays_per_launch": work["rays"],
+            "rank0_paths_per_launch": work["paths"],
             "sphere_tests_per_s": round(work["sphere_tests"] / avg_kernel_s, 1),
             "kernel_ms_avg": round(avg_kernel_s * 1e3, 3),
+            "kernel_ms_max_over_ranks": round(kmax, 3),
             "bvh": ds.bvh_info(),
-            "roofline": {
-                "bound": "valu",
-                "achieved": round(achieved, 3),
-                "peak": PEAK_F32_VALU_TFLOPS,
-                "unit": "TFLOP/s",
-                "frac": round(achieved / PEAK_F32_VALU_TFLOPS, 4),
-                "traffic": traffic,
-                "traffic_source": traffic_src,
-                "algorithmic_flop_per_launch": flops,
-                "algorithmic_bytes_per_launch": alg_bytes,
-                "effective_fetch_GBps": round(alg_bytes / avg_kernel_s / 1e9, 1),
-                "note": "f32 VALU issue bound (SURVEY 8d): 23 FLOP/sphere test + 12 FLOP/box test over the "
-                        "average HIP-event kernel time; peak = wave64 v_fma_f32 at 2 cycles on SIMD-32 "
-                        "(SURVEY 8d's 78.6 assumed 16-lane SIMDs)",
-            },
+            "roofline": roofline,
         }
+        if gather_ms is not None:
+            out["gather_ms"] = round(float(np.mean(gather_ms)), 3)
+            out["gather_note"] = "rank 0, HIP events between the end of its render and the end of the gather"
+            if bands:
+                out["rows_per_rank"] = [len(band_rows(H, BAND_ROWS, r, world)) for r in range(world)]
         if world == 1 and not args.no_breakdown:
             out["wall_clock_breakdown"] = wall_clock_breakdown(scene, accum, avg_kernel_s * 1e3)
-        if gather_ms is not None:
-            out["gather_ms"] = round(gather_ms, 3)
+        cpus = host_cpus()
+        if world == 1 and not args.no_extra:
+            if config != "C3":
+                out["c3_one_gpu"] = c3_one_gpu()
+            out["c1"] = c1_timings(cpus)
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(scene, args.cpu_seconds)
+            out["cpu_baseline"] = cpu_baseline(scene, args.cpu_seconds, cpus)
         print(json.dumps(out), flush=True)
     ds.close()
     if world > 1:

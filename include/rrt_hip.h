@@ -471,6 +471,16 @@ int32_t rrt_hip_render_rgb8(const RrtCamera *cam,
                             uint32_t total_spp, uint32_t n_gpus, uint32_t flags,
                             uint8_t *rgb8_out);
 
+/* rrt_hip_render_rgb8 with book-2/3 scene data (moving spheres, Perlin tables, quads, media,
+ * light lists); ext may be NULL. Same bytes as rrt_quantize_accum of rrt_hip_render_ex's accum. */
+int32_t rrt_hip_render_rgb8_ex(const RrtCamera *cam,
+                               const RrtSphere *spheres, uint32_t n_spheres,
+                               const RrtMaterial *materials, uint32_t n_materials,
+                               const RrtTexture *textures, uint32_t n_textures,
+                               const RrtSceneExt *ext,
+                               uint32_t total_spp, uint32_t n_gpus, uint32_t flags,
+                               uint8_t *rgb8_out);
+
 /* Enqueue the render_io quantiser on `stream` (hipStream_t, NULL = default): d_accum =
  * n_pixels float4 (RGB sums; w ignored), d_rgb8 = n_pixels*3 bytes, scale 1/samples_per_pixel
  * in f32 as render_io.rs:10 computes it. Asynchronous; byte-identical to rrt_quantize_accum. */

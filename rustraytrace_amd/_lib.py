@@ -62,6 +62,7 @@ EXPORTED_SYMBOLS = (
     "rrt_format_ppm_from_accum",
     "rrt_quantize_accum",
     "rrt_hip_render_rgb8",
+    "rrt_hip_render_rgb8_ex",
     "rrt_quantize_accum_async",
     "rrt_format_pnm_from_rgb8",
     "rrt_write_pnm_from_rgb8",
@@ -230,6 +231,8 @@ def load() -> ctypes.CDLL:
         "rrt_format_ppm_from_accum": (c_int32, [c_uint32, c_uint32, P, c_uint32, P, c_size_t, P]),
         "rrt_quantize_accum": (c_int32, [c_uint32, c_uint32, P, c_uint32, P]),
         "rrt_hip_render_rgb8": (c_int32, [P, P, c_uint32, P, c_uint32, P, c_uint32, c_uint32, c_uint32, c_uint32, P]),
+        "rrt_hip_render_rgb8_ex": (c_int32, [P, P, c_uint32, P, c_uint32, P, c_uint32, P, c_uint32, c_uint32, c_uint32,
+                                             P]),
         "rrt_quantize_accum_async": (c_int32, [c_uint32, P, c_uint32, P, P]),
         "rrt_format_pnm_from_rgb8": (c_int32, [c_uint32, c_uint32, P, c_int32, P, c_size_t, P]),
         "rrt_write_pnm_from_rgb8": (c_int32, [c_uint32, c_uint32, P, c_int32, c_char_p]),

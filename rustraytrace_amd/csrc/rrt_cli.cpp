@@ -194,13 +194,14 @@ int main(int argc, char **argv) {
     std::vector<float> accum;
     std::vector<uint8_t> rgb8;
     int rc;
-    if (!book1 || (host_quantise && !p6)) {  // float accum -> render_io on the host (book 2: rrt_hip_render_ex)
+    if (host_quantise && !p6) {  // float accum -> render_io on the host (rrt_hip_render_ex)
         accum.resize((size_t)w * h * 4);
         rc = rrt_hip_render_ex(&cam, spheres.data(), n, materials.data(), n_mat, nullptr, 0, &ext, spp, gpus, flags,
                                accum.data());
-    } else {  // render_io quantiser on the device (identical bytes), 3 B/pixel to the host
+    } else {  // render_io quantiser on the device (identical bytes), 3 B/pixel to the host, every book
         rgb8.resize((size_t)w * h * 3);
-        rc = rrt_hip_render_rgb8(&cam, spheres.data(), n, materials.data(), n_mat, nullptr, 0, spp, gpus, 0, rgb8.data());
+        rc = rrt_hip_render_rgb8_ex(&cam, spheres.data(), n, materials.data(), n_mat, nullptr, 0, &ext, spp, gpus,
+                                    flags, rgb8.data());
     }
     if (rc) {
         std::fprintf(stderr, "HIP render failed: %s\n", rrt_hip_last_error());  // main.rs:60-65

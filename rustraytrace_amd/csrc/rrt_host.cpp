@@ -1393,6 +1393,15 @@ int32_t rrt_hip_render_rgb8(const RrtCamera *cam, const RrtSphere *spheres, uint
                         n_gpus, flags, nullptr, rgb8_out);
 }
 
+int32_t rrt_hip_render_rgb8_ex(const RrtCamera *cam, const RrtSphere *spheres, uint32_t n_spheres,
+                               const RrtMaterial *materials, uint32_t n_materials, const RrtTexture *textures,
+                               uint32_t n_textures, const RrtSceneExt *ext, uint32_t total_spp, uint32_t n_gpus,
+                               uint32_t flags, uint8_t *rgb8_out) {
+    if (!rgb8_out) return fail(RRT_E_INVALID, "null camera or rgb8_out");
+    return render_frame(cam, spheres, n_spheres, materials, n_materials, textures, n_textures, ext, total_spp,
+                        n_gpus, flags, nullptr, rgb8_out);
+}
+
 int32_t rrt_quantize_accum_async(uint32_t n_pixels, const float *d_accum, uint32_t samples_per_pixel, uint8_t *d_rgb8,
                                  void *stream) {
     if (n_pixels && (!d_accum || !d_rgb8)) return fail(RRT_E_INVALID, "null d_accum or d_rgb8");

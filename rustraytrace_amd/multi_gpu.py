@@ -57,7 +57,10 @@ def main(argv=None) -> int:
     device = local % n_dev
     torch.cuda.set_device(device)
     backend = args.backend or "nccl"
-    if world > 1:
+    # An explicit --backend runs the process group and the gather even with one rank (the
+    # RCCL init + gather path exercised on a one-GPU box; RCCL refuses two ranks on one GPU).
+    use_dist = world > 1 or args.backend is not None
+    if use_dist:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         kw = {"device_id": torch.device(f"cuda:{device}")} if backend == "nccl" else {}
         dist.init_process_group(backend, rank=rank, world_size=world, **kw)
@@ -77,7 +80,7 @@ def main(argv=None) -> int:
     rows = ds.tile_rows(tile)
     accum = torch.empty((max(rows, 1), W, 4), dtype=torch.float32, device=f"cuda:{device}")
     stream = torch.cuda.current_stream()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
     start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -92,7 +95,7 @@ def main(argv=None) -> int:
 
     local_rows = accum[:rows]
     t = time.perf_counter()
-    if world > 1:
+    if use_dist:
         src = local_rows if backend == "nccl" else local_rows.cpu()
         img = gather_rows(src, H, args.band, dist)
         if backend == "nccl":
@@ -100,7 +103,7 @@ def main(argv=None) -> int:
     else:
         img = local_rows
     gather_ms = (time.perf_counter() - t) * 1e3
-    if world > 1:
+    if use_dist:
         dev = f"cuda:{device}" if backend == "nccl" else "cpu"
         stats = torch.tensor([kernel_ms, float(rays)], dtype=torch.float64, device=dev)
         kmax = stats[:1].clone()
@@ -120,11 +123,11 @@ def main(argv=None) -> int:
             else:
                 rrt.write_ppm_from_accum(W, H, host, S, args.out)
         print(json.dumps({
-            "config": args.config, "image": [W, H], "spp": S, "ranks": world, "backend": backend if world > 1 else None,
+            "config": args.config, "image": [W, H], "spp": S, "ranks": world, "backend": backend if use_dist else None,
             "split": f"{args.band}-row bands dealt round-robin", "kernel_ms_max_over_ranks": round(kernel_ms, 3),
             "gather_ms": round(gather_ms, 3), "rays": rays, "mrays_per_s": round(rays / kernel_ms / 1e3, 2),
         }), file=sys.stderr if args.out == "-" else sys.stdout, flush=True)
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
     return 0
 

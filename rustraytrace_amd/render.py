@@ -89,17 +89,20 @@ def render(scene: SceneData, spp: Optional[int] = None, n_gpus: int = 1, quiet: 
 
 
 def render_rgb8(scene: SceneData, spp: Optional[int] = None, n_gpus: int = 1, quiet: bool = True) -> np.ndarray:
-    """rrt_hip_render_rgb8: render and quantise on the device (render_io.rs quantiser);
-    returns (H, W, 3) uint8, identical to quantize_accum(render(scene)) at the same spp."""
+    """rrt_hip_render_rgb8_ex: render and quantise on the device (render_io.rs quantiser);
+    returns (H, W, 3) uint8, identical to quantize_accum(render(scene)) at the same spp, for
+    every book (the scene's RrtSceneExt — motion, Perlin tables, quads, media, lights — is passed)."""
     lib = _lib.load()
     out = np.zeros((scene.height, scene.width, 3), dtype=np.uint8)
     tex, ntex, keep = _textures(scene)
+    ext, keep_ext = scene_ext(scene)
     flags = scene.flags | (_lib.FLAG_QUIET if quiet else 0)
-    _lib.check(lib.rrt_hip_render_rgb8(_lib.ptr(scene.camera), _lib.ptr(scene.spheres), len(scene.spheres),
-                                       _lib.ptr(scene.materials), len(scene.materials),
-                                       ctypes.cast(tex, ctypes.c_void_p) if tex is not None else None, ntex,
-                                       int(spp or 0), int(n_gpus), flags, _lib.ptr(out)))
-    del keep
+    _lib.check(lib.rrt_hip_render_rgb8_ex(_lib.ptr(scene.camera), _lib.ptr(scene.spheres), len(scene.spheres),
+                                          _lib.ptr(scene.materials), len(scene.materials),
+                                          ctypes.cast(tex, ctypes.c_void_p) if tex is not None else None, ntex,
+                                          ctypes.byref(ext) if ext is not None else None,
+                                          int(spp or 0), int(n_gpus), flags, _lib.ptr(out)))
+    del keep, keep_ext
     return out
 
 

@@ -25,22 +25,53 @@ def _free_port():
     return port
 
 
-@pytest.mark.parametrize("ranks", [1, 2, 3])
-def test_row_bands_gathered_equal_one_gpu(tmp_path, ranks):
+@pytest.mark.parametrize("ranks,backend", [(1, "gloo"), (2, "gloo"), (3, "gloo"), (1, "nccl")])
+def test_row_bands_gathered_equal_one_gpu(tmp_path, ranks, backend):
+    # (1, "nccl"): the RCCL process group and gather on the device tensors (RCCL refuses two
+    # ranks on one GPU, so more ranks share the box's GPU over gloo).
     out = str(tmp_path / "accum.npy")
     ppm = str(tmp_path / "img.ppm")
     args = ["--config", "C2", "--width", "96", "--spp", "8", "--depth", "20", "--band", "8",
-            "--backend", "gloo", "--save-accum", out, "--out", ppm]
+            "--backend", backend, "--save-accum", out, "--out", ppm]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ranks}",
            "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", "-m", "rustraytrace_amd.multi_gpu"] + args
     env = dict(os.environ, PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""), OMP_NUM_THREADS="1")
     r = subprocess.run(cmd, capture_output=True, text=True, cwd=ROOT, env=env, timeout=110)
     assert r.returncode == 0, r.stderr[-2000:]
     line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
-    assert line["ranks"] == ranks and line["rays"] > 0
+    assert line["ranks"] == ranks and line["rays"] > 0 and line["backend"] == backend
     scene = rrt.config_scene("C2", image_width=96, samples_per_pixel=8, max_depth=20)
     want = rrt.render(scene)
     got = np.load(out)
     assert got.shape == want.shape and np.array_equal(got, want)
     with open(ppm, "rb") as f:
         assert f.read() == rrt.format_ppm_from_accum(scene.width, scene.height, want, scene.spp)
+
+
+@pytest.mark.parametrize("ranks", [1, 2])
+def test_bench_band_split_line(ranks):
+    # bench.py's N-rank path (C3's row-band split, gather inside the timed step) at a small size:
+    # 2 ranks share the GPU over gloo (RRT_BENCH_BACKEND rehearsal mode); 1 rank runs the C3
+    # default config only when launched with --config.
+    args = ["bench.py", "--gpus", str(ranks), "--config", "C3", "--width", "256", "--spp", "8", "--steps", "2",
+            "--warmup", "1", "--no-cpu-baseline", "--no-breakdown", "--no-extra"]
+    if ranks > 1:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ranks}",
+               "--master-addr", "127.0.0.1", f"--master-port={_free_port()}"] + args
+    else:
+        cmd = [sys.executable] + args
+    env = dict(os.environ, RRT_BENCH_BACKEND="gloo", OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, capture_output=True, text=True, cwd=ROOT, env=env, timeout=110)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == ranks and line["scaling"] == "strong" and line["config"]["image"] == [256, 144]
+    scene = rrt.config_scene("C3", image_width=256, samples_per_pixel=8)
+    ds = rrt.DeviceScene(scene)
+    want = ds.count_work(ds.tile(16, 0, 1, 0, 8))["rays"]
+    ds.close()
+    assert line["rays_per_step"] == want  # every band rendered exactly once per step
+    if ranks > 1:
+        assert "gather_ms" in line and "bands" in line["config"]["parallelism"]
+        assert sum(line["rows_per_rank"]) == 144
+    else:
+        assert "no gather" in line["config"]["parallelism"]

@@ -37,13 +37,21 @@ def test_device_quantiser_matches_host(n_px):
     assert np.array_equal(want, oracle.quantize_render_io(acc, spp))
 
 
-@pytest.mark.parametrize("cfg", ["rtow", "earth"])
+@pytest.mark.parametrize("cfg", ["rtow", "earth", "bouncing", "perlin", "cornell_box", "cornell_smoke", "book3"])
 def test_render_rgb8_equals_quantised_accum(cfg):
+    # Every book through rrt_hip_render_rgb8_ex: moving spheres (bouncing), Perlin tables,
+    # quads, media and the book-3 light list must reach the device quantiser path too.
     _torch()
+    small = dict(image_width=64, samples_per_pixel=9, max_depth=10)
     if cfg == "rtow":
         scene = rrt.rtow(image_width=96, samples_per_pixel=6, max_depth=10)
-    else:
+    elif cfg == "earth":
         scene = rrt.earth_light(image_width=80, samples_per_pixel=5, max_depth=8)
+    elif cfg == "book3":
+        scene = rrt.rest_of_your_life_scene(small)
+    else:
+        k = {"bouncing": 1, "perlin": 4, "cornell_box": 7, "cornell_smoke": 8}[cfg]
+        scene = rrt.next_week_scene(k, small)
     acc = rrt.render(scene)
     rgb = rrt.render_rgb8(scene)
     assert rgb.shape == (scene.height, scene.width, 3)
