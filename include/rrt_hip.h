@@ -456,6 +456,14 @@ int32_t rrt_format_ppm_from_accum(uint32_t width, uint32_t height, const float *
 int32_t rrt_quantize_accum(uint32_t width, uint32_t height, const float *accum,
                            uint32_t samples_per_pixel, uint8_t *rgb8);
 
+/* == books::in_one_weekend::color::write_color (color.rs:6-32), the books CPU path's quantiser,
+ * over a float accum: per channel x = (1.0 / spp) * sum in f64 (camera.rs:107, 80), sqrt if
+ * x > 0 else 0, Interval(0, 0.999).clamp, (256 * x) as i32 — so +inf gives 255 and NaN 0, where
+ * render_io maps every non-finite value to 0. rgb8[3*W*H]; format P3 (the same "r g b" lines
+ * camera.rs:87-94 prints) with rrt_format_pnm_from_rgb8. spp >= 1. */
+int32_t rrt_quantize_accum_books(uint32_t width, uint32_t height, const float *accum,
+                                 uint32_t samples_per_pixel, uint8_t *rgb8);
+
 /* ---- output step after the boundary: device quantiser, P6 ---------------
  * render_io.rs writes P3 ASCII (~25 MB at 1080p) from a float accum copied to the host
  * (16 B/pixel). These entries quantise on the device (3 B/pixel over PCIe) and format P3 or

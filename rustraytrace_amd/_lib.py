@@ -63,6 +63,7 @@ EXPORTED_SYMBOLS = (
     "rrt_quantize_accum",
     "rrt_hip_render_rgb8",
     "rrt_hip_render_rgb8_ex",
+    "rrt_quantize_accum_books",
     "rrt_quantize_accum_async",
     "rrt_format_pnm_from_rgb8",
     "rrt_write_pnm_from_rgb8",
@@ -230,6 +231,7 @@ def load() -> ctypes.CDLL:
         "rrt_write_ppm_from_accum": (c_int32, [c_uint32, c_uint32, P, c_uint32, c_char_p]),
         "rrt_format_ppm_from_accum": (c_int32, [c_uint32, c_uint32, P, c_uint32, P, c_size_t, P]),
         "rrt_quantize_accum": (c_int32, [c_uint32, c_uint32, P, c_uint32, P]),
+        "rrt_quantize_accum_books": (c_int32, [c_uint32, c_uint32, P, c_uint32, P]),
         "rrt_hip_render_rgb8": (c_int32, [P, P, c_uint32, P, c_uint32, P, c_uint32, c_uint32, c_uint32, c_uint32, P]),
         "rrt_hip_render_rgb8_ex": (c_int32, [P, P, c_uint32, P, c_uint32, P, c_uint32, P, c_uint32, c_uint32, c_uint32,
                                              P]),

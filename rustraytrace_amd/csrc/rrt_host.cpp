@@ -2090,6 +2090,26 @@ static void quantize_rgb8(size_t n_px, const float *accum, uint32_t spp, uint8_t
     });
 }
 
+// color.rs:6-32 write_color for one channel of pixel_samples_scale * pixel_color (f64, the books
+// CPU path's quantiser): linear_to_gamma (sqrt of a positive value, else 0), Interval(0, 0.999)
+// clamp (NaN passes through: both comparisons are false), 256 * x `as i32` (NaN -> 0, +inf was
+// clamped to 0.999 -> 255).
+static inline uint8_t books_channel(double x) {
+    x = x > 0.0 ? std::sqrt(x) : 0.0;
+    if (x < 0.0) x = 0.0;
+    if (x > 0.999) x = 0.999;
+    const double v = 256.0 * x;
+    return v != v ? (uint8_t)0 : (uint8_t)(int32_t)v;
+}
+
+static void quantize_rgb8_books(size_t n_px, const float *accum, uint32_t spp, uint8_t *rgb8) {
+    const double scale = 1.0 / (double)spp;  // camera.rs:107 pixel_samples_scale (spp >= 1)
+    parallel_chunks(n_px, 1u << 16, [&](size_t b, size_t e, unsigned) {
+        for (size_t i = b; i < e; ++i)
+            for (int c = 0; c < 3; ++c) rgb8[i * 3 + c] = books_channel(scale * (double)accum[i * 4 + c]);
+    });
+}
+
 // Decimal strings of 0..255 (no leading zeros) for the P3 "r g b\n" lines.
 struct DecTable {
     char s[256][4];
@@ -2170,6 +2190,13 @@ extern "C" {
 int32_t rrt_quantize_accum(uint32_t width, uint32_t height, const float *accum, uint32_t spp, uint8_t *rgb8) {
     if ((!accum || !rgb8) && (size_t)width * height) return fail(RRT_E_INVALID, "null accum or rgb8");
     quantize_rgb8((size_t)width * height, accum, spp, rgb8);
+    return RRT_OK;
+}
+
+int32_t rrt_quantize_accum_books(uint32_t width, uint32_t height, const float *accum, uint32_t spp, uint8_t *rgb8) {
+    if ((!accum || !rgb8) && (size_t)width * height) return fail(RRT_E_INVALID, "null accum or rgb8");
+    if (spp == 0) return fail(RRT_E_INVALID, "samples_per_pixel must be >= 1 (camera.rs pixel_samples_scale)");
+    quantize_rgb8_books((size_t)width * height, accum, spp, rgb8);
     return RRT_OK;
 }
 

@@ -166,6 +166,16 @@ def quantize_accum(width: int, height: int, accum: np.ndarray, samples_per_pixel
     return out
 
 
+def quantize_accum_books(width: int, height: int, accum: np.ndarray, samples_per_pixel: int) -> np.ndarray:
+    """color.rs:6-32 write_color (the books CPU path's f64 quantiser) over a float accum:
+    (H, W, 3) uint8. Differs from quantize_accum (render_io.rs) only on non-finite sums
+    (+inf -> 255 here, 0 there) and where f64 vs f32 scaling crosses a byte boundary."""
+    accum = np.ascontiguousarray(accum, dtype=np.float32)
+    out = np.zeros((height, width, 3), dtype=np.uint8)
+    _lib.check(_lib.load().rrt_quantize_accum_books(width, height, _lib.ptr(accum), samples_per_pixel, _lib.ptr(out)))
+    return out
+
+
 def device_count() -> int:
     n = ctypes.c_int32(0)
     _lib.check(_lib.load().rrt_device_count(ctypes.byref(n)))

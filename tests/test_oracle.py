@@ -119,6 +119,27 @@ def test_render_io_quantiser_edges_match_product():
     assert [list(map(int, l.split())) for l in lines[3:]] == ref.tolist()
 
 
+def test_books_quantiser_matches_write_color():
+    # product rrt_quantize_accum_books == the oracle's color.rs:6-32 restatement, per channel:
+    # (1/spp) * sum in f64, then write_color (inf -> 255, NaN -> 0)
+    spp = 7
+    rng = np.random.default_rng(5)
+    sums = np.concatenate([
+        np.array([0.0, 0.25, 1.0, 0.999 ** 2, INF, -INF, float("nan"), -0.5, 1e30, 4.0, 0.01, 3.99]) * spp,
+        rng.uniform(0, 1.2 * spp, 500), rng.uniform(0, 1e-4, 100)]).astype(np.float32)
+    n = len(sums) // 3
+    acc = np.zeros((n, 4), np.float32)
+    acc[:, :3] = sums[: 3 * n].reshape(n, 3)
+    got = rrt.quantize_accum_books(n, 1, acc, spp).reshape(-1, 3)
+    scale = 1.0 / spp
+    want = np.array([oracle.write_color(scale * acc[i, :3].astype(np.float64)) for i in range(n)])
+    assert np.array_equal(got, want)
+    # rows: (0, .25, 1), (.998, inf, -inf), (nan, -.5, 1e30): inf -> 255 in color.rs (render_io: 0)
+    assert got[:3].tolist() == [[0, 128, 255], [255, 255, 0], [0, 0, 255]]
+    with pytest.raises(rrt.RrtError):
+        rrt.quantize_accum_books(1, 1, acc[:1], 0)
+
+
 # ---- camera / image height (camera.rs:102-150, gpu/mod.rs:174-198) ----------------------------
 @pytest.mark.parametrize("w,h", [(400, 225), (1920, 1080), (3840, 2160), (64, 36), (1, 1)])
 def test_image_height(w, h):
