@@ -18,13 +18,19 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def counter(d, name):
-    vals = []
+def counter(d, name, kernel="rrt_render"):
+    """Average per dispatch of `name` over the dispatches whose kernel name contains `kernel`
+    (rocprofv3 writes one row per dispatch and counter; values summed over the row's dimensions)."""
+    per = {}
     for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(path)):
-            if "rrt_render" in r["Kernel_Name"] and r["Counter_Name"] == name:
-                vals.append(float(r["Counter_Value"]))
+            if kernel in r["Kernel_Name"] and r["Counter_Name"] == name:
+                key = (path, r.get("Dispatch_Id") or r.get("Correlation_Id") or len(per))
+                per[key] = per.get(key, 0.0) + float(r["Counter_Value"])
+    vals = list(per.values())
     if not vals:
+        if kernel != "rrt_render":
+            return 0.0, 0
         raise SystemExit(f"no {name} rows in {d}")
     return sum(vals) / len(vals), len(vals)
 
@@ -32,6 +38,8 @@ def counter(d, name):
 def main(fetch_dir, write_dir, config, width, spp, out):
     fetch_kib, n1 = counter(fetch_dir, "FETCH_SIZE")
     write_kib, n2 = counter(write_dir, "WRITE_SIZE")
+    cf_kib, nc = counter(fetch_dir, "FETCH_SIZE", "rrt_combine_chunks")
+    cw_kib, _ = counter(write_dir, "WRITE_SIZE", "rrt_combine_chunks")
     so = os.path.join(ROOT, "rustraytrace_amd", "librrt_hip.so")
     rec = {
         "config": config,
@@ -42,6 +50,9 @@ def main(fetch_dir, write_dir, config, width, spp, out):
         "write_size_kib": write_kib,
         "hbm_bytes_per_launch": int((fetch_kib + write_kib) * 1024),
         "hbm_bytes_per_launch_fetch_corrected": int((2 * fetch_kib + write_kib) * 1024),
+        "combine_dispatches": nc,
+        "combine_fetch_size_kib": cf_kib,
+        "combine_write_size_kib": cw_kib,
         "lib_sha256": hashlib.sha256(open(so, "rb").read()).hexdigest(),
         "note": "separate --pmc passes FETCH_SIZE / WRITE_SIZE on tools/prof_render.py (1 launch)",
     }
