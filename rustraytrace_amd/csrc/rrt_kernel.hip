@@ -41,6 +41,12 @@ namespace {
 #ifndef RRT_PHASE_TIMING
 #define RRT_PHASE_TIMING 0
 #endif
+#ifndef RRT_TRIM
+#define RRT_TRIM 1
+#endif
+#ifndef RRT_HOISTDIV
+#define RRT_HOISTDIV 1
+#endif
 
 // 64 if the calling lane is the wave's first active lane, else 0 (wave-level event count).
 __device__ __forceinline__ uint32_t wave_slot() {
@@ -274,8 +280,9 @@ __device__ __forceinline__ RayK ray_consts(V3 o, V3 d) {
 // [2^-64, 2^64] the expansion's v_div_scale / v_div_fmas / v_div_fixup are identities except
 // when |n| < 2^-103, where both results are below the 0.001 acceptance bound, so every
 // accept/reject decision and every accepted root equals the IEEE quotient (the oracle's).
+template <bool kFast = false>
 __device__ __forceinline__ float div_by_a(float n, const RayK &rk) {
-    if (rk.ra == 0.0f) return n / rk.a;
+    if (!kFast && rk.ra == 0.0f) return n / rk.a;
     const float q0 = n * rk.ra;
     const float e0 = __builtin_fmaf(-rk.a, q0, n);
     const float q1 = __builtin_fmaf(e0, rk.ra, q0);
@@ -445,11 +452,22 @@ __device__ __forceinline__ void test_prims(const PR &prim_cr, int first, int cou
 // Leaf primitives [first, first + count): the hit leaf children of one node visit, which are
 // adjacent in primitive order (sibling leaves split one range, rrt_host.cpp flatten2).
 // `skip` is the primitive the ray is leaving (exit_skip): tested and counted, never accepted.
-template <bool kCount, class PR>
+// The skip primitive is left out of the loop (it can never be accepted), so a lane whose range
+// holds it runs one iteration less. kFastDiv: every active lane's |d|^2 is in the range of the
+// per-ray reciprocal (the caller checked it wave-wide), so the root divisions take no branch.
+template <bool kCount, bool kFastDiv, class PR>
 __device__ __forceinline__ void test_range(const PR &prim_cr, int first, int count, V3 o, V3 d, const RayK &rk,
                                            int skip, float &closest, int &hit_prim, Counters &cnt) {
     const float a = rk.a;
+#if RRT_TRIM
+    const bool trim = (uint32_t)(skip - first) < (uint32_t)count;
+    const int n = count - (trim ? 1 : 0);
+    const int gap = trim ? skip : 0x7fffffff;
+    for (int k = 0; k < n; ++k) {
+        const int i = first + k + (first + k >= gap ? 1 : 0);
+#else
     for (int i = first; i < first + count; ++i) {
+#endif
         if (kCount) cnt.spheres++;
         if constexpr (RRT_PHASE_TIMING == 3) {
             cnt.d0 += wave_slot();
@@ -463,7 +481,7 @@ __device__ __forceinline__ void test_range(const PR &prim_cr, int first, int cou
                 bool hit;
                 if (PR::kHasMedia && j >= (int)prim_cr.n_quads) hit = medium_hit(prim_cr, j - (int)prim_cr.n_quads, o, d, rk, closest, tq);
                 else hit = quad_hit(prim_cr.qd[j], o, d, 0.001f, closest, tq);
-                if (hit && i != skip) {
+                if (hit && (RRT_TRIM || i != skip)) {
                     closest = tq;
                     hit_prim = i;
                 }
@@ -486,12 +504,12 @@ __device__ __forceinline__ void test_range(const PR &prim_cr, int first, int cou
         // whether or not the near one is accepted changes nothing, and the select form keeps the
         // leaf loop free of exec-mask branches and phi copies
         const float sq = __builtin_sqrtf(disc);
-        const float r0 = div_by_a(h - sq, rk);
-        const float r1 = div_by_a(h + sq, rk);
+        const float r0 = div_by_a<kFastDiv>(h - sq, rk);
+        const float r1 = div_by_a<kFastDiv>(h + sq, rk);
         const bool ok0 = 0.001f < r0 && r0 < closest;
         const bool ok1 = 0.001f < r1 && r1 < closest;
         const float root = ok0 ? r0 : r1;
-        if ((ok0 || ok1) && i != skip) {
+        if ((ok0 || ok1) && (RRT_TRIM || i != skip)) {
             closest = root;
             hit_prim = i;
         }
@@ -600,8 +618,14 @@ __device__ __forceinline__ bool trav_node(const Node *__restrict__ nodes, Stack 
 template <bool kCount, class PR>
 __device__ __forceinline__ void trav_leaves(const PR &prims, Leaves lv, V3 o, V3 d, const RayK &rk, int skip, Trav &t,
                                             Counters &cnt) {
-    test_range<kCount>(prims, (int)(lv & kLinkFirstMask), (int)(lv >> kLinkCountShift), o, d, rk, skip, t.closest,
-                       t.hit_prim, cnt);
+    const int first = (int)(lv & kLinkFirstMask), count = (int)(lv >> kLinkCountShift);
+#if RRT_HOISTDIV
+    if (__ballot(rk.ra == 0.0f) == 0) {
+        test_range<kCount, true>(prims, first, count, o, d, rk, skip, t.closest, t.hit_prim, cnt);
+        return;
+    }
+#endif
+    test_range<kCount, false>(prims, first, count, o, d, rk, skip, t.closest, t.hit_prim, cnt);
 }
 
 // BVH4 step: test the 4 child boxes, test leaf children's spheres in place, then descend
