@@ -968,9 +968,15 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
             continue;
         }
         const RrtSphere &sp = spheres[order[i]];
-        prim_cr[i] = make_float4(sp.center_radius[0], sp.center_radius[1], sp.center_radius[2],
-                                 std::max(sp.center_radius[3], 0.0f));
+        const float r = std::max(sp.center_radius[3], 0.0f);
         prim_mtl[i] = mats[sp.material_index];
+        if (book2) {
+            prim_cr[i] = make_float4(sp.center_radius[0], sp.center_radius[1], sp.center_radius[2], r);
+        } else {  // book-1 kernel layout: r * r in the record (one multiply less per test), r in b.w
+            const volatile float r2 = r * r;  // f32, rounded once like the kernel's r * r
+            prim_cr[i] = make_float4(sp.center_radius[0], sp.center_radius[1], sp.center_radius[2], r2);
+            std::memcpy(&prim_mtl[i].b.w, &r, sizeof(float));
+        }
         if (motion) {
             const float *m = motion + 4 * (size_t)order[i];
             prim_motion[i] = make_float4(m[0], m[1], m[2], 0.0f);

@@ -35,14 +35,14 @@ namespace {
 //   2: traversal wave-iterations x 64 / sum of tracing lanes per iteration / outer iterations
 //   3: leaf-loop wave-iterations x 64 / active lanes per leaf iteration / lanes taking the root branch
 //   4: shade entries x 64 / shading lanes / rejection-loop wave-iterations x 64
-#ifndef RRT_SPHERE_FMA
-#define RRT_SPHERE_FMA 0
-#endif
 #ifndef RRT_PHASE_TIMING
 #define RRT_PHASE_TIMING 0
 #endif
 #ifndef RRT_TRIM
 #define RRT_TRIM 1
+#endif
+#ifndef RRT_LEAN
+#define RRT_LEAN 1
 #endif
 #ifndef RRT_HOISTDIV
 #define RRT_HOISTDIV 1
@@ -113,8 +113,11 @@ __device__ __forceinline__ float rnd(RngState &s) { return (float)(rng_next(s) >
 // random_double_range(lo,hi) = u*(hi-lo) + lo  (rand 0.8 UniformFloat::sample_single order)
 __device__ __forceinline__ float rnd_range(RngState &s, float lo, float hi) { return rnd(s) * (hi - lo) + lo; }
 // rnd_range(s, -1, 1) in one rounding less work: u * 2^-24 * 2 is exact (power-of-two scalings
-// of a 24-bit integer), so u * 2^-23 - 1 rounds once, at the same add — identical bits.
-__device__ __forceinline__ float rnd_pm1(RngState &s) { return (float)(rng_next(s) >> 8) * 0x1.0p-23f - 1.0f; }
+// of a 24-bit integer), so u * 2^-23 - 1 rounds once, at the add — and fma(u, 2^-23, -1) rounds
+// the same exact product once: identical bits in one instruction.
+__device__ __forceinline__ float rnd_pm1(RngState &s) {
+    return __builtin_fmaf((float)(rng_next(s) >> 8), 0x1.0p-23f, -1.0f);
+}
 
 // vec3.rs:181-189 random_unit_vector: rejection in [-1,1)^3, accept 1e-160 < |p|^2 <= 1
 // (1e-160 underflows to 0 in f32: the one intentional f32 deviation).
@@ -306,6 +309,9 @@ struct Prims {
     uint64_t seg;  // the path's RNG state at this segment ^ (bounce << 32): key of the media draws
     static constexpr bool kHasQuads = kBook2 >= 2;
     static constexpr bool kHasMedia = kBook2 >= 3;
+    // Book-1 scenes store r * r (f32, rounded as the test would round it) in the record's w and
+    // the radius in the material record's b.w (rrt_host.cpp): one multiply less per sphere test.
+    static constexpr bool kR2 = kBook2 == 0;
     __device__ __forceinline__ float4 at(int i) const {
         float4 c = cr[i];
         if constexpr (kBook2) {
@@ -428,15 +434,9 @@ __device__ __forceinline__ void test_prims(const PR &prim_cr, int first, int cou
         if (i == skip) continue;
         const float4 cr = prim_cr.at(i);
         const V3 oc = v3(cr.x - o.x, cr.y - o.y, cr.z - o.z);
-#if RRT_SPHERE_FMA
-        const float h = __builtin_fmaf(d.z, oc.z, __builtin_fmaf(d.y, oc.y, d.x * oc.x));
-        const float c = __builtin_fmaf(-cr.w, cr.w, __builtin_fmaf(oc.z, oc.z, __builtin_fmaf(oc.y, oc.y, oc.x * oc.x)));
-        const float disc = __builtin_fmaf(h, h, -(a * c));
-#else
         const float h = dot(d, oc);
-        const float c = dot(oc, oc) - cr.w * cr.w;
+        const float c = dot(oc, oc) - (PR::kR2 ? cr.w : cr.w * cr.w);
         const float disc = h * h - a * c;
-#endif
         if (disc < 0.0f) continue;
         const float sq = __builtin_sqrtf(disc);
         float root = (h - sq) / a;
@@ -489,15 +489,24 @@ __device__ __forceinline__ void test_range(const PR &prim_cr, int first, int cou
             }
         }
         const V3 oc = v3(cr.x - o.x, cr.y - o.y, cr.z - o.z);
-#if RRT_SPHERE_FMA
-        const float h = __builtin_fmaf(d.z, oc.z, __builtin_fmaf(d.y, oc.y, d.x * oc.x));
-        const float c = __builtin_fmaf(-cr.w, cr.w, __builtin_fmaf(oc.z, oc.z, __builtin_fmaf(oc.y, oc.y, oc.x * oc.x)));
-        const float disc = __builtin_fmaf(h, h, -(a * c));
-#else
         const float h = dot(d, oc);
-        const float c = dot(oc, oc) - cr.w * cr.w;
+        const float c = dot(oc, oc) - (PR::kR2 ? cr.w : cr.w * cr.w);
         const float disc = h * h - a * c;
-#endif
+#if RRT_LEAN
+        // The far root (h + sq) / a is needed only when the near one is at or behind tmin (the
+        // ray starts inside the sphere): r1 >= r0 always (sq >= 0, a > 0, correctly rounded
+        // quotients are monotone), so r0 >= closest rejects both. A wave skips that rare branch
+        // when no lane takes it.
+        if (disc < 0.0f) continue;
+        if constexpr (RRT_PHASE_TIMING == 3) cnt.d2 += 1;
+        const float sq = __builtin_sqrtf(disc);
+        float root = div_by_a<kFastDiv>(h - sq, rk);
+        if (!(0.001f < root)) root = div_by_a<kFastDiv>(h + sq, rk);
+        if (0.001f < root && root < closest && (RRT_TRIM || i != skip)) {
+            closest = root;
+            hit_prim = i;
+        }
+#else
         if (disc < 0.0f) continue;
         if constexpr (RRT_PHASE_TIMING == 3) cnt.d2 += 1;
         // both roots, then selects: the far root is a pure function of (h, sq), so computing it
@@ -513,6 +522,7 @@ __device__ __forceinline__ void test_range(const PR &prim_cr, int first, int cou
             closest = root;
             hit_prim = i;
         }
+#endif
     }
 }
 
@@ -724,8 +734,9 @@ __device__ __forceinline__ void camera_ray(const KParams &P, uint32_t x, uint32_
         ox = (((float)si + rnd(ps.rng)) * P.recip_sqrt_spp) - 0.5f;
         oy = (((float)sj + rnd(ps.rng)) * P.recip_sqrt_spp) - 0.5f;
     } else {
-        ox = rnd(ps.rng) - 0.5f;
-        oy = rnd(ps.rng) - 0.5f;
+        // rnd - 0.5 (sample_square): the product u * 2^-24 is exact, so one fma rounds as the sub does
+        ox = __builtin_fmaf((float)(rng_next(ps.rng) >> 8), 0x1.0p-24f, -0.5f);
+        oy = __builtin_fmaf((float)(rng_next(ps.rng) >> 8), 0x1.0p-24f, -0.5f);
     }
     const float fi = (float)x + ox;
     const float fj = (float)y + oy;
@@ -934,7 +945,8 @@ __device__ __forceinline__ bool shade(const KParams &P, const PR &prims, const G
             outward = v3(qn.x, qn.y, qn.z);
         }
     } else {
-        const float inv_r = 1.0f / cr.w;
+        const float r = PR::kR2 ? __int_as_float(mtl[prim].b.w) : cr.w;
+        const float inv_r = 1.0f / r;
         outward = v3((p.x - cr.x) * inv_r, (p.y - cr.y) * inv_r, (p.z - cr.z) * inv_r);
     }
     const bool front = dot(ps.d, outward) < 0.0f;

@@ -9,6 +9,9 @@ for v in "$@"; do
   i=0
   while read -r group; do
     [ -z "$group" ] && continue
+    # keep only counters this rocprofv3 lists (an unknown name fails the pass)
+    group=$(for c in $group; do grep -qw "${c%_sum}" gpurun_out/counters_list.txt && echo -n "$c "; done)
+    [ -z "$group" ] && continue
     i=$((i+1))
     RRT_LIB_PATH=variants/$v/librrt_hip.so timeout -s KILL 120 rocprofv3 --pmc $group -d gpurun_out/pmc_${v}_$i -o p --output-format csv -- python3 tools/prof_render.py --config C2 --spp ${SPP:-64} --iters 1 > gpurun_out/pmc_${v}_$i.log 2>&1
     rc=$?
