@@ -765,6 +765,14 @@ int fill_params(RrtScene *s, const RrtTile *t, float *d_accum, rrt::KParams &p) 
     if (units > 0xFFFFFFFFull) return fail(RRT_E_INVALID, "tile too large: more than 2^32 work units");
     p.n_units = (uint32_t)units;
     p.n_big_units = p.n_work_tiles * p.n_big * 64u;
+    p.fd_tiles_x = rrt::make_fastdiv(p.tiles_x);
+    p.fd_band_rows = rrt::make_fastdiv(p.band_rows);
+    p.fd_n_ranks = rrt::make_fastdiv(p.n_ranks);
+    p.fd_chunk = rrt::make_fastdiv(p.chunk);
+    p.fd_chunk_small = rrt::make_fastdiv(p.chunk_small);
+    p.fd_sqrt_spp = rrt::make_fastdiv(p.sqrt_spp);
+    p.fd_pass_big = rrt::make_fastdiv(p.n_big);
+    p.fd_pass_tail = rrt::make_fastdiv(p.n_chunks - p.n_big);
     p.unit_counter = s->d_unit_counter;
     p.pass_chunks = p.n_chunks;
     if (p.n_chunks > 1) {  // partial sums [pass chunk][pixel], within the partial budget; grow on demand

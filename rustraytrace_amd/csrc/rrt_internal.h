@@ -100,6 +100,22 @@ struct GTexture {
 };
 
 // Everything the megakernel needs, passed by value (kernarg segment).
+// n / d for 0 <= n < 2^31 and a fixed d >= 1: q = (umulhi(n, m) + n) >> s with s = ceil(log2 d),
+// m = floor(2^32 (2^s - d) / d) + 1 (Granlund-Montgomery; exact, tests/test_oracle.py checks it).
+// d = 0 gives {0, 0} (callers never divide by it).
+struct FastDiv {
+    uint32_t m, s;
+};
+__host__ __device__ inline FastDiv make_fastdiv(uint32_t d) {
+    if (d == 0) return FastDiv{0u, 0u};
+    uint32_t s = 0;
+    while (s < 32 && (1ull << s) < d) ++s;
+    return FastDiv{(uint32_t)((((1ull << s) - d) << 32) / d + 1ull), s};
+}
+__host__ __device__ inline uint32_t fast_div(uint32_t n, FastDiv f) {
+    return (uint32_t)((((uint64_t)n * f.m) >> 32) + n) >> f.s;
+}
+
 struct KParams {
     const void *nodes;           // GNode[] (bvh_width 2) or GNode4[] (bvh_width 4)
     const float4 *prim_cr;       // sphere center.xyz, radius — in BVH leaf order
@@ -174,6 +190,9 @@ struct KParams {
     uint32_t n_big_units;     // n_work_tiles * pass_big * 64
     uint32_t n_units;         // n_work_tiles * pass_n * 64
     uint32_t n_cus;           // compute units of the device (grid sizing)
+    // Division by the queue's uniform divisors as multiply-high + add + shift (FastDiv): the
+    // generic 32-bit division sequence is ~35 instructions, paid at every unit start and end.
+    FastDiv fd_pass_big, fd_pass_tail, fd_tiles_x, fd_band_rows, fd_n_ranks, fd_chunk, fd_chunk_small, fd_sqrt_spp;
     uint32_t *unit_counter;   // device queue head (zeroed per launch)
     float4 *partial;          // [pass chunk][tile pixel] partial sums when n_chunks > 1: a chunk's
                               // pixels are contiguous, so an 8x8 tile's rows fill whole 128-B lines

@@ -730,7 +730,7 @@ template <bool kStrat>
 __device__ __forceinline__ void camera_ray(const KParams &P, uint32_t x, uint32_t y, uint32_t s, PathState &ps) {
     float ox, oy;
     if constexpr (kStrat) {  // sample_square_stratified (the_rest_of_your_life/camera.rs:173-177)
-        const uint32_t sj = s / P.sqrt_spp, si = s - sj * P.sqrt_spp;
+        const uint32_t sj = fast_div(s, P.fd_sqrt_spp), si = s - sj * P.sqrt_spp;
         ox = (((float)si + rnd(ps.rng)) * P.recip_sqrt_spp) - 0.5f;
         oy = (((float)sj + rnd(ps.rng)) * P.recip_sqrt_spp) - 0.5f;
     } else {
@@ -1319,19 +1319,20 @@ __device__ __forceinline__ void render_body(const KParams &P) {
                     // big chunks of every tile first, then the tail chunks (small units last)
                     uint32_t t, chunk;
                     if (u < P.n_big_units) {
-                        t = tc / P.pass_big;
+                        t = fast_div(tc, P.fd_pass_big);
                         chunk = P.chunk_begin + (tc - t * P.pass_big);
                     } else {
                         const uint32_t ns = P.pass_n - P.pass_big, tc2 = tc - (P.n_big_units >> 6);
-                        t = tc2 / ns;
+                        t = fast_div(tc2, P.fd_pass_tail);
                         chunk = P.chunk_begin + P.pass_big + (tc2 - t * ns);
                     }
-                    const uint32_t x = (t % P.tiles_x) * 8u + (lit & 7u);
-                    const uint32_t ly = (t / P.tiles_x) * 8u + (lit >> 3);
+                    const uint32_t ty = fast_div(t, P.fd_tiles_x);
+                    const uint32_t x = (t - ty * P.tiles_x) * 8u + (lit & 7u);
+                    const uint32_t ly = ty * 8u + (lit >> 3);
                     if (x < P.width && ly < P.tile_rows) {
                         // tile-local row -> global image row (row bands dealt round-robin over ranks)
-                        const uint32_t band = ly / P.band_rows;
-                        const uint32_t y = (band * P.n_ranks + P.rank) * P.band_rows + ly % P.band_rows;
+                        const uint32_t band = fast_div(ly, P.fd_band_rows);
+                        const uint32_t y = (band * P.n_ranks + P.rank) * P.band_rows + (ly - band * P.band_rows);
                         xy = x | (y << 16);
                         s = P.sample_begin + chunk_first(P, chunk);
                         s_hi = min(s + (chunk < P.n_big ? P.chunk : P.chunk_small), P.sample_end);
@@ -1442,9 +1443,10 @@ __device__ __forceinline__ void render_body(const KParams &P) {
                 // chunk index and tile-local row, re-derived from (y, s_hi) once per unit
                 const uint32_t rel = s_hi - 1u - P.sample_begin;
                 const uint32_t nbs = P.n_big * P.chunk;
-                const uint32_t chunk = rel < nbs ? rel / P.chunk : P.n_big + (rel - nbs) / P.chunk_small;
-                const uint32_t gb = y / P.band_rows;
-                const uint32_t ly = ((gb - P.rank) / P.n_ranks) * P.band_rows + (y - gb * P.band_rows);
+                const uint32_t chunk =
+                    rel < nbs ? fast_div(rel, P.fd_chunk) : P.n_big + fast_div(rel - nbs, P.fd_chunk_small);
+                const uint32_t gb = fast_div(y, P.fd_band_rows);
+                const uint32_t ly = fast_div(gb - P.rank, P.fd_n_ranks) * P.band_rows + (y - gb * P.band_rows);
                 const size_t px = (size_t)ly * P.width + x;
                 const float4 out = make_float4(sum.x, sum.y, sum.z, (float)(s_hi - (P.sample_begin + chunk_first(P, chunk))));
                 if (P.n_chunks == 1) P.accum[px] = out;
@@ -1623,6 +1625,8 @@ hipError_t launch_render_kernel(const KParams &p, bool count, hipStream_t stream
         q.pass_big = p.n_big;
         q.n_big_units = p.n_work_tiles * q.pass_big * 64u;
         q.n_units = p.n_work_tiles * q.pass_n * 64u;
+        q.fd_pass_big = make_fastdiv(q.pass_big);
+        q.fd_pass_tail = make_fastdiv(q.pass_n - q.pass_big);
         return launch_render_pass(q, count, stream);
     }
     for (uint32_t cb = 0; cb < p.n_chunks; cb += p.pass_chunks) {
@@ -1632,6 +1636,8 @@ hipError_t launch_render_kernel(const KParams &p, bool count, hipStream_t stream
         q.pass_big = cb < p.n_big ? std::min(p.n_big - cb, q.pass_n) : 0u;
         q.n_big_units = p.n_work_tiles * q.pass_big * 64u;
         q.n_units = p.n_work_tiles * q.pass_n * 64u;
+        q.fd_pass_big = make_fastdiv(q.pass_big);
+        q.fd_pass_tail = make_fastdiv(q.pass_n - q.pass_big);
         const hipError_t e = launch_render_pass(q, count, stream);
         if (e != hipSuccess) return e;
     }
