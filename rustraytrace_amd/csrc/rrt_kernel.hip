@@ -692,7 +692,10 @@ __device__ __forceinline__ bool trav_step4(const GNode4 *__restrict__ nodes, con
         t.node = idx[0];
         return false;
     }
-    if (t.sp == 0) return true;
+    if (t.sp == 0) {
+        t.node = -1;
+        return true;
+    }
     --t.sp;
     t.node = stack.load(t.sp);
     return false;
@@ -1288,8 +1291,11 @@ __device__ __forceinline__ void render_body(const KParams &P) {
     V3 sum = v3(0.0f, 0.0f, 0.0f);
     PathState ps;
     Trav tr;
+    // A lane is in the tree while tr.node >= 0 (or, inside the BVH2 loop, while it holds postponed
+    // leaf tests): lane state lives in VGPR integers, so updating it in divergent code is one
+    // v_mov instead of the three exec-mask merges a bool held in an SGPR pair costs.
+    tr.node = -1;
     bool need_ray = false;  // the lane must start the next segment of its path
-    bool tracing = false;
     uint32_t pool_base = 0, pool_left = 0;  // wave-uniform: claimed, not yet assigned units
     [[maybe_unused]] uint64_t ph0 = 0, ph1 = 0, ph2 = 0, tp = 0;
     for (;;) {
@@ -1358,7 +1364,6 @@ __device__ __forceinline__ void render_body(const KParams &P) {
             } else {
                 trav_begin(tr);
                 need_ray = false;
-                tracing = true;
                 started = true;
             }
         }
@@ -1373,43 +1378,39 @@ __device__ __forceinline__ void render_body(const KParams &P) {
             tp = t;
         }
         RayK rk;
-        if (tracing) rk = ray_consts(ps.o, ps.d);
+        if (tr.node >= 0) rk = ray_consts(ps.o, ps.d);
         const Prims<kBook2> pr{prims, motion, ps.time, P.quads, P.media, P.n_quads, rng_key(ps.rng) ^ ((uint64_t)ps.k << 32)};
         if constexpr (kWide) {
             for (;;) {
                 if constexpr (RRT_PHASE_TIMING == 2) {
                     ph0 += 64;
-                    ph1 += (uint64_t)__popcll(__ballot(tracing));
+                    ph1 += (uint64_t)__popcll(__ballot(tr.node >= 0));
                 }
-                if (tracing) {
-                    if (trav_step4<kCount>(nodes, pr, stack, ps.o, ps.d, rk, ps.skip, tr, cnt)) tracing = false;
-                }
-                if ((uint32_t)__popcll(__ballot(tracing)) <= min_active) break;
+                if (tr.node >= 0) trav_step4<kCount>(nodes, pr, stack, ps.o, ps.d, rk, ps.skip, tr, cnt);
+                if ((uint32_t)__popcll(__ballot(tr.node >= 0)) <= min_active) break;
             }
         } else {
             // BVH2 with postponed leaves: a lane whose visit hit leaf children waits (no further
             // node visits) until the wave runs its leaf loop, which happens once more than
             // leaf_min lanes wait, or no lane can take another node step, or before leaving.
             const uint32_t leaf_min = (live * P.leaf_frac) >> 8;
-            bool pend = false;
-            Leaves lv;
+            Leaves lv = 0;  // the postponed leaf range (0 = none: a range has count >= 1)
             for (;;) {
                 if constexpr (RRT_PHASE_TIMING == 2) {
                     ph0 += 64;
-                    ph1 += (uint64_t)__popcll(__ballot(tracing && !pend));
+                    ph1 += (uint64_t)__popcll(__ballot(tr.node >= 0 && lv == 0));
                 }
-                if (tracing && !pend) {
-                    pend = trav_node<kCount>(nodes, stack, rk, tr, lv, cnt);
-                    if (!pend && tr.node < 0) tracing = false;
+                if (tr.node >= 0 && lv == 0) {
+                    Leaves l;
+                    if (trav_node<kCount>(nodes, stack, rk, tr, l, cnt)) lv = l;
                 }
-                const uint64_t pm = __ballot(pend);
-                const uint64_t tm = __ballot(tracing);  // pend implies tracing
+                const uint64_t pm = __ballot(lv != 0);
+                const uint64_t tm = __ballot(tr.node >= 0 || lv != 0);
                 const bool leave = (uint32_t)__popcll(tm) <= min_active;
                 if (pm != 0 && (leave || (uint32_t)__popcll(pm) > leaf_min || (tm & ~pm) == 0)) {
-                    if (pend) {
+                    if (lv != 0) {
                         trav_leaves<kCount>(pr, lv, ps.o, ps.d, rk, ps.skip, tr, cnt);
-                        pend = false;
-                        if (tr.node < 0) tracing = false;
+                        lv = 0;
                     }
                 }
                 if (leave) break;
@@ -1420,7 +1421,7 @@ __device__ __forceinline__ void render_body(const KParams &P) {
             ph1 += t - tp;
             tp = t;
         }
-        if (has && !need_ray && !tracing) {
+        if (has && !need_ray && tr.node < 0) {
             need_ray = true;
             const Prims<kBook2> spr{prims, motion, ps.time, P.quads, P.media, P.n_quads, rng_key(ps.rng) ^ ((uint64_t)ps.k << 32)};
 #ifdef RRT_TRACE_X
