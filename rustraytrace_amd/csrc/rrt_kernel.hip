@@ -1283,7 +1283,8 @@ __device__ __forceinline__ void render_body(const KParams &P) {
     const uint32_t lane = threadIdx.x & 63u;
     Counters cnt = {0, 0, 0, 0, 0, 0};
     uint32_t w_rays = 0, w_paths = 0;  // wave-uniform (scalar) ray / path counts
-    bool has = false;     // lane owns a unit
+    // Per-lane flags as 0/1 integers (VGPRs) rather than bools (SGPR lane masks), see tr.node.
+    uint32_t has = 0;     // lane owns a unit
     bool q_open = true;   // wave-uniform: the queue may still hold units
     // lane's unit: global pixel (x | y << 16), next sample s, end of its sample chunk s_hi
     uint32_t xy = 0, s = 0, s_hi = 0;
@@ -1295,7 +1296,7 @@ __device__ __forceinline__ void render_body(const KParams &P) {
     // leaf tests): lane state lives in VGPR integers, so updating it in divergent code is one
     // v_mov instead of the three exec-mask merges a bool held in an SGPR pair costs.
     tr.node = -1;
-    bool need_ray = false;  // the lane must start the next segment of its path
+    uint32_t need_ray = 0;  // the lane must start the next segment of its path
     uint32_t pool_base = 0, pool_left = 0;  // wave-uniform: claimed, not yet assigned units
     [[maybe_unused]] uint64_t ph0 = 0, ph1 = 0, ph2 = 0, tp = 0;
     for (;;) {
@@ -1346,8 +1347,8 @@ __device__ __forceinline__ void render_body(const KParams &P) {
                         pkey = pixel_key(P, x, y);
                         ps.rng = path_rng_k(pkey, s);
                         camera_ray<kBook2 == 4>(P, x, y, s, ps);
-                        need_ray = true;
-                        has = true;
+                        need_ray = 1;
+                        has = 1;
                     }
                 }
             }
@@ -1356,15 +1357,15 @@ __device__ __forceinline__ void render_body(const KParams &P) {
         }
         if (__ballot(has) == 0) break;
 
-        bool seg_done = false;  // the lane's path ended without a query (depth limit)
-        bool started = false;   // the lane starts a closest-hit query this iteration
+        uint32_t seg_done = 0;  // the lane's path ended without a query (depth limit)
+        uint32_t started = 0;   // the lane starts a closest-hit query this iteration
         if (has && need_ray) {
             if (ps.k >= P.max_depth) {  // ray_color: depth <= 0 -> 0 (no query)
-                seg_done = true;
+                seg_done = 1;
             } else {
                 trav_begin(tr);
-                need_ray = false;
-                started = true;
+                need_ray = 0;
+                started = 1;
             }
         }
         w_rays += (uint32_t)__popcll(__ballot(started));
@@ -1422,7 +1423,7 @@ __device__ __forceinline__ void render_body(const KParams &P) {
             tp = t;
         }
         if (has && !need_ray && tr.node < 0) {
-            need_ray = true;
+            need_ray = 1;
             const Prims<kBook2> spr{prims, motion, ps.time, P.quads, P.media, P.n_quads, rng_key(ps.rng) ^ ((uint64_t)ps.k << 32)};
 #ifdef RRT_TRACE_X
             if ((xy & 0xffffu) == RRT_TRACE_X && (xy >> 16) == RRT_TRACE_Y && s == RRT_TRACE_S)
@@ -1430,8 +1431,8 @@ __device__ __forceinline__ void render_body(const KParams &P) {
                        ps.o.z, ps.d.x, ps.d.y, ps.d.z, tr.closest, tr.hit_prim, ps.T.x, ps.T.y, ps.T.z,
                        (unsigned long long)rng_key(ps.rng));
 #endif
-            if constexpr (kBook2 == 4) seg_done = shade_b3(P, spr, mtl, ps, tr.closest, tr.hit_prim, sum, cnt);
-            else seg_done = shade<kBook2>(P, spr, mtl, ps, tr.closest, tr.hit_prim, sum, cnt);
+            if constexpr (kBook2 == 4) seg_done = shade_b3(P, spr, mtl, ps, tr.closest, tr.hit_prim, sum, cnt) ? 1u : 0u;
+            else seg_done = shade<kBook2>(P, spr, mtl, ps, tr.closest, tr.hit_prim, sum, cnt) ? 1u : 0u;
         }
         w_paths += (uint32_t)__popcll(__ballot(seg_done));
         if (seg_done) {  // pixel_color += ray_color(..) (camera.rs:73-76): already in `sum`
@@ -1452,7 +1453,7 @@ __device__ __forceinline__ void render_body(const KParams &P) {
                 const float4 out = make_float4(sum.x, sum.y, sum.z, (float)(s_hi - (P.sample_begin + chunk_first(P, chunk))));
                 if (P.n_chunks == 1) P.accum[px] = out;
                 else P.partial[(size_t)(chunk - P.chunk_begin) * ((size_t)P.tile_rows * P.width) + px] = out;
-                has = false;
+                has = 0;
             }
         }
         if constexpr (RRT_PHASE_TIMING == 1) ph2 += __builtin_amdgcn_s_memtime() - tp;
