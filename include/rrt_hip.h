@@ -29,8 +29,10 @@ extern "C" {
 /* 1: book 1; 2: RrtSceneExt (motion, Perlin), kinds 5-6; 3: quads, constant-density media and
  * book-3 light lists in RrtSceneExt, kind 7, RRT_FLAG_BOOK3, rrt_build_next_week_scene /
  * rrt_build_rest_of_your_life_scene with struct outputs; 4: RrtBvhInfo.node_stride (80-B LDS /
- * 64-B global BVH2 nodes), xoshiro128+ path streams, tail-split accumulation chunks. */
-#define RRT_ABI_VERSION 4u
+ * 64-B global BVH2 nodes), xoshiro128+ path streams, tail-split accumulation chunks;
+ * 5: exit_skip (f32 bounces never re-hit the primitive they leave), rrt_hip_render_rgb8_ex,
+ * rrt_quantize_accum_books, chunk partials bounded by RRT_PARTIAL_MB (sample passes). */
+#define RRT_ABI_VERSION 5u
 
 /* ---- scene ABI (== src/gpu/mod.rs:13-42) ------------------------------------------ */
 
