@@ -1405,10 +1405,13 @@ __device__ __forceinline__ void render_body(const KParams &P) {
                     Leaves l;
                     if (trav_node<kCount>(nodes, stack, rk, tr, l, cnt)) lv = l;
                 }
+                // wave-uniform decisions in scalar registers, without short-circuit branches:
+                // pm = lanes waiting on leaf tests, tm = lanes still in the tree (pm is a subset)
                 const uint64_t pm = __ballot(lv != 0);
-                const uint64_t tm = __ballot(tr.node >= 0 || lv != 0);
+                const uint64_t tm = __ballot(tr.node >= 0) | pm;
                 const bool leave = (uint32_t)__popcll(tm) <= min_active;
-                if (pm != 0 && (leave || (uint32_t)__popcll(pm) > leaf_min || (tm & ~pm) == 0)) {
+                const bool batch = ((uint32_t)__popcll(pm) > leaf_min) | leave | (tm == pm);
+                if ((pm != 0) & batch) {
                     if (lv != 0) {
                         trav_leaves<kCount>(pr, lv, ps.o, ps.d, rk, ps.skip, tr, cnt);
                         lv = 0;
