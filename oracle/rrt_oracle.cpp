@@ -79,9 +79,29 @@ template <class T> Vec3<T> operator*(Vec3<T> a, T s) { return mk(a.e[0] * s, a.e
 template <class T> Vec3<T> operator*(T s, Vec3<T> a) { return a * s; }
 // vec3.rs:142-148: Div<f64> is (1.0 / rhs) * self
 template <class T> Vec3<T> operator/(Vec3<T> a, T s) { return (T(1) / s) * a; }
-template <class T> T length_squared(Vec3<T> v) { return v.e[0] * v.e[0] + v.e[1] * v.e[1] + v.e[2] * v.e[2]; }
+// f32 modes (TWIN, KBVH) evaluate dot products and sums of squares the way the kernel does:
+// u0*v0, then two fused multiply-adds (one rounding per term instead of two; rrt_kernel.hip dot).
+// BOOKS (f64) keeps the reference's unfused (u0*v0 + u1*v1) + u2*v2 (vec3.rs:156-158, Rust
+// never contracts).
+template <class T> T dot3(T a0, T b0, T a1, T b1, T a2, T b2) {
+    if constexpr (std::is_same_v<T, float>) return std::fma(a2, b2, std::fma(a1, b1, a0 * b0));
+    else return a0 * b0 + a1 * b1 + a2 * b2;
+}
+template <class T> T length_squared(Vec3<T> v) { return dot3(v.e[0], v.e[0], v.e[1], v.e[1], v.e[2], v.e[2]); }
 template <class T> T length(Vec3<T> v) { return std::sqrt(length_squared(v)); }
-template <class T> T dot(Vec3<T> u, Vec3<T> v) { return u.e[0] * v.e[0] + u.e[1] * v.e[1] + u.e[2] * v.e[2]; }
+template <class T> T dot(Vec3<T> u, Vec3<T> v) { return dot3(u.e[0], v.e[0], u.e[1], v.e[1], u.e[2], v.e[2]); }
+// Sphere::hit's discriminant h*h - a*c (sphere.rs:30); f32 modes fuse it like the kernel:
+// fma(h, h, -(a*c)).
+template <class T> T sphere_disc(T h, T a, T c) {
+    if constexpr (std::is_same_v<T, float>) return std::fma(h, h, -(a * c));
+    else return h * h - a * c;
+}
+// Ray::at (ray.rs: orig + t*dir) for the hit record; f32 modes fuse it like the kernel's shading.
+template <class T> Vec3<T> ray_at(Vec3<T> o, Vec3<T> d, T t) {
+    if constexpr (std::is_same_v<T, float>)
+        return mk(std::fma(t, d.e[0], o.e[0]), std::fma(t, d.e[1], o.e[1]), std::fma(t, d.e[2], o.e[2]));
+    else return o + t * d;
+}
 template <class T> Vec3<T> unit_vector(Vec3<T> v) { return v / length(v); }
 template <class T> bool near_zero(Vec3<T> v) {  // vec3.rs:38-41
     const T s = L(1e-8);
@@ -570,7 +590,7 @@ template <class T> struct World {
         const T a = length_squared(d);
         const T h = dot(d, oc);
         const T c = length_squared(oc) - radius * radius;
-        const T disc = h * h - a * c;
+        const T disc = sphere_disc(h, a, c);
         if (disc < T(0)) return false;
         const T sqrtd = std::sqrt(disc);
         T root = (h - sqrtd) / a;
@@ -590,7 +610,7 @@ template <class T> struct World {
         const T a = length_squared(d);
         const T h = dot(d, oc);
         const T c = length_squared(oc) - s.radius * s.radius;
-        const T disc = h * h - a * c;
+        const T disc = sphere_disc(h, a, c);
         if (disc < T(0)) return false;
         const T sqrtd = std::sqrt(disc);
         T root = (h - sqrtd) / a;
@@ -917,7 +937,7 @@ bool world_hit(const World<T> &w, Vec3<T> o, Vec3<T> d, T time, uint64_t seg, Re
         if (!w.hit(w.root, o, d, time, Interval<T>{L(0.001), std::numeric_limits<T>::infinity()}, h, tests, seg))
             return false;
     }
-    rec.p = o + h.t * d;  // Ray::at
+    rec.p = ray_at(o, d, h.t);  // Ray::at
     rec.prim = h.sphere;
     if ((size_t)h.sphere >= w.spheres.size() + w.quads.size()) {  // medium (constant_medium.rs:76-82)
         rec.outward = rec.normal = mk(T(1), T(0), T(0));
@@ -1652,7 +1672,7 @@ int oracle_sphere_hit(int f32, const double *center, double radius, const double
         const Vec3<T> O = mk((T)o[0], (T)o[1], (T)o[2]), D = mk((T)d[0], (T)d[1], (T)d[2]);
         T t;
         if (!w.hit_sphere(0, O, D, T(0), Interval<T>{(T)tmin, (T)tmax}, t, nullptr)) return 0;
-        const Vec3<T> p = O + t * D;
+        const Vec3<T> p = ray_at(O, D, t);
         const Vec3<T> out = (p - c) / r;
         const bool front = dot(D, out) < T(0);
         const Vec3<T> n = front ? out : -out;

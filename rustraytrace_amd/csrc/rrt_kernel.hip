@@ -16,9 +16,10 @@
 //   Russian roulette camera.rs:189-200 (this bounce's attenuation, clamp [.05,.95])
 //   sky / background camera.rs:206-208 / the_next_week/camera.rs:179-181
 //   emission, texture the_next_week/material.rs:41-53,131-135, texture.rs:177-196, sphere.rs:46-52
-// in f32 with every operation in the reference's order and no contraction (built with
-// -ffp-contract=off and correctly rounded f32 div/sqrt) so the CPU oracle (oracle/) can
-// reproduce each sample bit for bit. Throughput is carried front-to-back
+// in f32 with every operation in the reference's order (built with -ffp-contract=off and
+// correctly rounded f32 div/sqrt; the only fused multiply-adds are explicit: dot products and
+// sums of squares, the sphere discriminant h*h - a*c, Ray::at of the hit point, the slab test)
+// so the CPU oracle (oracle/) can reproduce each sample bit for bit. Throughput is carried front-to-back
 // (T <- T*att[*1/p]); the reference multiplies back-to-front through its recursion —
 // equal in exact arithmetic (documented in DESIGN.md).
 #include "rrt_internal.h"
@@ -63,8 +64,10 @@ __device__ __forceinline__ V3 add(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, 
 __device__ __forceinline__ V3 sub(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
 __device__ __forceinline__ V3 mul(V3 a, V3 b) { return v3(a.x * b.x, a.y * b.y, a.z * b.z); }
 __device__ __forceinline__ V3 muls(V3 a, float s) { return v3(a.x * s, a.y * s, a.z * s); }
-// vec3.rs:156-158 dot = (u0*v0 + u1*v1) + u2*v2
-__device__ __forceinline__ float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+// vec3.rs:156-158 dot = (u0*v0 + u1*v1) + u2*v2, here with the two adds fused into the products
+// (u0*v0, then fma, fma: one rounding per term instead of two, 3 VALU ops instead of 5 under
+// -ffp-contract=off; the oracle's f32 modes use the same form, oracle/rrt_oracle.cpp dot3).
+__device__ __forceinline__ float dot(V3 a, V3 b) { return __builtin_fmaf(a.z, b.z, __builtin_fmaf(a.y, b.y, a.x * b.x)); }
 __device__ __forceinline__ V3 cross(V3 a, V3 b) {  // vec3.rs cross
     return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }
@@ -131,7 +134,7 @@ __device__ __forceinline__ V3 random_unit_vector(RngState &s, C &cnt) {
         px = rnd_pm1(s);
         py = rnd_pm1(s);
         pz = rnd_pm1(s);
-        lensq = px * px + py * py + pz * pz;
+        lensq = __builtin_fmaf(pz, pz, __builtin_fmaf(py, py, px * px));
         if (0.0f < lensq && lensq <= 1.0f) break;
     }
     const float inv = 1.0f / __builtin_sqrtf(lensq);
@@ -382,7 +385,7 @@ __device__ __forceinline__ bool medium_hit(const PR &pr, int m, V3 o, V3 d, cons
         const V3 oc = v3(g.sphere.x - o.x, g.sphere.y - o.y, g.sphere.z - o.z);
         const float h = dot(d, oc);
         const float c = dot(oc, oc) - g.sphere.w * g.sphere.w;
-        const float disc = h * h - rk.a * c;
+        const float disc = __builtin_fmaf(h, h, -(rk.a * c));
         if (disc < 0.0f) return false;
         const float sq = __builtin_sqrtf(disc);
         const float r0 = div_by_a(h - sq, rk), r1 = div_by_a(h + sq, rk);
@@ -436,7 +439,7 @@ __device__ __forceinline__ void test_prims(const PR &prim_cr, int first, int cou
         const V3 oc = v3(cr.x - o.x, cr.y - o.y, cr.z - o.z);
         const float h = dot(d, oc);
         const float c = dot(oc, oc) - (PR::kR2 ? cr.w : cr.w * cr.w);
-        const float disc = h * h - a * c;
+        const float disc = __builtin_fmaf(h, h, -(a * c));
         if (disc < 0.0f) continue;
         const float sq = __builtin_sqrtf(disc);
         float root = (h - sq) / a;
@@ -491,7 +494,7 @@ __device__ __forceinline__ void test_range(const PR &prim_cr, int first, int cou
         const V3 oc = v3(cr.x - o.x, cr.y - o.y, cr.z - o.z);
         const float h = dot(d, oc);
         const float c = dot(oc, oc) - (PR::kR2 ? cr.w : cr.w * cr.w);
-        const float disc = h * h - a * c;
+        const float disc = __builtin_fmaf(h, h, -(a * c));
 #if RRT_LEAN
         // The far root (h + sq) / a is needed only when the near one is at or behind tmin (the
         // ray starts inside the sphere): r1 >= r0 always (sq >= 0, a > 0, correctly rounded
@@ -752,7 +755,7 @@ __device__ __forceinline__ void camera_ray(const KParams &P, uint32_t x, uint32_
         for (;;) {  // vec3.rs:172-179 random_in_unit_disk
             px = rnd_pm1(ps.rng);
             py = rnd_pm1(ps.rng);
-            if (px * px + py * py < 1.0f) break;
+            if (__builtin_fmaf(py, py, px * px) < 1.0f) break;
         }
         origin = v3(P.center[0] + P.disk_u[0] * px + P.disk_v[0] * py,
                     P.center[1] + P.disk_u[1] * px + P.disk_v[1] * py,
@@ -867,7 +870,7 @@ __device__ __forceinline__ float perlin_noise(const GPerlin *__restrict__ pt, V3
                 const float fi = di ? uu : 1.0f - uu;
                 const float fj = dj ? vv : 1.0f - vv;
                 const float fk = dk ? ww : 1.0f - ww;
-                accum = accum + fi * fj * fk * (c.x * wx + c.y * wy + c.z * wz);
+                accum = accum + fi * fj * fk * dot(v3(c.x, c.y, c.z), v3(wx, wy, wz));
             }
     return accum;
 }
@@ -934,7 +937,7 @@ __device__ __forceinline__ bool shade(const KParams &P, const PR &prims, const G
     }
     // HitRecord (sphere.rs:47-50, hittable.rs:20-32)
     const float4 cr = prims.at(prim);  // the sphere's center at the ray's time (sphere.rs:48)
-    const V3 p = v3(ps.o.x + ps.d.x * t, ps.o.y + ps.d.y * t, ps.o.z + ps.d.z * t);
+    const V3 p = v3(__builtin_fmaf(ps.d.x, t, ps.o.x), __builtin_fmaf(ps.d.y, t, ps.o.y), __builtin_fmaf(ps.d.z, t, ps.o.z));  // Ray::at, fused
     V3 outward;
     bool is_quad = false, is_medium = false;
     if (PR::kHasQuads && cr.w < 0.0f) {  // a quad's plane normal (quad.rs:79); a medium's (1, 0, 0)
@@ -1036,7 +1039,7 @@ __device__ __forceinline__ bool sphere_root(float4 c, V3 o, V3 d, float tmin) {
     const float a = dot(d, d);
     const float h = dot(d, oc);
     const float cc = dot(oc, oc) - c.w * c.w;
-    const float disc = h * h - a * cc;
+    const float disc = __builtin_fmaf(h, h, -(a * cc));
     if (disc < 0.0f) return false;
     const float sq = __builtin_sqrtf(disc);
     const float inf = __builtin_inff();
@@ -1108,7 +1111,7 @@ __device__ __forceinline__ bool shade_b3(const KParams &P, const PR &prims, cons
         return true;
     }
     const float4 cr = prims.at(prim);
-    const V3 p = v3(ps.o.x + ps.d.x * t, ps.o.y + ps.d.y * t, ps.o.z + ps.d.z * t);
+    const V3 p = v3(__builtin_fmaf(ps.d.x, t, ps.o.x), __builtin_fmaf(ps.d.y, t, ps.o.y), __builtin_fmaf(ps.d.z, t, ps.o.z));  // Ray::at, fused
     V3 outward;
     bool is_quad = false, is_medium = false;
     if (cr.w < 0.0f) {

@@ -15,6 +15,8 @@ Each case writes <name>.npz with:
 
 Round 2 regenerated every fixture: the f32 modes (and the kernel) gained exit_skip (the
 primitive a scattered ray leaves is not tested for a hit again; oracle/rrt_oracle.cpp).
+Regenerated again when the f32 modes and the kernel took fused multiply-adds for dot products,
+the sphere discriminant and Ray::at (oracle/rrt_oracle.cpp dot3 / sphere_disc / ray_at).
 
     python tests/golden/make_golden.py
 """
