@@ -31,8 +31,9 @@ extern "C" {
  * rrt_build_rest_of_your_life_scene with struct outputs; 4: RrtBvhInfo.node_stride (80-B LDS /
  * 64-B global BVH2 nodes), xoshiro128+ path streams, tail-split accumulation chunks;
  * 5: exit_skip (f32 bounces never re-hit the primitive they leave), rrt_hip_render_rgb8_ex,
- * rrt_quantize_accum_books, chunk partials bounded by RRT_PARTIAL_MB (sample passes). */
-#define RRT_ABI_VERSION 5u
+ * rrt_quantize_accum_books, chunk partials bounded by RRT_PARTIAL_MB (sample passes);
+ * 6: RrtBvhInfo.n_unbounded (scene-enclosing media tested after the BVH walk; was _pad). */
+#define RRT_ABI_VERSION 6u
 
 /* ---- scene ABI (== src/gpu/mod.rs:13-42) ------------------------------------------ */
 
@@ -317,7 +318,8 @@ typedef struct RrtBvhInfo {
     uint32_t max_leaf_param; /* leaf size the builder was asked for */
     uint32_t node_stride;    /* bytes per node: 80 (BVH2 staged in LDS: sign-ordered planes), 64 (BVH2 read
                                 from global memory), 128 (BVH4); layouts in DESIGN.md */
-    uint32_t _pad;
+    uint32_t n_unbounded;    /* the last n_unbounded primitives of the leaf order are not in the tree: media
+                                whose boundary sphere holds the whole scene, tested after the walk (ABI v6) */
 } RrtBvhInfo;
 int32_t rrt_scene_bvh_info(const RrtScene *scene, RrtBvhInfo *out);
 

@@ -49,7 +49,7 @@ mod imp {
     /// Suppress the library's own stderr progress lines (RRT_FLAG_QUIET).
     pub const RRT_FLAG_QUIET: u32 = 0x2;
     /// ABI this shim was written against (RRT_ABI_VERSION).
-    pub const RRT_ABI_VERSION: u32 = 5;
+    pub const RRT_ABI_VERSION: u32 = 6;
 
     #[link(name = "rrt_hip")]
     extern "C" {

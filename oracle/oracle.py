@@ -42,7 +42,7 @@ def load() -> ctypes.CDLL:
                                   c_uint32, c_uint32, c_int, P, P, P, c_uint32]
     lib.oracle_render_kbvh.restype = c_int
     lib.oracle_render_kbvh.argtypes = [P, P, c_uint32, P, c_uint32, P, c_uint32, P, c_uint32, P, c_uint32, c_uint32, P,
-                                       c_uint32, c_uint32, c_uint32, c_uint32, c_int, P, P, P, c_uint32]
+                                       c_uint32, c_uint32, c_uint32, c_uint32, c_uint32, c_int, P, P, P, c_uint32]
     lib.oracle_sin_f32.restype = None
     lib.oracle_sin_f32.argtypes = [c_uint32, P, P]
     lib.oracle_cos_f32.restype = None
@@ -172,9 +172,11 @@ def render(scene, mode=TWIN, rows=None, samples=None, threads=1, chunk=DEFAULT_C
 
 def render_kbvh(scene, nodes, order, layout, rows=None, samples=None, threads=1, chunk=DEFAULT_CHUNK):
     """TWIN arithmetic, closest hits by walking the kernel's own BVH in the kernel's order
-    (nodes/order/info from rustraytrace_amd.render.build_bvh; `layout` = that info dict, or the
-    node stride in bytes: 80 / 64 BVH2, 128 BVH4). Same return as render()."""
+    (nodes/order/info from rustraytrace_amd.render.build_bvh; `layout` = that info dict — its
+    node_stride and n_unbounded, the media tested after the walk — or the node stride in bytes:
+    80 / 64 BVH2, 128 BVH4, for trees without unbounded media). Same return as render()."""
     stride = int(layout["node_stride"]) if isinstance(layout, dict) else int(layout)
+    n_unbounded = int(layout.get("n_unbounded", 0)) if isinstance(layout, dict) else 0
     if stride not in (64, 80, 128):
         raise ValueError(f"render_kbvh: node stride {stride} (pass build_bvh's info dict)")
     lib = load()
@@ -195,7 +197,7 @@ def render_kbvh(scene, nodes, order, layout, rows=None, samples=None, threads=1,
     ext, keep_ext = _ext(scene)
     rc = lib.oracle_render_kbvh(_p(scene.camera), _p(scene.spheres), len(scene.spheres), _p(scene.materials),
                                 len(scene.materials), ctypes.cast(tex, c_void_p) if keep else None, len(keep), ext,
-                                int(scene.flags), _p(nodes), n_nodes, stride, _p(order), y0, y1, s0, s1,
+                                int(scene.flags), _p(nodes), n_nodes, stride, _p(order), n_unbounded, y0, y1, s0, s1,
                                 int(threads), _p(accum), ctypes.byref(rays), ctypes.byref(tests), int(chunk))
     del keep_ext
     if rc != 0:

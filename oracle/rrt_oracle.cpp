@@ -417,6 +417,9 @@ template <class T> struct World {
     bool book2 = false;  // moving spheres or checker / noise materials (kernel: kBook2)
     std::vector<BvhNode<T>> nodes;
     ChildRef root{false, -1};
+    // f32 modes: the unbounded media's primitive ids, tested after the tree walk (not in the tree;
+    // unbounded_media). BOOKS keeps every primitive in its tree (bvh.rs).
+    std::vector<int32_t> unbounded;
 
     ChildRef build(std::vector<int32_t> &objs, size_t lo, size_t hi) {  // bvh.rs:21-156
         const size_t span = hi - lo;
@@ -654,6 +657,10 @@ struct KTree {
     const uint8_t *nodes = nullptr;
     uint32_t n_nodes = 0;
     const uint32_t *order = nullptr;  // leaf-order primitive -> original sphere index
+    // the unbounded media (RrtBvhInfo.n_unbounded): the last entries of the leaf order, not in the
+    // tree, tested after the walk
+    const uint32_t *unbounded = nullptr;
+    uint32_t n_unbounded = 0;
 };
 
 // 1/d clamped to +-2^64: a zero direction component gives a huge finite slope instead of inf,
@@ -794,9 +801,66 @@ template <class T> struct Cam {
     bool no_exit_skip = false;  // diagnostic mode bit 0x200: f32 modes without exit_skip
 };
 
+// The kernel's unbounded media (rrt_host.cpp unbounded_media, restated): in medium order, at most
+// 4, each sphere-bounded medium whose box [c - r, c + r] holds every other primitive's extent
+// (sphere boxes and the ends of their motion, quad corners q, q + u, q + v, (q + u) + v, the other
+// media's boundaries), in f64 from the f32 inputs. A scheduling choice of the kernel (such a
+// medium is tested after the BVH walk, its hit unchanged); the f32 modes follow it so that the
+// GPU's closest hits stay reproducible bit for bit.
+std::vector<uint32_t> unbounded_media(const RrtSphere *s, uint32_t n, const RrtSceneExt *ext) {
+    std::vector<uint32_t> out;
+    const uint32_t nmd = ext && ext->media ? ext->n_media : 0u;
+    const uint32_t nq = ext && ext->quads ? ext->n_quads : 0u;
+    const float *motion = ext ? ext->sphere_motion : nullptr;
+    for (uint32_t m = 0; m < nmd && out.size() < 4; ++m) {
+        const RrtMedium &md = ext->media[m];
+        if (md.boundary_kind != RRT_BOUNDARY_SPHERE) continue;
+        const double r = std::max((double)md.sphere[3], 0.0);
+        double lo[3], hi[3];
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = (double)md.sphere[a] - r;
+            hi[a] = (double)md.sphere[a] + r;
+        }
+        bool inside = true;
+        auto point = [&](double x, double y, double z, double ext_r) {
+            const double v[3] = {x, y, z};
+            for (int a = 0; a < 3; ++a)
+                if (!(lo[a] <= v[a] - ext_r && v[a] + ext_r <= hi[a])) inside = false;
+        };
+        auto corners = [&](const RrtQuad &q) {
+            point(q.q[0], q.q[1], q.q[2], 0.0);
+            point((double)q.q[0] + q.u[0], (double)q.q[1] + q.u[1], (double)q.q[2] + q.u[2], 0.0);
+            point((double)q.q[0] + q.v[0], (double)q.q[1] + q.v[1], (double)q.q[2] + q.v[2], 0.0);
+            point(((double)q.q[0] + q.u[0]) + q.v[0], ((double)q.q[1] + q.u[1]) + q.v[1],
+                  ((double)q.q[2] + q.u[2]) + q.v[2], 0.0);
+        };
+        for (uint32_t i = 0; i < n; ++i) {
+            const float *c = s[i].center_radius;
+            const double ri = std::max((double)c[3], 0.0);
+            point(c[0], c[1], c[2], ri);
+            if (motion) {
+                const float *mv = motion + 4 * (size_t)i;
+                point((double)(c[0] + mv[0]), (double)(c[1] + mv[1]), (double)(c[2] + mv[2]), ri);
+            }
+        }
+        for (uint32_t j = 0; j < nq; ++j) corners(ext->quads[j]);
+        for (uint32_t k = 0; k < nmd; ++k) {
+            if (k == m) continue;
+            const RrtMedium &o = ext->media[k];
+            if (o.boundary_kind == RRT_BOUNDARY_SPHERE)
+                point(o.sphere[0], o.sphere[1], o.sphere[2], std::max((double)o.sphere[3], 0.0));
+            else
+                for (uint32_t q = 0; q < o.count; ++q) corners(ext->boundary_quads[o.first + q]);
+        }
+        if (inside) out.push_back(m);
+    }
+    return out;
+}
+
 template <class T>
 void load_world(World<T> &w, Cam<T> &cam, const RrtCamera *c, const RrtSphere *s, uint32_t n, const RrtMaterial *m,
-                uint32_t nm, const RrtTexture *tex, uint32_t ntex, uint32_t flags, const RrtSceneExt *ext) {
+                uint32_t nm, const RrtTexture *tex, uint32_t ntex, uint32_t flags, const RrtSceneExt *ext,
+                bool all_in_tree = false) {
     auto v3 = [](const float *f) { return mk<T>((T)f[0], (T)f[1], (T)f[2]); };
     cam.center = v3(c->origin);
     cam.p00 = v3(c->pixel00);
@@ -905,11 +969,16 @@ void load_world(World<T> &w, Cam<T> &cam, const RrtCamera *c, const RrtSphere *s
         w.lights.push_back(lt);
     }
     const uint32_t np = n + nq + nmd;
-    if (np) {
-        std::vector<int32_t> objs(np);
-        for (uint32_t i = 0; i < np; ++i) objs[i] = (int32_t)i;
-        w.root = w.build(objs, 0, np);
-    }
+    std::vector<int32_t> objs;
+    std::vector<bool> out_of_tree(np, false);
+    if constexpr (std::is_same_v<T, float>)
+        for (uint32_t m : all_in_tree ? std::vector<uint32_t>{} : unbounded_media(s, n, ext)) {
+            out_of_tree[n + nq + m] = true;
+            w.unbounded.push_back((int32_t)(n + nq + m));
+        }
+    for (uint32_t i = 0; i < np; ++i)
+        if (!out_of_tree[i]) objs.push_back((int32_t)i);
+    if (!objs.empty()) w.root = w.build(objs, 0, objs.size());
 }
 
 template <class T> struct Record {
@@ -924,14 +993,25 @@ bool world_hit(const World<T> &w, Vec3<T> o, Vec3<T> d, T time, uint64_t seg, Re
                const KTree *kt = nullptr, int32_t skip = -1) {  // camera.rs:187
     Hit<T> h;
     if constexpr (std::is_same_v<T, float>) {
+        bool any;
         if (kt) {
-            if (!kbvh_hit(w, *kt, o, d, time, h, tests, seg, skip)) return false;
+            any = kbvh_hit(w, *kt, o, d, time, h, tests, seg, skip);
         } else {
-            if (w.root.index < 0) return false;
-            if (!w.hit(w.root, o, d, time, Interval<T>{L(0.001), std::numeric_limits<T>::infinity()}, h, tests, seg,
-                       skip))
-                return false;
+            any = w.root.index >= 0 &&
+                  w.hit(w.root, o, d, time, Interval<T>{L(0.001), std::numeric_limits<T>::infinity()}, h, tests, seg, skip);
         }
+        // the unbounded media, after the walk, against its closest hit (the kernel's order)
+        const uint32_t nu = kt ? kt->n_unbounded : (uint32_t)w.unbounded.size();
+        for (uint32_t g = 0; g < nu; ++g) {
+            const int32_t p = kt ? (int32_t)kt->unbounded[g] : w.unbounded[g];
+            T t;
+            if (w.hit_prim(p, o, d, time, Interval<T>{L(0.001), any ? h.t : std::numeric_limits<T>::infinity()}, t,
+                           tests, seg, skip)) {
+                h = Hit<T>{t, p};
+                any = true;
+            }
+        }
+        if (!any) return false;
     } else {
         if (w.root.index < 0) return false;
         if (!w.hit(w.root, o, d, time, Interval<T>{L(0.001), std::numeric_limits<T>::infinity()}, h, tests, seg))
@@ -1443,7 +1523,9 @@ int render(const RrtCamera *c, const RrtSphere *s, uint32_t n, const RrtMaterial
            const KTree *kt = nullptr) {
     World<T> w;
     Cam<T> cam;
-    load_world(w, cam, c, s, n, m, nm, tex, ntex, flags, ext);
+    // diagnostic mode bit 0x400: the f32 TWIN tree keeps the unbounded media (tests: the scheduling
+    // choice of testing them after the walk does not change the image)
+    load_world(w, cam, c, s, n, m, nm, tex, ntex, flags, ext, (mode & 0x400) != 0);
     cam.no_exit_skip = (mode & 0x200) != 0;
     if (y1 > cam.height) y1 = cam.height;
     if (y0 > y1) return -1;
@@ -1560,16 +1642,21 @@ int oracle_render(const RrtCamera *cam, const RrtSphere *s, uint32_t n, const Rr
 int oracle_render_kbvh(const RrtCamera *cam, const RrtSphere *s, uint32_t n, const RrtMaterial *m, uint32_t nm,
                        const RrtTexture *tex, uint32_t ntex, const RrtSceneExt *ext, uint32_t flags, const void *nodes,
                        uint32_t n_nodes,
-                       uint32_t width, const uint32_t *order, uint32_t y0, uint32_t y1, uint32_t s0, uint32_t s1,
-                       int threads, double *accum, uint64_t *rays, uint64_t *sphere_tests, uint32_t chunk) {
+                       uint32_t width, const uint32_t *order, uint32_t n_unbounded, uint32_t y0, uint32_t y1,
+                       uint32_t s0, uint32_t s1, int threads, double *accum, uint64_t *rays, uint64_t *sphere_tests,
+                       uint32_t chunk) {
     // `width` is the node stride in bytes: 80 / 64 (BVH2 layouts), 128 (BVH4)
     if (!cam || !accum || !nodes || (width != 64 && width != 80 && width != 128)) return -1;
+    const uint32_t np = n + (ext && ext->quads ? ext->n_quads : 0u) + (ext && ext->media ? ext->n_media : 0u);
+    if (n_unbounded > np) return -1;
     KTree kt;
     kt.width = width == 128 ? 4 : 2;
     kt.stride = width;
     kt.nodes = static_cast<const uint8_t *>(nodes);
     kt.n_nodes = n_nodes;
     kt.order = order;
+    kt.unbounded = order + (np - n_unbounded);
+    kt.n_unbounded = n_unbounded;
     return render<float>(cam, s, n, m, nm, tex, ntex, ext, flags, 0, y0, y1, s0, s1, threads, accum, rays, sphere_tests,
                          chunk, &kt);
 }

@@ -170,7 +170,7 @@ class RrtBvhInfo(ctypes.Structure):
         ("width", c_uint32),
         ("max_leaf_param", c_uint32),
         ("node_stride", c_uint32),
-        ("_pad", c_uint32),
+        ("n_unbounded", c_uint32),
     ]
 
     def as_dict(self):

@@ -345,6 +345,11 @@ struct FlatBvh {
     // BVH2: every node whose children are both leaves has them adjacent in primitive order
     // (right.first == left.first + left.count), so the kernel tests the hit ones as one range
     bool sibling_leaves_adjacent = true;
+    // Unbounded media: sphere-bounded media whose box holds every other primitive's (a fog around
+    // the whole scene, the_next_week/mod.rs:563-566). Every ray's box test would pass them, so they
+    // are not in the tree: they follow its primitives in leaf order (the last n_unbounded entries)
+    // and each closest-hit query tests them after the walk, every lane of the wave together.
+    uint32_t n_unbounded = 0;
 };
 
 // Conservative slab test in f32. The kernel's plane distance fma(P, inv, -o*inv) differs from
@@ -604,6 +609,53 @@ bool scene_lds_fit(size_t node_bytes, size_t n_prims, bool book2) {
     return node_bytes + n_prims * (rrt::kPrimBytes + (book2 ? rrt::kMotionBytes : 0)) <= rrt::kLdsSceneBudget;
 }
 
+// The unbounded media (FlatBvh::n_unbounded), in medium order, at most kMaxUnbounded: a
+// sphere-bounded medium whose box [c - r, c + r] holds every other primitive's extent — sphere
+// boxes (both ends of a motion), quad corners q, q + u, q + v, (q + u) + v, the other media's
+// boundaries — in f64 from the f32 inputs. Only a scheduling choice: a medium's hit does not
+// depend on when the query tests it (its free flight is clipped to the closest hit so far, and
+// the per-(path, segment, medium) draw is fixed), so testing it after the walk returns the same
+// closest hit. The oracle's f32 modes restate the rule (oracle/rrt_oracle.cpp unbounded_media).
+std::vector<uint32_t> unbounded_media(const RrtSphere *spheres, uint32_t n_spheres, const ExtView &ex) {
+    std::vector<uint32_t> out;
+    for (uint32_t m = 0; m < ex.n_media && out.size() < rrt::kMaxUnbounded; ++m) {
+        const RrtMedium &md = ex.media[m];
+        if (md.boundary_kind != RRT_BOUNDARY_SPHERE) continue;
+        const double r = std::max((double)md.sphere[3], 0.0);
+        double lo[3], hi[3];
+        for (int a = 0; a < 3; ++a) lo[a] = (double)md.sphere[a] - r, hi[a] = (double)md.sphere[a] + r;
+        bool ok = true;
+        auto pt = [&](double x, double y, double z, double e) {
+            const double v[3] = {x, y, z};
+            for (int a = 0; a < 3; ++a) ok = ok && lo[a] <= v[a] - e && v[a] + e <= hi[a];
+        };
+        auto quad = [&](const RrtQuad &q) {
+            pt(q.q[0], q.q[1], q.q[2], 0.0);
+            pt((double)q.q[0] + q.u[0], (double)q.q[1] + q.u[1], (double)q.q[2] + q.u[2], 0.0);
+            pt((double)q.q[0] + q.v[0], (double)q.q[1] + q.v[1], (double)q.q[2] + q.v[2], 0.0);
+            pt(((double)q.q[0] + q.u[0]) + q.v[0], ((double)q.q[1] + q.u[1]) + q.v[1], ((double)q.q[2] + q.u[2]) + q.v[2], 0.0);
+        };
+        for (uint32_t i = 0; i < n_spheres && ok; ++i) {
+            const float *c = spheres[i].center_radius;
+            const double ri = std::max((double)c[3], 0.0);
+            pt(c[0], c[1], c[2], ri);
+            if (ex.motion) {
+                const float *mv = ex.motion + 4 * (size_t)i;
+                pt((double)(c[0] + mv[0]), (double)(c[1] + mv[1]), (double)(c[2] + mv[2]), ri);
+            }
+        }
+        for (uint32_t j = 0; j < ex.n_quads && ok; ++j) quad(ex.quads[j]);
+        for (uint32_t k = 0; k < ex.n_media && ok; ++k) {
+            if (k == m) continue;
+            const RrtMedium &o = ex.media[k];
+            if (o.boundary_kind == RRT_BOUNDARY_SPHERE) pt(o.sphere[0], o.sphere[1], o.sphere[2], std::max((double)o.sphere[3], 0.0));
+            else for (uint32_t q = 0; q < o.count && ok; ++q) quad(ex.bquads[o.first + q]);
+        }
+        if (ok) out.push_back(m);
+    }
+    return out;
+}
+
 // BVH2 node layout: the sign-ordered 80-B nodes when `lds_fit(bytes of those nodes)` says the
 // scene will be staged in LDS, else the 64-B global-memory nodes.
 FlatBvh build_bvh(const RrtSphere *spheres, uint32_t n_spheres, const ExtView &ex, uint32_t width,
@@ -638,17 +690,21 @@ FlatBvh build_bvh(const RrtSphere *spheres, uint32_t n_spheres, const ExtView &e
         boxes[n_spheres + n_quads + m] = b;
     }
     const uint32_t n_prims = n_spheres + n_quads + ex.n_media;
+    const std::vector<uint32_t> unb = unbounded_media(spheres, n_spheres, ex);
     Builder bld(boxes, max_leaf);
+    for (uint32_t m : unb) bld.objs.erase(std::find(bld.objs.begin(), bld.objs.end(), n_spheres + n_quads + m));
+    const uint32_t n_tree = (uint32_t)bld.objs.size();
     if (const char *e = std::getenv("RRT_BVH_SPLIT")) bld.sweep = std::strcmp(e, "binned") != 0;
     if (const char *e = std::getenv("RRT_SAH_CT")) bld.node_cost = std::atof(e);
     FlatBvh fb;
-    if (n_prims == 0) {  // root with never-hit children
+    if (n_tree == 0) {  // root with never-hit children
         Builder::BNode empty;
         empty.box = never_hit_box();
         empty.leaf = true;
         bld.bin.push_back(empty);
     }
-    const int32_t root = n_prims == 0 ? 0 : bld.build(0, n_prims);
+    (void)n_prims;
+    const int32_t root = n_tree == 0 ? 0 : bld.build(0, n_tree);
     if (width == 4) {
         fb = flatten4(bld, root);
     } else {
@@ -656,6 +712,8 @@ FlatBvh build_bvh(const RrtSphere *spheres, uint32_t n_spheres, const ExtView &e
         if (!lds_fit(fb.bytes.size())) fb = flatten2<rrt::GNodeG>(bld, root);
     }
     order = bld.objs;
+    for (uint32_t m : unb) order.push_back(n_spheres + n_quads + m);
+    fb.n_unbounded = (uint32_t)unb.size();
     return fb;
 }
 
@@ -1095,6 +1153,7 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
     p.height = (uint32_t)hf;
     p.n_nodes = fb.n_nodes;
     p.n_prims = n_prims;
+    p.n_unbounded = fb.n_unbounded;
     p.stack_depth = fb.stack_need;
     p.bvh_width = fb.width;
     // BVH2: the node layout already encodes the choice (80-B sign-ordered nodes are the LDS ones)
@@ -1124,6 +1183,7 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
     bi.node_stride = fb.stride;
     bi.width = fb.width;
     bi.max_leaf_param = max_leaf;
+    bi.n_unbounded = fb.n_unbounded;
     bi.prim_bytes = (uint64_t)n_prims * (rrt::kPrimBytes + (book2 ? rrt::kMotionBytes : 0)) +
                     (uint64_t)gquads.size() * sizeof(rrt::GQuad) + (uint64_t)n_media * sizeof(rrt::GMedium);
     *out = s;
@@ -1187,6 +1247,7 @@ int32_t rrt_build_bvh_ex(const RrtSphere *spheres, uint32_t n_spheres, const Rrt
                            (uint64_t)ex.n_media * sizeof(rrt::GMedium);
         info->width = fb.width;
         info->max_leaf_param = max_leaf;
+        info->n_unbounded = fb.n_unbounded;
     }
     if (nodes_cap == 0) return RRT_OK;
     if (!nodes_out || nodes_cap < fb.bytes.size() || (order.size() && !prim_order_out))

@@ -35,6 +35,7 @@ static_assert(sizeof(GNodeG) == 64, "GNodeG must be 64 B");
 constexpr uint32_t kLinkCountShift = 28;
 constexpr uint32_t kLinkFirstMask = (1u << kLinkCountShift) - 1u;
 constexpr uint32_t kMaxLeafPrims = 7;  // two leaf children's counts share one 4-bit field
+constexpr uint32_t kMaxUnbounded = 4;  // media tested outside the BVH (rrt_host.cpp unbounded_media)
 
 // BVH4 node, 128 B: the boxes of 4 children as SoA float4s (child c in component c), the
 // child refs and primitive counts (0 = internal node). Collapsed from the binary SAH tree.
@@ -159,6 +160,7 @@ struct KParams {
 
     uint32_t n_nodes;
     uint32_t n_prims;
+    uint32_t n_unbounded;   // the last n_unbounded leaf-order primitives: media tested after the walk
     uint32_t n_perlin;
     uint32_t n_quads;       // the scene's quads (boundary quads follow them)
     uint32_t n_media;

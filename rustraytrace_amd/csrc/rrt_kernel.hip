@@ -1431,6 +1431,22 @@ __device__ __forceinline__ void render_body(const KParams &P) {
         if (has && !need_ray && tr.node < 0) {
             need_ray = 1;
             const Prims<kBook2> spr{prims, motion, ps.time, P.quads, P.media, P.n_quads, rng_key(ps.rng) ^ ((uint64_t)ps.k << 32)};
+            if constexpr (Prims<kBook2>::kHasMedia) {
+                // The unbounded media (a fog around the whole scene; rrt_host.cpp unbounded_media):
+                // not in the tree, tested here against the closest hit of the walk, every lane whose
+                // query ended this iteration together. The same hit as testing them in the tree: the
+                // free flight is clipped to the closest hit so far and the draw is fixed per
+                // (path, segment, medium). rk is this iteration's: the lane was in the tree.
+                for (uint32_t u = P.n_prims - P.n_unbounded; u < P.n_prims; ++u) {
+                    if (kCount) cnt.spheres++;
+                    const int m = (int)(-prims[u].w) - 1 - (int)P.n_quads;
+                    float tm;
+                    if (medium_hit(spr, m, ps.o, ps.d, rk, tr.closest, tm)) {
+                        tr.closest = tm;
+                        tr.hit_prim = (int)u;
+                    }
+                }
+            }
 #ifdef RRT_TRACE_X
             if ((xy & 0xffffu) == RRT_TRACE_X && (xy >> 16) == RRT_TRACE_Y && s == RRT_TRACE_S)
                 printf("K k=%u o=(%a %a %a) d=(%a %a %a) t=%a prim=%d T=(%a %a %a) rng=%llx\n", ps.k, ps.o.x, ps.o.y,

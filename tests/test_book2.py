@@ -170,6 +170,27 @@ def test_book2_kbvh_agrees_with_books_tree(scene):
     assert np.array_equal(a, b) and (ra == rb or sc.quads is not None)
 
 
+@pytest.mark.parametrize("scene", [9, 10])
+def test_unbounded_media_tested_after_the_walk(scene):
+    # final_scene's fog (a sphere medium of radius 5000 around everything) is left out of the
+    # kernel's tree and tested after the walk (rrt_host.cpp unbounded_media); the f32 modes follow.
+    # A scheduling choice: the oracle's diagnostic mode 0x400 keeps it in the tree, same image.
+    sc = rrt.next_week_scene(scene, dict(image_width=64, samples_per_pixel=8))
+    nodes, order, info = build_bvh(sc)
+    n_prims = len(sc.spheres) + len(sc.quads) + len(sc.media)
+    fog = len(sc.spheres) + len(sc.quads) + int(np.argmax(sc.media["sphere"][:, 3]))
+    assert info["n_unbounded"] == 1 and len(order) == n_prims and order[-1] == fog
+    a, ra, ta = oracle.render(sc, oracle.TWIN, threads=8)
+    b, rb, tb = oracle.render(sc, oracle.TWIN | 0x400, threads=8)
+    assert np.array_equal(a, b) and ra == rb and ta < tb
+
+
+def test_bounded_media_stay_in_the_tree():
+    for scene in (8,):  # cornell_smoke: box-bounded media
+        _, _, info = build_bvh(rrt.next_week_scene(scene, dict(image_width=32, samples_per_pixel=1)))
+        assert info["n_unbounded"] == 0
+
+
 def test_motion_blur_changes_the_image():
     # the moving spheres are sampled along their motion: zeroing the motion changes the picture
     sc = rrt.next_week_scene(1, dict(image_width=48, samples_per_pixel=8, max_depth=6))
