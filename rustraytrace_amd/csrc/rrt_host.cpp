@@ -1159,6 +1159,13 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
     // BVH2: the node layout already encodes the choice (80-B sign-ordered nodes are the LDS ones)
     p.scene_in_lds = fb.width == 2 ? fb.stride == (uint32_t)sizeof(rrt::GNode)
                                    : scene_lds_fit(fb.bytes.size(), n_prims, book2);
+    {  // Perlin tables in LDS when the block's LDS (stack + staged scene + tables) stays within 64 KB
+        const size_t stack = ((size_t)p.stack_depth * rrt::kBlock * (fb.n_nodes > 65535u ? 4u : 2u) + 15u) / 16u * 16u;
+        const size_t scene = p.scene_in_lds ? fb.bytes.size() + (size_t)n_prims * (rrt::kPrimBytes + (book2 ? rrt::kMotionBytes : 0)) : 0;
+        p.perlin_in_lds = book2 && n_perlin > 0 &&
+                          stack + scene + (size_t)n_perlin * sizeof(rrt::GPerlin) <= 64u * 1024u ? 1u : 0u;
+        if (const char *e = std::getenv("RRT_PERLIN_IN_LDS")) p.perlin_in_lds = p.perlin_in_lds && std::atoi(e) != 0;
+    }
     p.trav_frac = 32;
     p.leaf_frac = 32;
     p.min_waves = 6;

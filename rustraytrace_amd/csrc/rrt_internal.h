@@ -162,6 +162,7 @@ struct KParams {
     uint32_t n_prims;
     uint32_t n_unbounded;   // the last n_unbounded leaf-order primitives: media tested after the walk
     uint32_t n_perlin;
+    uint32_t perlin_in_lds; // book-2 kernels stage the Perlin tables in LDS after the scene
     uint32_t n_quads;       // the scene's quads (boundary quads follow them)
     uint32_t n_media;
     uint32_t n_lights;

@@ -310,6 +310,7 @@ struct Prims {
     const GMedium *md;  // media, tagged -(1 + n_quads + index)
     uint32_t n_quads;
     uint64_t seg;  // the path's RNG state at this segment ^ (bounce << 32): key of the media draws
+    const GPerlin *perlin;  // Perlin tables (LDS copy when staged, else KParams.perlin)
     static constexpr bool kHasQuads = kBook2 >= 2;
     static constexpr bool kHasMedia = kBook2 >= 3;
     // Book-1 scenes store r * r (f32, rounded as the test would round it) in the record's w and
@@ -855,23 +856,21 @@ __device__ __forceinline__ float perlin_noise(const GPerlin *__restrict__ pt, V3
     const float uu = u * u * (3.0f - 2.0f * u);
     const float vv = v * v * (3.0f - 2.0f * v);
     const float ww = w * w * (3.0f - 2.0f * w);
+    // the two permutation entries per axis, read once (the corner loop indexes them by its bits)
+    const uint32_t px0 = pt->perm[(uint32_t)i & 255u] & 0xffu, px1 = pt->perm[(uint32_t)(i + 1) & 255u] & 0xffu;
+    const uint32_t py0 = (pt->perm[(uint32_t)j & 255u] >> 8) & 0xffu, py1 = (pt->perm[(uint32_t)(j + 1) & 255u] >> 8) & 0xffu;
+    const uint32_t pz0 = (pt->perm[(uint32_t)k & 255u] >> 16) & 0xffu, pz1 = (pt->perm[(uint32_t)(k + 1) & 255u] >> 16) & 0xffu;
     float accum = 0.0f;
 #pragma unroll 1
-    for (int di = 0; di < 2; ++di)
-#pragma unroll 1
-        for (int dj = 0; dj < 2; ++dj)
-#pragma unroll 1
-            for (int dk = 0; dk < 2; ++dk) {
-                const uint32_t px = pt->perm[(uint32_t)(i + di) & 255u] & 0xffu;
-                const uint32_t py = (pt->perm[(uint32_t)(j + dj) & 255u] >> 8) & 0xffu;
-                const uint32_t pz = (pt->perm[(uint32_t)(k + dk) & 255u] >> 16) & 0xffu;
-                const float4 c = pt->randvec[px ^ py ^ pz];
-                const float wx = u - (float)di, wy = v - (float)dj, wz = w - (float)dk;
-                const float fi = di ? uu : 1.0f - uu;
-                const float fj = dj ? vv : 1.0f - vv;
-                const float fk = dk ? ww : 1.0f - ww;
-                accum = accum + fi * fj * fk * dot(v3(c.x, c.y, c.z), v3(wx, wy, wz));
-            }
+    for (int corner = 0; corner < 8; ++corner) {  // (di, dj, dk) in perlin_interp's nested order
+        const int di = corner >> 2, dj = (corner >> 1) & 1, dk = corner & 1;
+        const float4 c = pt->randvec[(di ? px1 : px0) ^ (dj ? py1 : py0) ^ (dk ? pz1 : pz0)];
+        const float wx = u - (float)di, wy = v - (float)dj, wz = w - (float)dk;
+        const float fi = di ? uu : 1.0f - uu;
+        const float fj = dj ? vv : 1.0f - vv;
+        const float fk = dk ? ww : 1.0f - ww;
+        accum = accum + fi * fj * fk * dot(v3(c.x, c.y, c.z), v3(wx, wy, wz));
+    }
     return accum;
 }
 
@@ -983,7 +982,7 @@ __device__ __forceinline__ bool shade(const KParams &P, const PR &prims, const G
             att = checker_even(m.a.w, p) ? v3(m.a.x, m.a.y, m.a.z)
                                          : v3(__int_as_float(m.b.y), __int_as_float(m.b.z), __int_as_float(m.b.w));
         } else if (kBook2 && kind == 6) {  // NoiseTexture at p
-            const float g = noise_value(P.perlin + m.b.z, m.a.w, p);
+            const float g = noise_value(prims.perlin + m.b.z, m.a.w, p);
             att = v3(g, g, g);
         } else {
             att = v3(m.a.x, m.a.y, m.a.z);
@@ -1182,7 +1181,7 @@ __device__ __forceinline__ bool shade_b3(const KParams &P, const PR &prims, cons
         att = checker_even(m.a.w, p) ? v3(m.a.x, m.a.y, m.a.z)
                                      : v3(__int_as_float(m.b.y), __int_as_float(m.b.z), __int_as_float(m.b.w));
     } else if (kind == 6) {
-        const float g = noise_value(P.perlin + m.b.z, m.a.w, p);
+        const float g = noise_value(prims.perlin + m.b.z, m.a.w, p);
         att = v3(g, g, g);
     } else {
         att = v3(m.a.x, m.a.y, m.a.z);
@@ -1274,6 +1273,22 @@ __device__ __forceinline__ void render_body(const KParams &P) {
         prims = reinterpret_cast<const float4 *>(dst + nn);
         mtl = reinterpret_cast<const GMaterial *>(dst + nn + P.n_prims);
         if constexpr (kBook2) motion = reinterpret_cast<const float4 *>(dst + nn + P.n_prims + nm);
+    }
+    // Perlin tables (5 KB each) staged in LDS after the scene: a noise texture value reads 56
+    // lattice corners, each a permutation lookup then a dependent gradient load, so from L2 its
+    // 7 octaves are a chain of ~100 round trips.
+    const GPerlin *perlin = P.perlin;
+    if constexpr (kBook2 != 0) {
+        if (P.perlin_in_lds) {
+            size_t off16 = (P.stack_depth * kBlock * sizeof(StackT) + 15u) / 16u;
+            if constexpr (kLds) off16 += P.n_nodes * (uint32_t)(sizeof(Node) / 16) + 3u * P.n_prims + P.n_prims;
+            uint4 *dst = lds_dyn + off16;
+            const uint4 *src = reinterpret_cast<const uint4 *>(P.perlin);
+            const uint32_t n16 = P.n_perlin * (uint32_t)(sizeof(GPerlin) / 16);
+            for (uint32_t i = threadIdx.x; i < n16; i += kBlock) dst[i] = src[i];
+            __syncthreads();
+            perlin = reinterpret_cast<const GPerlin *>(dst);
+        }
     }
     LdsStack<StackT> stack;
     stack.init(lds_stack, threadIdx.x);
@@ -1383,7 +1398,7 @@ __device__ __forceinline__ void render_body(const KParams &P) {
         }
         RayK rk;
         if (tr.node >= 0) rk = ray_consts(ps.o, ps.d);
-        const Prims<kBook2> pr{prims, motion, ps.time, P.quads, P.media, P.n_quads, rng_key(ps.rng) ^ ((uint64_t)ps.k << 32)};
+        const Prims<kBook2> pr{prims, motion, ps.time, P.quads, P.media, P.n_quads, rng_key(ps.rng) ^ ((uint64_t)ps.k << 32), perlin};
         if constexpr (kWide) {
             for (;;) {
                 if constexpr (RRT_PHASE_TIMING == 2) {
@@ -1430,7 +1445,7 @@ __device__ __forceinline__ void render_body(const KParams &P) {
         }
         if (has && !need_ray && tr.node < 0) {
             need_ray = 1;
-            const Prims<kBook2> spr{prims, motion, ps.time, P.quads, P.media, P.n_quads, rng_key(ps.rng) ^ ((uint64_t)ps.k << 32)};
+            const Prims<kBook2> spr{prims, motion, ps.time, P.quads, P.media, P.n_quads, rng_key(ps.rng) ^ ((uint64_t)ps.k << 32), perlin};
             if constexpr (Prims<kBook2>::kHasMedia) {
                 // The unbounded media (a fog around the whole scene; rrt_host.cpp unbounded_media):
                 // not in the tree, tested here against the closest hit of the walk, every lane whose
@@ -1583,6 +1598,7 @@ hipError_t launch_variant(const KParams &p, bool count, hipStream_t stream) {
     if (kLds)
         lds += (size_t)p.n_nodes * (kWide ? sizeof(GNode4) : sizeof(GNode)) +  // LDS BVH2 = GNode
                (size_t)p.n_prims * (kPrimBytes + (kBook2 ? kMotionBytes : 0));
+    if (kBook2 && p.perlin_in_lds) lds += (size_t)p.n_perlin * sizeof(GPerlin);
     auto kernel = count ? rrt_render<kLds, true, StackT, kWide, kWaves, kBook2>
                         : rrt_render<kLds, false, StackT, kWide, kWaves, kBook2>;
     // Persistent grid: as many blocks as can be resident (occupancy at this LDS size), capped
