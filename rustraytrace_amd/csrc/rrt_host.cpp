@@ -1101,7 +1101,7 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
         if ((rc = upload(&s->d_texs, texs.data(), texs.size(), "texture table"))) break;
         if (hipMalloc((void **)&s->d_counters, 8 * sizeof(unsigned long long)) != hipSuccess ||
             hipMalloc((void **)&s->d_work_counters, 8 * sizeof(unsigned long long)) != hipSuccess ||
-            hipMalloc((void **)&s->d_unit_counter, 64) != hipSuccess) {
+            hipMalloc((void **)&s->d_unit_counter, rrt::kQueues * 128u) != hipSuccess) {
             rc = fail(RRT_E_NOMEM, "hipMalloc counters failed");
             break;
         }

@@ -196,13 +196,14 @@ struct KParams {
     // Division by the queue's uniform divisors as multiply-high + add + shift (FastDiv): the
     // generic 32-bit division sequence is ~35 instructions, paid at every unit start and end.
     FastDiv fd_pass_big, fd_pass_tail, fd_tiles_x, fd_band_rows, fd_n_ranks, fd_chunk, fd_chunk_small, fd_sqrt_spp;
-    uint32_t *unit_counter;   // device queue head (zeroed per launch)
+    uint32_t *unit_counter;   // device queue heads: kQueues counters 128 B apart (zeroed per launch)
     float4 *partial;          // [pass chunk][tile pixel] partial sums when n_chunks > 1: a chunk's
                               // pixels are contiguous, so an 8x8 tile's rows fill whole 128-B lines
 };
 
 // Traversal stack entries held in LDS per lane: up to 64 (BVH depth <= 63).
 constexpr int kMaxStackDepth = 64;
+constexpr uint32_t kQueues = 8;  // work-queue counters (blocks dealt round-robin, one per XCD)
 #ifndef RRT_BLOCK
 #define RRT_BLOCK 512
 #endif

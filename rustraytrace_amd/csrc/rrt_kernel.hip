@@ -48,6 +48,9 @@ namespace {
 #ifndef RRT_HOISTDIV
 #define RRT_HOISTDIV 1
 #endif
+#ifndef RRT_XQ
+#define RRT_XQ 1
+#endif
 
 // 64 if the calling lane is the wave's first active lane, else 0 (wave-level event count).
 __device__ __forceinline__ uint32_t wave_slot() {
@@ -1315,17 +1318,31 @@ __device__ __forceinline__ void render_body(const KParams &P) {
     // v_mov instead of the three exec-mask merges a bool held in an SGPR pair costs.
     tr.node = -1;
     uint32_t need_ray = 0;  // the lane must start the next segment of its path
-    uint32_t pool_base = 0, pool_left = 0;  // wave-uniform: claimed, not yet assigned units
+    // wave-uniform: claimed, not yet assigned units (RRT_XQ: pool_base starts in the block's queue)
+    uint32_t pool_base = RRT_XQ ? (blockIdx.x & (kQueues - 1u)) * 64u : 0u, pool_left = 0;
     [[maybe_unused]] uint64_t ph0 = 0, ph1 = 0, ph2 = 0, tp = 0;
     for (;;) {
         if constexpr (RRT_PHASE_TIMING == 1) tp = __builtin_amdgcn_s_memtime();
         if constexpr (RRT_PHASE_TIMING == 2) ph2++;
         uint64_t idle = __ballot(!has);
         if (idle != 0 && pool_left == 0 && q_open) {
+#if RRT_XQ
+            // kQueues interleaved queues with a counter each, 128 B apart: tile-chunk group g
+            // (64 units) is queue g % kQueues's (g / kQueues)-th claim, and the blocks are dealt to
+            // the queues as blockIdx % kQueues (on MI355X the blocks' XCDs). One counter took every
+            // wave's claims: device-scope atomics on one address serialise, which cost cheap-ray,
+            // low-spp frames a third of their time. The grid has >= kQueues blocks (launch_variant),
+            // and pool_base always lies in the wave's queue (it starts at the queue's first group).
+            const uint32_t xq = (pool_base >> 6) & (kQueues - 1u);
+            uint32_t k = 0;
+            if (lane == 0) k = atomicAdd(P.unit_counter + 32u * xq, 1u);
+            const uint32_t base = (__shfl(k, 0, 64) * kQueues + xq) * 64u;
+#else
             // one atomic claims a whole tile-chunk (64 units) for this wave
             uint32_t base = 0;
             if (lane == 0) base = atomicAdd(P.unit_counter, 64u);
             base = __shfl(base, 0, 64);
+#endif
             if (base >= P.n_units) {
                 q_open = false;
             } else {
@@ -1608,8 +1625,9 @@ hipError_t launch_variant(const KParams &p, bool count, hipStream_t stream) {
     if (e != hipSuccess) return e;
     if (per_cu < 1) per_cu = 1;
     const uint32_t want = (p.n_units + kBlock - 1) / kBlock;
-    const uint32_t blocks = std::min<uint32_t>(want, (uint32_t)per_cu * p.n_cus);
-    e = hipMemsetAsync(p.unit_counter, 0, sizeof(uint32_t), stream);
+    // at least kQueues blocks, so every work queue has a block (spare blocks find no work and exit)
+    const uint32_t blocks = std::max<uint32_t>(std::min<uint32_t>(want, (uint32_t)per_cu * p.n_cus), RRT_XQ ? kQueues : 1u);
+    e = hipMemsetAsync(p.unit_counter, 0, kQueues * 32u * sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(kernel, dim3(blocks), dim3(kBlock), lds, stream, p);
     e = hipGetLastError();
