@@ -51,9 +51,6 @@ namespace {
 #ifndef RRT_XQ
 #define RRT_XQ 1
 #endif
-#ifndef RRT_RUV_ITERS
-#define RRT_RUV_ITERS 4
-#endif
 
 // 64 if the calling lane is the wave's first active lane, else 0 (wave-level event count).
 __device__ __forceinline__ uint32_t wave_slot() {
@@ -146,31 +143,6 @@ __device__ __forceinline__ V3 random_unit_vector(RngState &s, C &cnt) {
     const float inv = 1.0f / __builtin_sqrtf(lensq);
     return v3(px * inv, py * inv, pz * inv);
 }
-
-#if RRT_RUV_ITERS
-// random_unit_vector split across shading passes: at most RRT_RUV_ITERS candidates per call.
-// Returns false when none was accepted; the lane's stream has advanced past the rejected
-// candidates, so the next call continues the same sequence of draws (identical results). A wave
-// otherwise runs the loop as long as its unluckiest lane: 5.7 wave iterations per pass for 1.9
-// expected per lane.
-template <typename C>
-__device__ __forceinline__ bool random_unit_vector_part(RngState &s, V3 &out, C &cnt) {
-    float px, py, pz, lensq;
-#pragma unroll 1
-    for (int it = 0; it < RRT_RUV_ITERS; ++it) {
-        if constexpr (RRT_PHASE_TIMING == 4) cnt.d2 += wave_slot();
-        px = rnd_pm1(s);
-        py = rnd_pm1(s);
-        pz = rnd_pm1(s);
-        lensq = __builtin_fmaf(pz, pz, __builtin_fmaf(py, py, px * px));
-        if (0.0f < lensq && lensq <= 1.0f) break;
-    }
-    if (!(0.0f < lensq && lensq <= 1.0f)) return false;  // the last candidate was rejected too
-    const float inv = 1.0f / __builtin_sqrtf(lensq);
-    out = v3(px * inv, py * inv, pz * inv);
-    return true;
-}
-#endif
 
 // vec3.rs:201-203 reflect = v - n*(2*dot(v,n))
 __device__ __forceinline__ V3 reflect(V3 v, V3 n) { return sub(v, muls(n, 2.0f * dot(v, n))); }
@@ -946,11 +918,9 @@ __device__ __forceinline__ V3 texel(const KParams &P, int tex, float u, float v)
 // After the closest-hit query of the current segment (prim < 0: miss): background, or
 // emission / scatter / RR (camera.rs:182-209). Returns true when the path has ended; a
 // path ending at the sky or an emitter adds T*Le to `sum`.
-// Returns 1 when the path has ended, 0 when it continues, 2 (RRT_RUV_ITERS, book 1) when the
-// random unit vector is not drawn yet: the lane shades again in the next pass, from the same hit.
 template <int kBook2, typename C, class PR>
-__device__ __forceinline__ int shade(const KParams &P, const PR &prims, const GMaterial *mtl, PathState &ps,
-                                     float t, int prim, V3 &sum, C &cnt) {
+__device__ __forceinline__ bool shade(const KParams &P, const PR &prims, const GMaterial *mtl, PathState &ps,
+                                      float t, int prim, V3 &sum, C &cnt) {
     if constexpr (RRT_PHASE_TIMING == 4) {
         cnt.d0 += wave_slot();
         cnt.d1 += 1;
@@ -965,7 +935,7 @@ __device__ __forceinline__ int shade(const KParams &P, const PR &prims, const GM
             bg = v3((1.0f - a) * 1.0f + a * 0.5f, (1.0f - a) * 1.0f + a * 0.7f, (1.0f - a) * 1.0f + a * 1.0f);
         }
         sum = add(sum, mul(ps.T, bg));
-        return 1;
+        return true;
     }
     // HitRecord (sphere.rs:47-50, hittable.rs:20-32)
     const float4 cr = prims.at(prim);  // the sphere's center at the ray's time (sphere.rs:48)
@@ -995,20 +965,12 @@ __device__ __forceinline__ int shade(const KParams &P, const PR &prims, const GM
     V3 dir;
     if (kind == 4) {  // DiffuseLight: emitted, scatter None
         sum = add(sum, mul(ps.T, v3(m.a.x, m.a.y, m.a.z)));
-        return 1;
+        return true;
     }
     // Lambertian and Metal both draw one random_unit_vector and nothing else before RR: one
     // rejection loop for both kinds (a wave mixing them runs it once, not twice).
     V3 r = v3(0.0f, 0.0f, 0.0f);
-#if RRT_RUV_ITERS
-    if constexpr (kBook2 == 0) {
-        if (kind != 2 && !random_unit_vector_part(ps.rng, r, cnt)) return 2;
-    } else {
-        if (kind != 2) r = random_unit_vector(ps.rng, cnt);
-    }
-#else
     if (kind != 2) r = random_unit_vector(ps.rng, cnt);
-#endif
     if (kBook2 && kind == 7) {  // Isotropic (material.rs:153-158): a fresh random_unit_vector
         dir = r;
         att = v3(m.a.x, m.a.y, m.a.z);
@@ -1031,7 +993,7 @@ __device__ __forceinline__ int shade(const KParams &P, const PR &prims, const GM
     } else if (kind == 1) {  // Metal (material.rs:53-64)
         const V3 refl = unit(reflect(ps.d, nrm));
         dir = add(refl, muls(r, m.a.w));
-        if (!(dot(dir, nrm) > 0.0f)) return 1;  // absorbed
+        if (!(dot(dir, nrm) > 0.0f)) return true;  // absorbed
         att = v3(m.a.x, m.a.y, m.a.z);
     } else {  // Dielectric (material.rs:83-102)
         const float eta = __int_as_float(m.b.y);
@@ -1051,7 +1013,7 @@ __device__ __forceinline__ int shade(const KParams &P, const PR &prims, const GM
         if (att.z > pr) pr = att.z;
         if (pr < 0.05f) pr = 0.05f;
         if (pr > 0.95f) pr = 0.95f;
-        if (rnd(ps.rng) > pr) return 1;
+        if (rnd(ps.rng) > pr) return true;
         ps.T = muls(mul(ps.T, att), 1.0f / pr);
     } else {
         ps.T = mul(ps.T, att);
@@ -1060,7 +1022,7 @@ __device__ __forceinline__ int shade(const KParams &P, const PR &prims, const GM
     ps.d = dir;
     ps.k++;
     ps.skip = exit_skip(is_quad, is_medium, front, dir, nrm, prim);
-    return 0;
+    return false;
 }
 
 // ---- book 3 (the_rest_of_your_life): pdfs, light sampling, the MIS shading step ---------------
@@ -1524,11 +1486,7 @@ __device__ __forceinline__ void render_body(const KParams &P) {
                        (unsigned long long)rng_key(ps.rng));
 #endif
             if constexpr (kBook2 == 4) seg_done = shade_b3(P, spr, mtl, ps, tr.closest, tr.hit_prim, sum, cnt) ? 1u : 0u;
-            else {
-                const int st = shade<kBook2>(P, spr, mtl, ps, tr.closest, tr.hit_prim, sum, cnt);
-                seg_done = st == 1 ? 1u : 0u;
-                if (st == 2) need_ray = 0;  // shade again next pass (same hit, the stream continues)
-            }
+            else seg_done = shade<kBook2>(P, spr, mtl, ps, tr.closest, tr.hit_prim, sum, cnt) ? 1u : 0u;
         }
         w_paths += (uint32_t)__popcll(__ballot(seg_done));
         if (seg_done) {  // pixel_color += ray_color(..) (camera.rs:73-76): already in `sum`
