@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -737,6 +738,7 @@ struct RrtScene {
     uint32_t *d_unit_counter = nullptr;             // persistent-queue head
     float4 *d_partial = nullptr;                    // chunk partial sums
     size_t partial_cap = 0;                         // float4 elements
+    uint32_t last_groups = 0, last_passes = 0;      // the last launch: 64-unit groups per pass, passes
     rrt::KParams base{};
     RrtBvhInfo info{};
 };
@@ -1303,8 +1305,33 @@ int32_t rrt_render_tile_async(RrtScene *scene, const RrtTile *tile, float *d_acc
         return RRT_OK;
     }
     HIP_TRY(rrt::launch_render(p, (hipStream_t)stream), "render kernel launch");
+    const uint32_t per_pass = (p.pass_chunks == 0 || p.pass_chunks >= p.n_chunks) ? p.n_chunks : p.pass_chunks;
+    scene->last_passes = (p.n_chunks + per_pass - 1) / per_pass;
+    scene->last_groups = p.n_work_tiles * per_pass;
     return RRT_OK;
 }
+
+namespace {
+// Progress of a render in flight on `scene`'s device (the one-shot call): the work queues' heads
+// read on a side stream while the kernel runs. Head q counts the claims of queue q (group g =
+// claim * kQueues + q), capped at the queue's groups; a pass boundary resets the heads. Returns
+// the fraction in [0, 1), or -1 when the heads cannot be read.
+double render_progress(RrtScene *scene, hipStream_t side, uint32_t *host_heads, uint32_t &pass, uint32_t &last_sum) {
+    if (hipMemcpyAsync(host_heads, scene->d_unit_counter, rrt::kQueues * 128u, hipMemcpyDeviceToHost, side) != hipSuccess ||
+        hipStreamSynchronize(side) != hipSuccess)
+        return -1.0;
+    const uint32_t groups = scene->last_groups, passes = std::max(1u, scene->last_passes);
+    uint32_t sum = 0;
+    for (uint32_t q = 0; q < rrt::kQueues; ++q) {
+        const uint32_t mine = groups > q ? (groups - q + rrt::kQueues - 1) / rrt::kQueues : 0u;
+        sum += std::min(host_heads[32u * q], mine);
+    }
+    if (sum + groups / 4 < last_sum && pass + 1 < passes) ++pass;  // the heads were reset: next pass
+    last_sum = sum;
+    const double in_pass = groups ? (double)sum / groups : 0.0;
+    return std::min(0.999, (pass + in_pass) / passes);
+}
+}  // namespace
 
 int32_t rrt_scene_read_counters(RrtScene *scene, RrtCounters *out) {
     if (!scene || !out) return fail(RRT_E_INVALID, "null scene or out");
@@ -1369,6 +1396,7 @@ static int32_t render_frame(const RrtCamera *cam, const RrtSphere *spheres, uint
     std::string first_err;
     int first_rc = RRT_OK;
     std::atomic<uint32_t> done{0};
+    std::vector<double> frac(n_gpus, 0.0);  // per-GPU progress (guarded by mu)
     auto worker = [&](uint32_t g) {
         auto set_err = [&](int rc) {
             std::lock_guard<std::mutex> lk(mu);
@@ -1396,6 +1424,36 @@ static int32_t render_frame(const RrtCamera *cam, const RrtSphere *spheres, uint
             return set_err(RRT_E_NOMEM);
         }
         rc = rrt_render_tile_async(scene, &tile, d_accum, nullptr);
+        if (!rc && !(flags & RRT_FLAG_QUIET)) {
+            // within-GPU progress (the reference prints one line per sample pass, cuda/mod.rs:426-431):
+            // poll the work-queue heads every 100 ms while the kernel runs
+            hipEvent_t ev = nullptr;
+            hipStream_t side = nullptr;
+            uint32_t *heads = nullptr;
+            if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess && hipEventRecord(ev, nullptr) == hipSuccess &&
+                hipStreamCreateWithFlags(&side, hipStreamNonBlocking) == hipSuccess &&
+                hipHostMalloc((void **)&heads, rrt::kQueues * 128u, 0) == hipSuccess) {
+                uint32_t pass = 0, last_sum = 0;
+                int shown = -1;
+                while (hipEventQuery(ev) == hipErrorNotReady) {
+                    std::this_thread::sleep_for(std::chrono::milliseconds(100));
+                    const double f = render_progress(scene, side, heads, pass, last_sum);
+                    if (f < 0.0) break;
+                    std::lock_guard<std::mutex> lk(mu);
+                    frac[g] = f;
+                    double all = 0.0;
+                    for (double x : frac) all += x;
+                    const int pct = (int)(100.0 * all / n_gpus);
+                    if (pct != shown) {
+                        shown = pct;
+                        std::fprintf(stderr, "\rHIP progress: %d%% (%u/%u GPUs done)", pct, done.load(), n_gpus);
+                    }
+                }
+            }
+            if (heads) (void)hipHostFree(heads);
+            if (side) (void)hipStreamDestroy(side);
+            if (ev) (void)hipEventDestroy(ev);
+        }
         if (!rc && rgb8_out) {
             const float scale = 1.0f / (float)total_spp;  // render_io.rs:10
             e = rrt::launch_quantize(d_accum, d_rgb8, (uint32_t)n_px, scale, nullptr);
@@ -1431,7 +1489,10 @@ static int32_t render_frame(const RrtCamera *cam, const RrtSphere *spheres, uint
         const uint32_t d = ++done;
         if (!(flags & RRT_FLAG_QUIET)) {
             std::lock_guard<std::mutex> lk(mu);
-            std::fprintf(stderr, "\rHIP progress: %u/%u GPUs (%.1f%%)", d, n_gpus, 100.0 * d / n_gpus);
+            frac[g] = 1.0;
+            double all = 0.0;
+            for (double x : frac) all += x;
+            std::fprintf(stderr, "\rHIP progress: %d%% (%u/%u GPUs done)", (int)(100.0 * all / n_gpus), d, n_gpus);
             if (d == n_gpus) std::fprintf(stderr, "\n");
         }
     };

@@ -79,3 +79,21 @@ def test_cli_output_paths_agree(tmp_path):
     assert head == b"P6\n64 36"
     vals = [int(v) for v in outs["dev"].split(b"\n255\n", 1)[1].split()]
     assert list(px) == vals
+
+
+def test_cli_reports_progress_within_the_render(tmp_path):
+    # rrt_hip_render polls the work-queue heads while the kernel runs and prints the fraction
+    # done (the reference prints one line per sample pass, cuda/mod.rs:426-431): a ~0.4 s render
+    # shows intermediate percentages, increasing, then 100 % with the GPU count.
+    import os
+    import re
+    import subprocess
+
+    _torch()
+    cli = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "rustraytrace_amd", "rrt")
+    r = subprocess.run([cli, "--backend", "hip", "in_one_weekend", "--image_width", "1920", "--samples_per_pixel",
+                        "2048", "-o", str(tmp_path / "p.ppm"), "--p6"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    pcts = [int(p) for p in re.findall(r"HIP progress: (\d+)%", r.stderr)]
+    assert pcts and pcts[-1] == 100 and "(1/1 GPUs done)" in r.stderr
+    assert any(0 < p < 100 for p in pcts) and pcts == sorted(pcts)
