@@ -1168,8 +1168,12 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
                           stack + scene + (size_t)n_perlin * sizeof(rrt::GPerlin) <= 64u * 1024u ? 1u : 0u;
         if (const char *e = std::getenv("RRT_PERLIN_IN_LDS")) p.perlin_in_lds = p.perlin_in_lds && std::atoi(e) != 0;
     }
-    p.trav_frac = 32;
-    p.leaf_frac = 32;
+    // traversal exit / leaf batch thresholds (x/256 of the live lanes), same-box sweeps against 32/32:
+    // book-1 LDS scenes 56/56 (C2 +0.6 %, C4 +0.25 %); L2 scenes 64/48 (C5 +2.0 %, final_scene and
+    // bouncing spheres +4 %); book-2/3 LDS scenes keep 32/32 (56/56: cornell_box +5 %, but
+    // cornell_smoke -10 %, perlin_spheres -4 %)
+    p.trav_frac = p.scene_in_lds ? (book2 ? 32 : 56) : 64;
+    p.leaf_frac = p.scene_in_lds ? (book2 ? 32 : 56) : 48;
     p.min_waves = 6;
     p.chunk = accum_chunk();
     {
