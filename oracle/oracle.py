@@ -18,7 +18,7 @@ TWIN, BOOKS = 0, 1
 # Accum summation chunk K of the HIP backend (include/rrt_hip.h rrt_accum_chunk): (S-1)/K chunks
 # of K samples, then chunks of max(1, K/8) for the tail; samples summed in order within a chunk,
 # chunk sums added in order.
-DEFAULT_CHUNK = 64
+DEFAULT_CHUNK = 128
 
 _LIB = None
 
