@@ -238,7 +238,9 @@ uint32_t rrt_hip_abi_version(void);
 
 /* Summation order of the accum: a pixel's RGB = sum over consecutive chunks of its S samples
  * (counted from the tile's sample_begin) of each chunk's in-order sample sum, chunks added in
- * order: ((c0 + c1) + c2) + ... With K = rrt_accum_chunk() and k = max(1, K / 8): the first
+ * order: ((c0 + c1) + c2) + ... With K = rrt_accum_chunk() when S > 2 * rrt_accum_chunk(), else
+ * K = rrt_accum_chunk() / 2 (ABI v6: big chunks at high spp, small ones at low spp), and
+ * k = max(1, K / 8): the first
  * nb = (S - 1) / K chunks hold K samples each (nb = 0 when S <= K), the remaining S - nb*K
  * samples form chunks of k (the last one possibly shorter) — small units at the end of the
  * work queue keep the persistent grid's tail short. Needed to reproduce it bit for bit.

@@ -138,9 +138,9 @@ def test_multi_gpu_one_shot_equals_single():
 
 @pytest.mark.parametrize("spp,s0", [(200, 0), (130, 7), (128, 0), (100, 3), (9, 0), (129, 0), (300, 0)])
 def test_chunked_accumulation_matches_oracle(spp, s0):
-    # K = 128, tail chunks of 16: (128, 0): S == K, no big chunk, eight 16-sample tail chunks;
-    # (100, 3): 6 x 16 + a 4-sample last chunk; (9, 0): one chunk; (129, 0): 128 + 1; (200, 0): 128
-    # + 4 x 16 + 8; (300, 0): 2 x 128 + 2 x 16 + 12.
+    # rrt_accum_chunk() = 128; frames of S <= 256 samples use K = 64 (tail chunks of 8), larger
+    # ones K = 128 (tail chunks of 16): (128, 0): 64 + 8 x 8; (100, 3): 64 + 4 x 8 + 4; (9, 0):
+    # 8 + 1; (129, 0): 2 x 64 + 1; (200, 0): 3 x 64 + 8; (300, 0): 2 x 128 + 2 x 16 + 12.
     # > rrt_accum_chunk() samples: the persistent queue splits pixels into chunks whose sums are
     # combined in chunk order; the oracle reproduces that order (rows, partial last chunk, offset).
     assert rrt._lib.load().rrt_accum_chunk() == oracle.DEFAULT_CHUNK
@@ -152,9 +152,10 @@ def test_chunked_accumulation_matches_oracle(spp, s0):
 
 
 def test_sample_passes_are_bit_identical(monkeypatch):
-    # A 1 MiB partial budget holds 4 chunks of this 160x90 frame (230 KB each): its 9 chunks
-    # (1 x 128 samples, then 7 x 16 + 10) run as 3 sample passes of 4, 4, 1 chunks — the first
-    # mixes big and tail chunks — whose combines continue one fold: same bits as one pass.
+    # A 1 MiB partial budget holds 4 chunks of this 160x90 frame (230 KB each): its 11 chunks
+    # (K = 64 at 250 spp: 3 x 64 samples, then 7 x 8 + 2) run as 3 sample passes of 4, 4, 3
+    # chunks — the first mixes big and tail chunks — whose combines continue one fold: same bits
+    # as one pass.
     scene = rrt.rtow(image_width=160, samples_per_pixel=250, max_depth=8)
     one, _, ctr1, _ = gpu_tile(scene)
     monkeypatch.setenv("RRT_PARTIAL_MB", "1")
