@@ -51,6 +51,19 @@ namespace {
 #ifndef RRT_XQ
 #define RRT_XQ 1
 #endif
+// Wave issue priority per loop phase (s_setprio levels 0-3; see the work loop's head).
+#ifndef RRT_PRIO_REFILL
+#define RRT_PRIO_REFILL 2
+#endif
+#ifndef RRT_PRIO_NODE
+#define RRT_PRIO_NODE 1
+#endif
+#ifndef RRT_PRIO_LEAF
+#define RRT_PRIO_LEAF 2
+#endif
+#ifndef RRT_PRIO_SHADE
+#define RRT_PRIO_SHADE 0
+#endif
 
 // 64 if the calling lane is the wave's first active lane, else 0 (wave-level event count).
 __device__ __forceinline__ uint32_t wave_slot() {
@@ -1328,7 +1341,7 @@ __device__ __forceinline__ void render_body(const KParams &P) {
         // older wave): refill and segment start 2, node steps 1, leaf batches 2, shading 0. A wave
         // that shades runs long divergent code; the others hold its successors' work and LDS
         // requests. Same-box against all-equal priorities: C2 +3.0 %, C4 +3.5 %, C5 +2.4 %.
-        __builtin_amdgcn_s_setprio(2);
+        __builtin_amdgcn_s_setprio(RRT_PRIO_REFILL);
         uint64_t idle = __ballot(!has);
         if (idle != 0 && pool_left == 0 && q_open) {
 #if RRT_XQ
@@ -1435,7 +1448,7 @@ __device__ __forceinline__ void render_body(const KParams &P) {
             // node visits) until the wave runs its leaf loop, which happens once more than
             // leaf_min lanes wait, or no lane can take another node step, or before leaving.
             const uint32_t leaf_min = (live * P.leaf_frac) >> 8;
-            __builtin_amdgcn_s_setprio(1);  // the node steps (phase priorities: see the loop head)
+            __builtin_amdgcn_s_setprio(RRT_PRIO_NODE);  // the node steps (phase priorities: see the loop head)
             Leaves lv = 0;  // the postponed leaf range (0 = none: a range has count >= 1)
             for (;;) {
                 if constexpr (RRT_PHASE_TIMING == 2) {
@@ -1453,17 +1466,17 @@ __device__ __forceinline__ void render_body(const KParams &P) {
                 const bool leave = (uint32_t)__popcll(tm) <= min_active;
                 const bool batch = ((uint32_t)__popcll(pm) > leaf_min) | leave | (tm == pm);
                 if ((pm != 0) & batch) {
-                    __builtin_amdgcn_s_setprio(2);
+                    __builtin_amdgcn_s_setprio(RRT_PRIO_LEAF);
                     if (lv != 0) {
                         trav_leaves<kCount>(pr, lv, ps.o, ps.d, rk, ps.skip, tr, cnt);
                         lv = 0;
                     }
-                    __builtin_amdgcn_s_setprio(1);
+                    __builtin_amdgcn_s_setprio(RRT_PRIO_NODE);
                 }
                 if (leave) break;
             }
         }
-        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_s_setprio(RRT_PRIO_SHADE);
         if constexpr (RRT_PHASE_TIMING == 1) {
             const uint64_t t = __builtin_amdgcn_s_memtime();
             ph1 += t - tp;
