@@ -51,6 +51,9 @@ namespace {
 #ifndef RRT_XQ
 #define RRT_XQ 1
 #endif
+#ifndef RRT_RUV_PAIR
+#define RRT_RUV_PAIR 0
+#endif
 // Wave issue priority per loop phase (s_setprio levels 0-3; see the work loop's head).
 #ifndef RRT_PRIO_REFILL
 #define RRT_PRIO_REFILL 2
@@ -145,6 +148,37 @@ __device__ __forceinline__ float rnd_pm1(RngState &s) {
 template <typename C>
 __device__ __forceinline__ V3 random_unit_vector(RngState &s, C &cnt) {
     float px, py, pz, lensq;
+#if RRT_RUV_PAIR
+    // two candidates per iteration; the stream is rewound to just after the first when it is
+    // accepted, so the draws consumed are the same as one candidate per iteration
+#if RRT_RUV_PAIR == 2
+    px = rnd_pm1(s);  // (2: one candidate first, then pairs)
+    py = rnd_pm1(s);
+    pz = rnd_pm1(s);
+    lensq = __builtin_fmaf(pz, pz, __builtin_fmaf(py, py, px * px));
+    if (!(0.0f < lensq && lensq <= 1.0f))
+#endif
+    for (;;) {
+        px = rnd_pm1(s);
+        py = rnd_pm1(s);
+        pz = rnd_pm1(s);
+        lensq = __builtin_fmaf(pz, pz, __builtin_fmaf(py, py, px * px));
+        const RngState s1 = s;
+        const float qx = rnd_pm1(s), qy = rnd_pm1(s), qz = rnd_pm1(s);
+        const float l2 = __builtin_fmaf(qz, qz, __builtin_fmaf(qy, qy, qx * qx));
+        if (0.0f < lensq && lensq <= 1.0f) {
+            s = s1;
+            break;
+        }
+        if (0.0f < l2 && l2 <= 1.0f) {
+            px = qx;
+            py = qy;
+            pz = qz;
+            lensq = l2;
+            break;
+        }
+    }
+#else
     for (;;) {
         if constexpr (RRT_PHASE_TIMING == 4) cnt.d2 += wave_slot();
         px = rnd_pm1(s);
@@ -153,6 +187,7 @@ __device__ __forceinline__ V3 random_unit_vector(RngState &s, C &cnt) {
         lensq = __builtin_fmaf(pz, pz, __builtin_fmaf(py, py, px * px));
         if (0.0f < lensq && lensq <= 1.0f) break;
     }
+#endif
     const float inv = 1.0f / __builtin_sqrtf(lensq);
     return v3(px * inv, py * inv, pz * inv);
 }
