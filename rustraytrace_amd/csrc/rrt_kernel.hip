@@ -351,7 +351,11 @@ __device__ __forceinline__ float div_by_a(float n, const RayK &rk) {
 // center at the ray's time, center1 + time * (center2 - center1) (the_next_week/sphere.rs:44:
 // Ray::at; static book-2 spheres carry a zero motion).
 // kBook2: 0 = book-1 scenes, 1 = book 2 (motion, procedural textures), 2 = book 2 with quads,
-// 3 = book 2 with quads and media, 4 = book 3 (all of book 2 + the MIS integrator)
+// 3 = book 2 with quads and media, 4 = book 3 (all of book 2 + the MIS integrator);
+// kBook1Untextured (-1) = book-1 scenes without an image-textured material: the texture path
+// (acos, atan2, the texel fetch) is compiled out. It is dead code at run time in such scenes, but
+// it costs registers: the C2 kernel spills 19 SGPRs instead of 33 without it, C2 +1.0 % same-box.
+constexpr int kBook1Untextured = -1;
 template <int kBook2>
 struct Prims {
     const float4 *cr;
@@ -366,10 +370,10 @@ struct Prims {
     static constexpr bool kHasMedia = kBook2 >= 3;
     // Book-1 scenes store r * r (f32, rounded as the test would round it) in the record's w and
     // the radius in the material record's b.w (rrt_host.cpp): one multiply less per sphere test.
-    static constexpr bool kR2 = kBook2 == 0;
+    static constexpr bool kR2 = kBook2 <= 0;
     __device__ __forceinline__ float4 at(int i) const {
         float4 c = cr[i];
-        if constexpr (kBook2) {
+        if constexpr (kBook2 > 0) {
             const float4 m = mo[i];
             c.x = c.x + time * m.x;
             c.y = c.y + time * m.y;
@@ -1019,20 +1023,20 @@ __device__ __forceinline__ bool shade(const KParams &P, const PR &prims, const G
     // rejection loop for both kinds (a wave mixing them runs it once, not twice).
     V3 r = v3(0.0f, 0.0f, 0.0f);
     if (kind != 2) r = random_unit_vector(ps.rng, cnt);
-    if (kBook2 && kind == 7) {  // Isotropic (material.rs:153-158): a fresh random_unit_vector
+    if (kBook2 > 0 && kind == 7) {  // Isotropic (material.rs:153-158): a fresh random_unit_vector
         dir = r;
         att = v3(m.a.x, m.a.y, m.a.z);
     } else if (kind != 1 && kind != 2) {  // Lambertian, plain or textured (material.rs:28-40; book 2 :41-53)
         dir = add(nrm, r);
         if (__builtin_fabsf(dir.x) < 1e-8f && __builtin_fabsf(dir.y) < 1e-8f && __builtin_fabsf(dir.z) < 1e-8f) dir = nrm;
-        if (kind == 3) {  // ImageTexture at the sphere's (u, v) (sphere.rs:46-52)
+        if (kBook2 != kBook1Untextured && kind == 3) {  // ImageTexture at the sphere's (u, v) (sphere.rs:46-52)
             const float theta = rrt_acosf(-outward.y);
             const float phi = rrt_atan2f(-outward.z, outward.x) + kPi;
             att = texel(P, m.b.z, phi / (2.0f * kPi), theta / kPi);
-        } else if (kBook2 && kind == 5) {  // CheckerTexture at p
+        } else if (kBook2 > 0 && kind == 5) {  // CheckerTexture at p
             att = checker_even(m.a.w, p) ? v3(m.a.x, m.a.y, m.a.z)
                                          : v3(__int_as_float(m.b.y), __int_as_float(m.b.z), __int_as_float(m.b.w));
-        } else if (kBook2 && kind == 6) {  // NoiseTexture at p
+        } else if (kBook2 > 0 && kind == 6) {  // NoiseTexture at p
             const float g = noise_value(prims.perlin + m.b.z, m.a.w, p);
             att = v3(g, g, g);
         } else {
@@ -1315,7 +1319,7 @@ __device__ __forceinline__ void render_body(const KParams &P) {
         const uint4 *src_m = reinterpret_cast<const uint4 *>(P.prim_mtl);
         const uint32_t nm = P.n_prims * (uint32_t)(sizeof(GMaterial) / 16);
         for (uint32_t i = threadIdx.x; i < nm; i += kBlock) dst[nn + P.n_prims + i] = src_m[i];
-        if constexpr (kBook2) {
+        if constexpr (kBook2 > 0) {
             const uint4 *src_v = reinterpret_cast<const uint4 *>(P.prim_motion);
             for (uint32_t i = threadIdx.x; i < P.n_prims; i += kBlock) dst[nn + P.n_prims + nm + i] = src_v[i];
         }
@@ -1323,13 +1327,13 @@ __device__ __forceinline__ void render_body(const KParams &P) {
         nodes = reinterpret_cast<const Node *>(dst);
         prims = reinterpret_cast<const float4 *>(dst + nn);
         mtl = reinterpret_cast<const GMaterial *>(dst + nn + P.n_prims);
-        if constexpr (kBook2) motion = reinterpret_cast<const float4 *>(dst + nn + P.n_prims + nm);
+        if constexpr (kBook2 > 0) motion = reinterpret_cast<const float4 *>(dst + nn + P.n_prims + nm);
     }
     // Perlin tables (5 KB each) staged in LDS after the scene: a noise texture value reads 56
     // lattice corners, each a permutation lookup then a dependent gradient load, so from L2 its
     // 7 octaves are a chain of ~100 round trips.
     const GPerlin *perlin = P.perlin;
-    if constexpr (kBook2 != 0) {
+    if constexpr (kBook2 > 0) {
         if (P.perlin_in_lds) {
             size_t off16 = (P.stack_depth * kBlock * sizeof(StackT) + 15u) / 16u;
             if constexpr (kLds) off16 += P.n_nodes * (uint32_t)(sizeof(Node) / 16) + 3u * P.n_prims + P.n_prims;
@@ -1671,8 +1675,8 @@ hipError_t launch_variant(const KParams &p, bool count, hipStream_t stream) {
     size_t lds = ((size_t)p.stack_depth * kBlock * sizeof(StackT) + 15u) / 16u * 16u;
     if (kLds)
         lds += (size_t)p.n_nodes * (kWide ? sizeof(GNode4) : sizeof(GNode)) +  // LDS BVH2 = GNode
-               (size_t)p.n_prims * (kPrimBytes + (kBook2 ? kMotionBytes : 0));
-    if (kBook2 && p.perlin_in_lds) lds += (size_t)p.n_perlin * sizeof(GPerlin);
+               (size_t)p.n_prims * (kPrimBytes + (kBook2 > 0 ? kMotionBytes : 0));
+    if (kBook2 > 0 && p.perlin_in_lds) lds += (size_t)p.n_perlin * sizeof(GPerlin);
     auto kernel = count ? rrt_render<kLds, true, StackT, kWide, kWaves, kBook2>
                         : rrt_render<kLds, false, StackT, kWide, kWaves, kBook2>;
     // Persistent grid: as many blocks as can be resident (occupancy at this LDS size), capped
@@ -1699,7 +1703,7 @@ template <bool kWide, int kBook2>
 hipError_t launch_width(const KParams &p, bool count, hipStream_t stream) {
     if (p.stack_depth > (uint32_t)kMaxStackDepth) return hipErrorInvalidValue;
     if (p.n_nodes > 65535u) return launch_variant<false, uint32_t, kWide, kBook2>(p, count, stream);
-    if constexpr (kBook2 != 0) {
+    if constexpr (kBook2 > 0) {
         // Book-2 variants (motion, textures, quads) need ~105 VGPRs: bounded to the 80 of 6
         // waves/SIMD they spill 17-22 dwords and run 3-14% slower than unbounded (4 waves/SIMD);
         // a 5-wave bound (96 VGPRs, 1-3 spills) measured 0-8% slower too.
@@ -1728,7 +1732,11 @@ hipError_t launch_render_pass(const KParams &p, bool count, hipStream_t stream) 
         if (p.n_media) return launch_width<false, 3>(p, count, stream);
         return p.n_quads ? launch_width<false, 2>(p, count, stream) : launch_width<false, 1>(p, count, stream);
     }
-    return p.bvh_width == 4 ? launch_width<true, 0>(p, count, stream) : launch_width<false, 0>(p, count, stream);
+    if (p.bvh_width == 4) return launch_width<true, 0>(p, count, stream);
+    // Scenes staged in LDS without image textures run the kernel with the texture path compiled
+    // out (C2 +1.0 %); for scenes read from L2 it measured −0.4 % on C5, so they keep class 0.
+    if (!p.image_tex && p.scene_in_lds) return launch_width<false, kBook1Untextured>(p, count, stream);
+    return launch_width<false, 0>(p, count, stream);
 }
 
 // One launch (+ combine) per sample pass of at most p.pass_chunks chunks, in chunk order.
