@@ -788,8 +788,27 @@ __device__ __forceinline__ int exit_skip(bool is_quad, bool is_medium, bool fron
 }
 
 // Camera::get_ray (camera.rs:152-180) for global pixel (x, y) and the path's RNG.
+#ifndef RRT_KARG_CAM
+#define RRT_KARG_CAM 1
+#endif
+// The camera block re-read from the kernarg segment at each use (scalar loads through the scalar
+// cache) rather than 19 values the compiler would hold in SGPRs across the whole work loop: the
+// asm makes the pointer opaque, so the loads cannot be hoisted out of the loop.
+__device__ __forceinline__ const __attribute__((address_space(4))) KParams *kernarg_params() {
+    auto q = (const __attribute__((address_space(4))) KParams *)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(q));
+    return q;
+}
+// a FastDiv member read through either view of the parameters
+template <class FD>
+__device__ __forceinline__ FastDiv fdiv(const FD &f) { return FastDiv{f.m, f.s}; }
 template <bool kStrat>
 __device__ __forceinline__ void camera_ray(const KParams &P, uint32_t x, uint32_t y, uint32_t s, PathState &ps) {
+#if RRT_KARG_CAM
+    const auto &C = *kernarg_params();
+#else
+    const KParams &C = P;
+#endif
     float ox, oy;
     if constexpr (kStrat) {  // sample_square_stratified (the_rest_of_your_life/camera.rs:173-177)
         const uint32_t sj = fast_div(s, P.fd_sqrt_spp), si = s - sj * P.sqrt_spp;
@@ -802,23 +821,23 @@ __device__ __forceinline__ void camera_ray(const KParams &P, uint32_t x, uint32_
     }
     const float fi = (float)x + ox;
     const float fj = (float)y + oy;
-    const V3 sample = v3(P.p00[0] + P.du[0] * fi + P.dv[0] * fj,
-                         P.p00[1] + P.du[1] * fi + P.dv[1] * fj,
-                         P.p00[2] + P.du[2] * fi + P.dv[2] * fj);
-    V3 origin = v3(P.center[0], P.center[1], P.center[2]);
-    if (P.defocus_radius > 0.0f) {
+    const V3 sample = v3(C.p00[0] + C.du[0] * fi + C.dv[0] * fj,
+                         C.p00[1] + C.du[1] * fi + C.dv[1] * fj,
+                         C.p00[2] + C.du[2] * fi + C.dv[2] * fj);
+    V3 origin = v3(C.center[0], C.center[1], C.center[2]);
+    if (C.defocus_radius > 0.0f) {
         float px, py;
         for (;;) {  // vec3.rs:172-179 random_in_unit_disk
             px = rnd_pm1(ps.rng);
             py = rnd_pm1(ps.rng);
             if (__builtin_fmaf(py, py, px * px) < 1.0f) break;
         }
-        origin = v3(P.center[0] + P.disk_u[0] * px + P.disk_v[0] * py,
-                    P.center[1] + P.disk_u[1] * px + P.disk_v[1] * py,
-                    P.center[2] + P.disk_u[2] * px + P.disk_v[2] * py);
+        origin = v3(C.center[0] + C.disk_u[0] * px + C.disk_v[0] * py,
+                    C.center[1] + C.disk_u[1] * px + C.disk_v[1] * py,
+                    C.center[2] + C.disk_u[2] * px + C.disk_v[2] * py);
     }
     ps.time = 0.0f;
-    if (P.flags & 0x1u) ps.time = rnd(ps.rng);  // RRT_FLAG_RAY_TIME (the_next_week/camera.rs:160)
+    if (C.flags & 0x1u) ps.time = rnd(ps.rng);  // RRT_FLAG_RAY_TIME (the_next_week/camera.rs:160)
     ps.skip = -1;
     ps.o = origin;
     ps.d = sub(sample, origin);
@@ -829,7 +848,8 @@ __device__ __forceinline__ void camera_ray(const KParams &P, uint32_t x, uint32_
 // The path's RNG stream for sample s of global pixel (x, y): xoshiro128+ state
 // (z, key | 1 << 32) with key = splitmix64((seed << 32) ^ pixel) and z = splitmix64(key + s).
 // The key is computed once per work unit (pixel, sample chunk) and held (+0.6 % on C2).
-__device__ __forceinline__ uint64_t pixel_key(const KParams &P, uint32_t x, uint32_t y) {
+template <class KP>
+__device__ __forceinline__ uint64_t pixel_key(const KP &P, uint32_t x, uint32_t y) {
     return splitmix64(((uint64_t)P.seed << 32) ^ (uint64_t)(y * P.width + x));
 }
 __device__ __forceinline__ RngState path_rng_k(uint64_t key, uint32_t s) { return rng_seed(splitmix64(key + s), key); }
@@ -1287,7 +1307,8 @@ __device__ __forceinline__ bool shade_b3(const KParams &P, const PR &prims, cons
 }
 
 // First sample (relative to sample_begin) of chunk c of a pixel (rrt_accum_chunk's schedule).
-__device__ __forceinline__ uint32_t chunk_first(const KParams &P, uint32_t c) {
+template <class KP>
+__device__ __forceinline__ uint32_t chunk_first(const KP &P, uint32_t c) {
     return c < P.n_big ? c * P.chunk : P.n_big * P.chunk + (c - P.n_big) * P.chunk_small;
 }
 
@@ -1413,30 +1434,35 @@ __device__ __forceinline__ void render_body(const KParams &P) {
             if (!has && r < n) {
                 const uint32_t u = pool_base + r;
                 {
+#if RRT_KARG_CAM
+                    const auto &Q = *kernarg_params();
+#else
+                    const KParams &Q = P;
+#endif
                     const uint32_t lit = u & 63u;
                     const uint32_t tc = u >> 6;
                     // big chunks of every tile first, then the tail chunks (small units last)
                     uint32_t t, chunk;
-                    if (u < P.n_big_units) {
-                        t = fast_div(tc, P.fd_pass_big);
-                        chunk = P.chunk_begin + (tc - t * P.pass_big);
+                    if (u < Q.n_big_units) {
+                        t = fast_div(tc, fdiv(Q.fd_pass_big));
+                        chunk = Q.chunk_begin + (tc - t * Q.pass_big);
                     } else {
-                        const uint32_t ns = P.pass_n - P.pass_big, tc2 = tc - (P.n_big_units >> 6);
-                        t = fast_div(tc2, P.fd_pass_tail);
-                        chunk = P.chunk_begin + P.pass_big + (tc2 - t * ns);
+                        const uint32_t ns = Q.pass_n - Q.pass_big, tc2 = tc - (Q.n_big_units >> 6);
+                        t = fast_div(tc2, fdiv(Q.fd_pass_tail));
+                        chunk = Q.chunk_begin + Q.pass_big + (tc2 - t * ns);
                     }
-                    const uint32_t ty = fast_div(t, P.fd_tiles_x);
-                    const uint32_t x = (t - ty * P.tiles_x) * 8u + (lit & 7u);
+                    const uint32_t ty = fast_div(t, fdiv(Q.fd_tiles_x));
+                    const uint32_t x = (t - ty * Q.tiles_x) * 8u + (lit & 7u);
                     const uint32_t ly = ty * 8u + (lit >> 3);
-                    if (x < P.width && ly < P.tile_rows) {
+                    if (x < Q.width && ly < Q.tile_rows) {
                         // tile-local row -> global image row (row bands dealt round-robin over ranks)
-                        const uint32_t band = fast_div(ly, P.fd_band_rows);
-                        const uint32_t y = (band * P.n_ranks + P.rank) * P.band_rows + (ly - band * P.band_rows);
+                        const uint32_t band = fast_div(ly, fdiv(Q.fd_band_rows));
+                        const uint32_t y = (band * Q.n_ranks + Q.rank) * Q.band_rows + (ly - band * Q.band_rows);
                         xy = x | (y << 16);
-                        s = P.sample_begin + chunk_first(P, chunk);
-                        s_hi = min(s + (chunk < P.n_big ? P.chunk : P.chunk_small), P.sample_end);
+                        s = Q.sample_begin + chunk_first(Q, chunk);
+                        s_hi = min(s + (chunk < Q.n_big ? Q.chunk : Q.chunk_small), Q.sample_end);
                         sum = v3(0.0f, 0.0f, 0.0f);
-                        pkey = pixel_key(P, x, y);
+                        pkey = pixel_key(Q, x, y);
                         ps.rng = path_rng_k(pkey, s);
                         camera_ray<kBook2 == 4>(P, x, y, s, ps);
                         need_ray = 1;
@@ -1557,17 +1583,22 @@ __device__ __forceinline__ void render_body(const KParams &P) {
                 ps.rng = path_rng_k(pkey, s);
                 camera_ray<kBook2 == 4>(P, x, y, s, ps);
             } else {  // unit complete: the chunk's sum, in sample order
+#if RRT_KARG_CAM
+                const auto &Q = *kernarg_params();
+#else
+                const KParams &Q = P;
+#endif
                 // chunk index and tile-local row, re-derived from (y, s_hi) once per unit
-                const uint32_t rel = s_hi - 1u - P.sample_begin;
-                const uint32_t nbs = P.n_big * P.chunk;
+                const uint32_t rel = s_hi - 1u - Q.sample_begin;
+                const uint32_t nbs = Q.n_big * Q.chunk;
                 const uint32_t chunk =
-                    rel < nbs ? fast_div(rel, P.fd_chunk) : P.n_big + fast_div(rel - nbs, P.fd_chunk_small);
-                const uint32_t gb = fast_div(y, P.fd_band_rows);
-                const uint32_t ly = fast_div(gb - P.rank, P.fd_n_ranks) * P.band_rows + (y - gb * P.band_rows);
-                const size_t px = (size_t)ly * P.width + x;
-                const float4 out = make_float4(sum.x, sum.y, sum.z, (float)(s_hi - (P.sample_begin + chunk_first(P, chunk))));
-                if (P.n_chunks == 1) P.accum[px] = out;
-                else P.partial[(size_t)(chunk - P.chunk_begin) * ((size_t)P.tile_rows * P.width) + px] = out;
+                    rel < nbs ? fast_div(rel, fdiv(Q.fd_chunk)) : Q.n_big + fast_div(rel - nbs, fdiv(Q.fd_chunk_small));
+                const uint32_t gb = fast_div(y, fdiv(Q.fd_band_rows));
+                const uint32_t ly = fast_div(gb - Q.rank, fdiv(Q.fd_n_ranks)) * Q.band_rows + (y - gb * Q.band_rows);
+                const size_t px = (size_t)ly * Q.width + x;
+                const float4 out = make_float4(sum.x, sum.y, sum.z, (float)(s_hi - (Q.sample_begin + chunk_first(Q, chunk))));
+                if (Q.n_chunks == 1) Q.accum[px] = out;
+                else Q.partial[(size_t)(chunk - Q.chunk_begin) * ((size_t)Q.tile_rows * Q.width) + px] = out;
                 has = 0;
             }
         }
