@@ -1189,7 +1189,7 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
         p.n_cus = (uint32_t)cus;
     }
     if (const char *e = std::getenv("RRT_MIN_WAVES")) p.min_waves = (uint32_t)std::atoi(e);
-    p.global_waves = 6;
+    p.global_waves = 7;  // L2 scenes: 256 x 7 (rrt_kernel.hip launch_width); 6 = 512 x 6, < 6 no bound
     if (const char *e = std::getenv("RRT_GLOBAL_WAVES")) p.global_waves = (uint32_t)std::atoi(e);
     if (const char *e = std::getenv("RRT_TRAV_FRAC")) p.trav_frac = (uint32_t)std::min(256, std::max(0, std::atoi(e)));
     if (const char *e = std::getenv("RRT_LEAF_FRAC")) p.leaf_frac = (uint32_t)std::min(256, std::max(0, std::atoi(e)));

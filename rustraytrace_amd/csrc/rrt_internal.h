@@ -213,6 +213,8 @@ constexpr uint32_t kQueues = 8;  // work-queue counters (blocks dealt round-robi
 #endif
 constexpr int kBlock = RRT_BLOCK;          // threads per block (4 or 8 waves)
 constexpr int kWavesPerSimd = RRT_WAVES;   // launch-bounds occupancy target of the main variant
+constexpr int kGlobalBlock = 256;         // book-1 kernels whose scene is read from L2: block size
+constexpr int kGlobalWaves = 7;           // and waves per SIMD (72 VGPRs)
 // Per-block LDS budget for staging the scene (BVH nodes + spheres + per-sphere materials)
 // next to the stack. RTOW: 13.5 KB nodes + 486 x 48 B = 36.9 KB; + ~11 KB of stack per
 // 512-thread block keeps 3 blocks (6 waves/SIMD) within the CU's 160 KB.

@@ -51,6 +51,15 @@ namespace {
 #ifndef RRT_XQ
 #define RRT_XQ 1
 #endif
+#ifndef RRT_B2_WAVES  // book-2 kernels (classes 1-3): launch bound (1 = none) and block size
+#define RRT_B2_WAVES 5
+#endif
+#ifndef RRT_B2_BLOCK
+#define RRT_B2_BLOCK 256
+#endif
+#ifndef RRT_UNTEX_L2
+#define RRT_UNTEX_L2 0
+#endif
 #ifndef RRT_RUV_PAIR
 #define RRT_RUV_PAIR 0
 #endif
@@ -587,7 +596,7 @@ __device__ __forceinline__ void test_range(const PR &prim_cr, int first, int cou
 
 // Traversal stack in LDS. 16-bit entries: the dword at (depth, wave, k) holds lanes k and
 // k+32, which the LDS serves in different cycles (2 x 32-lane groups), so no bank conflicts.
-template <typename StackT>
+template <typename StackT, int kBlk>
 struct LdsStack {
     StackT *base;
     __device__ __forceinline__ void init(StackT *lds, uint32_t tid) {
@@ -598,8 +607,8 @@ struct LdsStack {
             base = lds + tid;
         }
     }
-    __device__ __forceinline__ void store(int sp, int v) { base[sp * kBlock] = (StackT)v; }
-    __device__ __forceinline__ int load(int sp) const { return (int)base[sp * kBlock]; }
+    __device__ __forceinline__ void store(int sp, int v) { base[sp * kBlk] = (StackT)v; }
+    __device__ __forceinline__ int load(int sp) const { return (int)base[sp * kBlk]; }
 };
 
 // Resumable BVH traversal: one call = one node. The state lives in registers (+ the LDS stack)
@@ -1318,10 +1327,10 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
     return v;
 }
 
-template <bool kLds, bool kCount, typename StackT, bool kWide, int kBook2>
+template <bool kLds, bool kCount, typename StackT, bool kWide, int kBook2, int kBlk>
 __device__ __forceinline__ void render_body(const KParams &P) {
     extern __shared__ uint4 lds_dyn[];
-    // LDS layout: [traversal stack: stack_depth x kBlock x StackT, 16-B aligned][nodes][primitives]
+    // LDS layout: [traversal stack: stack_depth x kBlk x StackT, 16-B aligned][nodes][primitives]
     StackT *lds_stack = reinterpret_cast<StackT *>(lds_dyn);
     // BVH2 nodes: sign-ordered 80-B GNode when staged in LDS, 64-B GNodeG in global memory
     using Node = typename std::conditional<kWide, GNode4, typename std::conditional<kLds, GNode, GNodeG>::type>::type;
@@ -1331,18 +1340,18 @@ __device__ __forceinline__ void render_body(const KParams &P) {
     const float4 *motion = P.prim_motion;
     if constexpr (kLds) {
         // Stage the whole BVH + spheres + their materials (KB-sized) in LDS once per block.
-        uint4 *dst = lds_dyn + (P.stack_depth * kBlock * sizeof(StackT) + 15u) / 16u;
+        uint4 *dst = lds_dyn + (P.stack_depth * kBlk * sizeof(StackT) + 15u) / 16u;
         const uint4 *src_n = reinterpret_cast<const uint4 *>(P.nodes);
         const uint32_t nn = P.n_nodes * (uint32_t)(sizeof(Node) / 16);
-        for (uint32_t i = threadIdx.x; i < nn; i += kBlock) dst[i] = src_n[i];
+        for (uint32_t i = threadIdx.x; i < nn; i += kBlk) dst[i] = src_n[i];
         const uint4 *src_p = reinterpret_cast<const uint4 *>(P.prim_cr);
-        for (uint32_t i = threadIdx.x; i < P.n_prims; i += kBlock) dst[nn + i] = src_p[i];
+        for (uint32_t i = threadIdx.x; i < P.n_prims; i += kBlk) dst[nn + i] = src_p[i];
         const uint4 *src_m = reinterpret_cast<const uint4 *>(P.prim_mtl);
         const uint32_t nm = P.n_prims * (uint32_t)(sizeof(GMaterial) / 16);
-        for (uint32_t i = threadIdx.x; i < nm; i += kBlock) dst[nn + P.n_prims + i] = src_m[i];
+        for (uint32_t i = threadIdx.x; i < nm; i += kBlk) dst[nn + P.n_prims + i] = src_m[i];
         if constexpr (kBook2 > 0) {
             const uint4 *src_v = reinterpret_cast<const uint4 *>(P.prim_motion);
-            for (uint32_t i = threadIdx.x; i < P.n_prims; i += kBlock) dst[nn + P.n_prims + nm + i] = src_v[i];
+            for (uint32_t i = threadIdx.x; i < P.n_prims; i += kBlk) dst[nn + P.n_prims + nm + i] = src_v[i];
         }
         __syncthreads();
         nodes = reinterpret_cast<const Node *>(dst);
@@ -1356,17 +1365,17 @@ __device__ __forceinline__ void render_body(const KParams &P) {
     const GPerlin *perlin = P.perlin;
     if constexpr (kBook2 > 0) {
         if (P.perlin_in_lds) {
-            size_t off16 = (P.stack_depth * kBlock * sizeof(StackT) + 15u) / 16u;
+            size_t off16 = (P.stack_depth * kBlk * sizeof(StackT) + 15u) / 16u;
             if constexpr (kLds) off16 += P.n_nodes * (uint32_t)(sizeof(Node) / 16) + 3u * P.n_prims + P.n_prims;
             uint4 *dst = lds_dyn + off16;
             const uint4 *src = reinterpret_cast<const uint4 *>(P.perlin);
             const uint32_t n16 = P.n_perlin * (uint32_t)(sizeof(GPerlin) / 16);
-            for (uint32_t i = threadIdx.x; i < n16; i += kBlock) dst[i] = src[i];
+            for (uint32_t i = threadIdx.x; i < n16; i += kBlk) dst[i] = src[i];
             __syncthreads();
             perlin = reinterpret_cast<const GPerlin *>(dst);
         }
     }
-    LdsStack<StackT> stack;
+    LdsStack<StackT, kBlk> stack;
     stack.init(lds_stack, threadIdx.x);
 
     // Persistent waves over a global queue of work units. A unit is (pixel, chunk of
@@ -1636,9 +1645,9 @@ __device__ __forceinline__ void render_body(const KParams &P) {
     }
 }
 
-template <bool kLds, bool kCount, typename StackT, bool kWide, int kWaves, int kBook2>
-__global__ __launch_bounds__(kBlock, kWaves) void rrt_render(KParams P) {
-    render_body<kLds, kCount, StackT, kWide, kBook2>(P);
+template <bool kLds, bool kCount, typename StackT, bool kWide, int kWaves, int kBook2, int kBlk>
+__global__ __launch_bounds__(kBlk, kWaves) void rrt_render(KParams P) {
+    render_body<kLds, kCount, StackT, kWide, kBook2, kBlk>(P);
 }
 
 // The pass's chunk sums into accum, continuing the left fold over chunks in order: the first
@@ -1700,28 +1709,28 @@ __global__ __launch_bounds__(256) void rrt_quantize(const float4 *__restrict__ a
     }
 }
 
-template <bool kLds, typename StackT, bool kWide, int kBook2, int kWaves = 1>
+template <bool kLds, typename StackT, bool kWide, int kBook2, int kWaves = 1, int kBlk = kBlock>
 hipError_t launch_variant(const KParams &p, bool count, hipStream_t stream) {
     if (p.n_units == 0) return hipSuccess;
-    size_t lds = ((size_t)p.stack_depth * kBlock * sizeof(StackT) + 15u) / 16u * 16u;
+    size_t lds = ((size_t)p.stack_depth * kBlk * sizeof(StackT) + 15u) / 16u * 16u;
     if (kLds)
         lds += (size_t)p.n_nodes * (kWide ? sizeof(GNode4) : sizeof(GNode)) +  // LDS BVH2 = GNode
                (size_t)p.n_prims * (kPrimBytes + (kBook2 > 0 ? kMotionBytes : 0));
     if (kBook2 > 0 && p.perlin_in_lds) lds += (size_t)p.n_perlin * sizeof(GPerlin);
-    auto kernel = count ? rrt_render<kLds, true, StackT, kWide, kWaves, kBook2>
-                        : rrt_render<kLds, false, StackT, kWide, kWaves, kBook2>;
+    auto kernel = count ? rrt_render<kLds, true, StackT, kWide, kWaves, kBook2, kBlk>
+                        : rrt_render<kLds, false, StackT, kWide, kWaves, kBook2, kBlk>;
     // Persistent grid: as many blocks as can be resident (occupancy at this LDS size), capped
     // by the work; the queue counter is zeroed on the stream before the launch.
     int per_cu = 0;
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, lds);
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlk, lds);
     if (e != hipSuccess) return e;
     if (per_cu < 1) per_cu = 1;
-    const uint32_t want = (p.n_units + kBlock - 1) / kBlock;
+    const uint32_t want = (p.n_units + kBlk - 1) / kBlk;
     // at least kQueues blocks, so every work queue has a block (spare blocks find no work and exit)
     const uint32_t blocks = std::max<uint32_t>(std::min<uint32_t>(want, (uint32_t)per_cu * p.n_cus), RRT_XQ ? kQueues : 1u);
     e = hipMemsetAsync(p.unit_counter, 0, kQueues * 32u * sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(kernel, dim3(blocks), dim3(kBlock), lds, stream, p);
+    hipLaunchKernelGGL(kernel, dim3(blocks), dim3(kBlk), lds, stream, p);
     e = hipGetLastError();
     if (e != hipSuccess || p.n_chunks <= 1) return e;
     const uint32_t n_pixels = p.tile_rows * p.width;
@@ -1735,14 +1744,25 @@ hipError_t launch_width(const KParams &p, bool count, hipStream_t stream) {
     if (p.stack_depth > (uint32_t)kMaxStackDepth) return hipErrorInvalidValue;
     if (p.n_nodes > 65535u) return launch_variant<false, uint32_t, kWide, kBook2>(p, count, stream);
     if constexpr (kBook2 > 0) {
-        // Book-2 variants (motion, textures, quads) need ~105 VGPRs: bounded to the 80 of 6
-        // waves/SIMD they spill 17-22 dwords and run 3-14% slower than unbounded (4 waves/SIMD);
-        // a 5-wave bound (96 VGPRs, 1-3 spills) measured 0-8% slower too.
+        // Book-2 variants (motion, textures, quads) need ~105 VGPRs unbounded. In round 1, with
+        // 40-110 spilled SGPRs, a 6-wave bound cost 3-14 % and a 5-wave bound 0-8 %.
+        // Book 2 (classes 1-3): 256-thread blocks at 5 waves/SIMD (96 VGPRs). Measured on the
+        // 1/4-spp scene table against 512 threads unbounded (~105 VGPRs, 4 waves): +2 ... +16 %
+        // on every book-2 scene once the parameter spills were gone (256 x 4: +-1 %, 256 x 6:
+        // -21 ... +9 %). Book 3 (class 4, the light-list pdfs) keeps the unbounded 512: -8 % at 5.
+        if constexpr (kBook2 != 4 && RRT_B2_WAVES > 1)
+            return p.scene_in_lds ? launch_variant<true, uint16_t, kWide, kBook2, RRT_B2_WAVES, RRT_B2_BLOCK>(p, count, stream)
+                                  : launch_variant<false, uint16_t, kWide, kBook2, RRT_B2_WAVES, RRT_B2_BLOCK>(p, count, stream);
         return p.scene_in_lds ? launch_variant<true, uint16_t, kWide, kBook2>(p, count, stream)
                               : launch_variant<false, uint16_t, kWide, kBook2>(p, count, stream);
     } else {
         if (!kWide && p.scene_in_lds && p.min_waves >= 6)
             return launch_variant<true, uint16_t, kWide, kBook2, kWavesPerSimd>(p, count, stream);
+        // Scenes read from L2 (C5) hold only the stack in LDS: 256-thread blocks at 7 waves/SIMD
+        // (72 VGPRs), which 512-thread blocks cannot reach (3.5 blocks); C5 +2.8 % same-box over
+        // 512 x 6 (256 x 8, 64 VGPRs: -16 %, spills).
+        if (!kWide && !p.scene_in_lds && p.global_waves >= 7)
+            return launch_variant<false, uint16_t, kWide, kBook2, kGlobalWaves, kGlobalBlock>(p, count, stream);
         if (!kWide && !p.scene_in_lds && p.global_waves >= 6)
             return launch_variant<false, uint16_t, kWide, kBook2, kWavesPerSimd>(p, count, stream);
         return p.scene_in_lds ? launch_variant<true, uint16_t, kWide, kBook2>(p, count, stream)
@@ -1766,7 +1786,7 @@ hipError_t launch_render_pass(const KParams &p, bool count, hipStream_t stream) 
     if (p.bvh_width == 4) return launch_width<true, 0>(p, count, stream);
     // Scenes staged in LDS without image textures run the kernel with the texture path compiled
     // out (C2 +1.0 %); for scenes read from L2 it measured −0.4 % on C5, so they keep class 0.
-    if (!p.image_tex && p.scene_in_lds) return launch_width<false, kBook1Untextured>(p, count, stream);
+    if (!p.image_tex && (p.scene_in_lds || RRT_UNTEX_L2)) return launch_width<false, kBook1Untextured>(p, count, stream);
     return launch_width<false, 0>(p, count, stream);
 }
 
