@@ -1139,6 +1139,9 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
     p.sqrt_spp = sqrt_spp;
     p.image_tex = 0;
     for (uint32_t i = 0; i < n_materials; ++i) p.image_tex |= materials[i].kind == RRT_MAT_TEXTURED_LAMBERTIAN ? 1u : 0u;
+    p.specular = 0;
+    for (uint32_t i = 0; i < n_materials; ++i)
+        p.specular |= materials[i].kind == RRT_MAT_METAL || materials[i].kind == RRT_MAT_DIELECTRIC ? 1u : 0u;
     p.recip_sqrt_spp = sqrt_spp ? (float)(1.0 / (double)sqrt_spp) : 0.0f;  // camera.rs:117
     p.tex_pool = s->d_tex_pool;
     p.texs = s->d_texs;

@@ -167,6 +167,7 @@ struct KParams {
     uint32_t n_media;
     uint32_t n_lights;
     uint32_t image_tex;     // some material samples an image texture (book-1 kernels: texture path compiled in)
+    uint32_t specular;      // some material is metal or dielectric (book-1 kernels: those branches compiled in)
     uint32_t sqrt_spp;      // book 3: stratified camera samples (sqrt_spp^2 per pixel)
     float recip_sqrt_spp;   // 1/sqrt_spp in f64, rounded
     uint32_t stack_depth;   // entries needed (BVH depth + 1)

@@ -57,6 +57,9 @@ namespace {
 #ifndef RRT_B2_BLOCK
 #define RRT_B2_BLOCK 256
 #endif
+#ifndef RRT_DIFFUSE_CLASS
+#define RRT_DIFFUSE_CLASS 1
+#endif
 #ifndef RRT_UNTEX_L2
 #define RRT_UNTEX_L2 0
 #endif
@@ -365,6 +368,9 @@ __device__ __forceinline__ float div_by_a(float n, const RayK &rk) {
 // (acos, atan2, the texel fetch) is compiled out. It is dead code at run time in such scenes, but
 // it costs registers: the C2 kernel spills 19 SGPRs instead of 33 without it, C2 +1.0 % same-box.
 constexpr int kBook1Untextured = -1;
+// kBook1Diffuse (-2) = book-1 scenes whose materials are all Lambertian (plain or image-textured)
+// or emissive: the metal and dielectric branches are compiled out (C4, C1).
+constexpr int kBook1Diffuse = -2;
 template <int kBook2>
 struct Prims {
     const float4 *cr;
@@ -1051,11 +1057,11 @@ __device__ __forceinline__ bool shade(const KParams &P, const PR &prims, const G
     // Lambertian and Metal both draw one random_unit_vector and nothing else before RR: one
     // rejection loop for both kinds (a wave mixing them runs it once, not twice).
     V3 r = v3(0.0f, 0.0f, 0.0f);
-    if (kind != 2) r = random_unit_vector(ps.rng, cnt);
+    if (kBook2 == kBook1Diffuse || kind != 2) r = random_unit_vector(ps.rng, cnt);
     if (kBook2 > 0 && kind == 7) {  // Isotropic (material.rs:153-158): a fresh random_unit_vector
         dir = r;
         att = v3(m.a.x, m.a.y, m.a.z);
-    } else if (kind != 1 && kind != 2) {  // Lambertian, plain or textured (material.rs:28-40; book 2 :41-53)
+    } else if (kBook2 == kBook1Diffuse || (kind != 1 && kind != 2)) {  // Lambertian, plain or textured (material.rs:28-40; book 2 :41-53)
         dir = add(nrm, r);
         if (__builtin_fabsf(dir.x) < 1e-8f && __builtin_fabsf(dir.y) < 1e-8f && __builtin_fabsf(dir.z) < 1e-8f) dir = nrm;
         if (kBook2 != kBook1Untextured && kind == 3) {  // ImageTexture at the sphere's (u, v) (sphere.rs:46-52)
@@ -1786,6 +1792,7 @@ hipError_t launch_render_pass(const KParams &p, bool count, hipStream_t stream) 
     if (p.bvh_width == 4) return launch_width<true, 0>(p, count, stream);
     // Scenes staged in LDS without image textures run the kernel with the texture path compiled
     // out (C2 +1.0 %); for scenes read from L2 it measured −0.4 % on C5, so they keep class 0.
+    if (RRT_DIFFUSE_CLASS && !p.specular && p.scene_in_lds) return launch_width<false, kBook1Diffuse>(p, count, stream);
     if (!p.image_tex && (p.scene_in_lds || RRT_UNTEX_L2)) return launch_width<false, kBook1Untextured>(p, count, stream);
     return launch_width<false, 0>(p, count, stream);
 }
