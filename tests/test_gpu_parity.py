@@ -170,3 +170,35 @@ def test_zero_samples_tile():
     scene = rrt.rtow(image_width=16, samples_per_pixel=4, max_depth=4)
     gpu, idx, ctr, _ = gpu_tile(scene, s0=3, s1=3)
     assert np.all(gpu == 0) and ctr["rays"] == 0
+
+
+def _book1_scene(kinds, textured):
+    """A small book-1 scene with the given material kinds (0 Lambertian, 1 metal, 2 dielectric,
+    4 light), optionally with the earth texture on the big sphere; sky background, defocus on."""
+    from rustraytrace_amd import scenes as sc
+
+    mats = [sc._material(3 if textured else 0, (0.5, 0.5, 0.5), tex=0)]
+    sph = [sc._sphere((0.0, -1000.0, 0.0), 1000.0, 0), sc._sphere((0.0, 1.0, 0.0), 1.0, 0)]
+    for i, k in enumerate(kinds):
+        mats.append(sc._material(k, (0.7, 0.6, 0.5), fuzz=0.2, ref_idx=1.5))
+        sph.append(sc._sphere((-3.0 + 2.0 * i, 0.6, 1.5), 0.6, len(mats) - 1))
+    mats, sph = np.concatenate(mats), np.concatenate(sph)
+    cam = sc.make_camera(aspect_ratio=16.0 / 9.0, image_width=48, samples_per_pixel=4, max_depth=12, vfov=30.0,
+                         lookfrom=(6.0, 2.5, 8.0), lookat=(0.0, 0.5, 0.0), defocus_angle=0.6, focus_dist=9.0,
+                         seed=7, n_spheres=len(sph))
+    return sc.SceneData(cam, sph, mats, textures=[sc.earth_texture()] if textured else [], name="book1_classes")
+
+
+@pytest.mark.parametrize("in_lds", ["1", "0"])
+@pytest.mark.parametrize("kinds,textured", [((1, 2), True), ((0, 4), True), ((0, 4), False), ((1, 2), False)],
+                         ids=["tex+specular", "tex+diffuse", "diffuse", "specular"])
+def test_book1_kernel_classes_match_oracle(monkeypatch, kinds, textured, in_lds):
+    # The host picks the book-1 kernel by the materials present and by where the scene lives:
+    # textures and metal/dielectric compiled in or out (classes 0, -1, -2) on LDS scenes, the
+    # 256 x 7 launch for scenes read from L2 (RRT_SCENE_IN_LDS=0). Every combination is
+    # bit-exact against the oracle.
+    monkeypatch.setenv("RRT_SCENE_IN_LDS", in_lds)
+    scene = _book1_scene(kinds, textured)
+    gpu = rrt.render(scene)
+    ref, _, _ = oracle.render(scene, oracle.TWIN)
+    assert_bit_exact(gpu, ref, scene.spp)
