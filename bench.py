@@ -10,8 +10,8 @@ on the device by the kernel itself.
   the strong-scaling base of the N > 1 runs), the C1 CPU-path config timed on the CPU and the
   GPU (`c1`), the wall-clock split and the CPU baseline.
 * N > 1 (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): config C3,
-  3840x2160x2048 spp, tile-split the north star's way: 16-row bands dealt
-  round-robin (band b -> rank b mod N), every rank renders its bands over all samples, and the
+  3840x2160x2048 spp, tile-split the north star's way: row bands (15 rows at
+  2/4/8 ranks, so every rank owns 2160/N rows; `distributed.balanced_band`) dealt round-robin (band b -> rank b mod N), every rank renders its bands over all samples, and the
   float tiles are gathered to rank 0 over RCCL inside the timed step (`distributed.gather_rows`).
   Strong scaling: the frame is fixed, value = all ranks' rays / the max over ranks of the timed
   wall-clock. `--split samples` is the opt-in weak-scaling mode (every rank renders the whole
@@ -265,7 +265,7 @@ def main():
     import torch.distributed as dist
 
     import rustraytrace_amd as rrt
-    from rustraytrace_amd.distributed import band_rows, gather_rows, gather_sample_ranges
+    from rustraytrace_amd.distributed import balanced_band, band_rows, gather_rows, gather_sample_ranges
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -291,8 +291,10 @@ def main():
     scene = rrt.config_scene(config, **kw)
     W, H, S = scene.width, scene.height, scene.spp
     ds = rrt.DeviceScene(scene, device=device)
+    # bands of equal count per rank when the height allows it (C3: 15 rows at 2/4/8 ranks)
+    band = balanced_band(H, world) if (bands and world > 1) else BAND_ROWS
     if bands:
-        tile = ds.tile(band_rows=BAND_ROWS, rank=rank, n_ranks=world, sample_begin=0, sample_end=S)
+        tile = ds.tile(band_rows=band, rank=rank, n_ranks=world, sample_begin=0, sample_end=S)
         rows = ds.tile_rows(tile)
     else:
         tile = ds.tile(band_rows=BAND_ROWS, rank=0, n_ranks=1, sample_begin=rank * S, sample_end=(rank + 1) * S)
@@ -304,7 +306,7 @@ def main():
     def gather():  # the one exchange: tiles (bands) or partial accums (samples) -> rank 0
         src = accum[:rows] if backend == "nccl" else accum[:rows].cpu()
         if bands:
-            image[0] = gather_rows(src, H, BAND_ROWS, dist)
+            image[0] = gather_rows(src, H, band, dist)
         else:
             image[0] = gather_sample_ranges(src, dist)
 
@@ -363,7 +365,7 @@ def main():
         if rows == H:  # the PMC record is of a whole-frame launch
             traffic, traffic_src = load_traffic(traffic_json, config, W, S, rrt._lib.LIB_PATH)
         if bands:
-            split = (f"{BAND_ROWS}-row bands dealt round-robin over {world} rank(s), RCCL gather of the float tiles "
+            split = (f"{band}-row bands dealt round-robin over {world} rank(s), RCCL gather of the float tiles "
                      f"to rank 0 inside the timed step" if world > 1 else
                      "whole frame on 1 GPU (the band split with one rank), no gather")
         else:
@@ -426,7 +428,7 @@ def main():
             out["gather_ms"] = round(float(np.mean(gather_ms)), 3)
             out["gather_note"] = "rank 0, HIP events between the end of its render and the end of the gather"
             if bands:
-                out["rows_per_rank"] = [len(band_rows(H, BAND_ROWS, r, world)) for r in range(world)]
+                out["rows_per_rank"] = [len(band_rows(H, band, r, world)) for r in range(world)]
         if world == 1 and not args.no_breakdown:
             out["wall_clock_breakdown"] = wall_clock_breakdown(scene, accum, avg_kernel_s * 1e3)
         cpus = host_cpus()

@@ -30,6 +30,19 @@ def band_rows(height: int, band: int, rank: int, n_ranks: int) -> np.ndarray:
     return np.asarray(rows, dtype=np.int64)
 
 
+def balanced_band(height: int, n_ranks: int, max_band: int = 16, min_band: int = 8) -> int:
+    """Rows per band: the largest b in [min_band, max_band] with height % (b * n_ranks) == 0, so
+    every rank owns the same number of bands and rows; max_band when no such b exists.
+
+    C3 (2160 rows) at 16-row bands leaves 135 bands: at 2/4/8 ranks the busiest rank owns 0.74 %
+    more rows than the mean, and the frame waits for it. 15-row bands give 144 = 8 x 18. The image
+    does not depend on the band height (every pixel is keyed by its global index)."""
+    for b in range(max_band, min_band - 1, -1):
+        if height % (b * n_ranks) == 0:
+            return b
+    return max_band
+
+
 def sample_range(spp_per_rank: int, rank: int) -> tuple:
     return rank * spp_per_rank, (rank + 1) * spp_per_rank
 

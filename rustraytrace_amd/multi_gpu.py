@@ -30,7 +30,8 @@ def parse(argv=None):
     ap.add_argument("--width", type=int, default=None, help="image_width override")
     ap.add_argument("--spp", type=int, default=None, help="samples_per_pixel override")
     ap.add_argument("--depth", type=int, default=None, help="max_depth override")
-    ap.add_argument("--band", type=int, default=16, help="rows per band")
+    ap.add_argument("--band", type=int, default=0,
+                    help="rows per band (0: the largest of 16..8 that gives every rank the same rows, else 16)")
     ap.add_argument("--backend", default=None, help="nccl (RCCL, default with >1 rank) or gloo")
     ap.add_argument("--out", default=None, help="PPM path on rank 0 ('-' = stdout, default: none)")
     ap.add_argument("--p6", action="store_true", help="binary P6 instead of the reference's P3")
@@ -46,7 +47,7 @@ def main(argv=None) -> int:
 
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import rustraytrace_amd as rrt
-    from rustraytrace_amd.distributed import gather_rows
+    from rustraytrace_amd.distributed import balanced_band, gather_rows
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -76,6 +77,8 @@ def main(argv=None) -> int:
     W, H, S = scene.width, scene.height, scene.spp
 
     ds = rrt.DeviceScene(scene, device=device)
+    if args.band <= 0:
+        args.band = balanced_band(H, world)
     tile = ds.tile(band_rows=args.band, rank=rank, n_ranks=world, sample_begin=0, sample_end=S)
     rows = ds.tile_rows(tile)
     accum = torch.empty((max(rows, 1), W, 4), dtype=torch.float32, device=f"cuda:{device}")

@@ -25,13 +25,15 @@ def _free_port():
     return port
 
 
-@pytest.mark.parametrize("ranks,backend", [(1, "gloo"), (2, "gloo"), (3, "gloo"), (1, "nccl")])
-def test_row_bands_gathered_equal_one_gpu(tmp_path, ranks, backend):
+@pytest.mark.parametrize("ranks,backend,band", [(1, "gloo", 8), (2, "gloo", 8), (3, "gloo", 8), (1, "nccl", 8),
+                                                (2, "gloo", 0)])
+def test_row_bands_gathered_equal_one_gpu(tmp_path, ranks, backend, band):
+    # band 0: balanced_band picks the height (54 rows, 2 ranks: 9-row bands, 27 rows each).
     # (1, "nccl"): the RCCL process group and gather on the device tensors (RCCL refuses two
     # ranks on one GPU, so more ranks share the box's GPU over gloo).
     out = str(tmp_path / "accum.npy")
     ppm = str(tmp_path / "img.ppm")
-    args = ["--config", "C2", "--width", "96", "--spp", "8", "--depth", "20", "--band", "8",
+    args = ["--config", "C2", "--width", "96", "--spp", "8", "--depth", "20", "--band", str(band),
             "--backend", backend, "--save-accum", out, "--out", ppm]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ranks}",
            "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", "-m", "rustraytrace_amd.multi_gpu"] + args
@@ -73,5 +75,6 @@ def test_bench_band_split_line(ranks):
     if ranks > 1:
         assert "gather_ms" in line and "bands" in line["config"]["parallelism"]
         assert sum(line["rows_per_rank"]) == 144
+        assert line["rows_per_rank"] == [144 // ranks] * ranks  # balanced_band: 12-row bands
     else:
         assert "no gather" in line["config"]["parallelism"]
