@@ -3,8 +3,9 @@
 One process per GPU. The scene and BVH are replicated (KB-sized); the work is split one of two
 ways, with no data-path collective until the single final exchange:
 
-* rows    (strong scaling, C3): 16-row bands dealt round-robin over ranks (rank r owns bands
-          b with b % n == r), which balances cheap sky rows against expensive ground rows.
+* rows    (strong scaling, C3): row bands (`balanced_band`: 15 rows for C3 at 2/4/8 ranks)
+          dealt round-robin over ranks (rank r owns bands b with b % n == r), which balances
+          cheap sky rows against expensive ground rows.
           Rank 0 receives every rank's rows and places them — the image is bit-identical to a
           1-GPU render because every pixel is computed by the same lane program from the same
           (seed, pixel, sample) keys.

@@ -6,7 +6,7 @@ One process per GPU, launched by torch.distributed.run:
     python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
         --master-port 29500 -m rustraytrace_amd.multi_gpu --config C3 --out image.ppm
 
-Every rank builds the same scene and BVH (KB-sized, replicated), renders the 16-row bands it
+Every rank builds the same scene and BVH (KB-sized, replicated), renders the row bands it
 owns (band b goes to rank b mod n) over all samples, and the float tiles are gathered to rank 0
 (`distributed.gather_rows`), which writes the render_io.rs PPM. The image is bit-identical to a
 1-GPU render: each pixel's samples are keyed by (seed, global pixel, sample) only. Rank 0 prints
