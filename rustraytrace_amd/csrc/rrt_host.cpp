@@ -814,8 +814,8 @@ int fill_params(RrtScene *s, const RrtTile *t, float *d_accum, rrt::KParams &p) 
     p.n_ranks = t->n_ranks;
     p.sample_begin = t->sample_begin;
     p.sample_end = t->sample_end;
-    p.tiles_x = (p.width + 7u) / 8u;
-    p.n_work_tiles = p.tiles_x * ((p.tile_rows + 7u) / 8u);
+    p.tiles_x = (p.width + rrt::kTileW - 1u) / rrt::kTileW;
+    p.n_work_tiles = p.tiles_x * ((p.tile_rows + rrt::kTileH - 1u) / rrt::kTileH);
     const uint32_t S = t->sample_end - t->sample_begin;
     // the frame's chunk (rrt_accum_chunk): K when S > 2K, else K/2 — big chunks pay at high spp
     // (per-unit cost), small ones at low spp (drain granularity)

@@ -212,6 +212,11 @@ constexpr uint32_t kQueues = 8;  // work-queue counters (blocks dealt round-robi
 #ifndef RRT_WAVES
 #define RRT_WAVES 6
 #endif
+#ifndef RRT_TILE_W
+#define RRT_TILE_W 8
+#endif
+// work-unit tile: 64 consecutive unit ids = kTileW x kTileH pixels of one chunk
+constexpr uint32_t kTileW = RRT_TILE_W, kTileH = 64u / RRT_TILE_W;
 constexpr int kBlock = RRT_BLOCK;          // threads per block (4 or 8 waves)
 constexpr int kWavesPerSimd = RRT_WAVES;   // launch-bounds occupancy target of the main variant
 constexpr int kGlobalBlock = 256;         // book-1 kernels whose scene is read from L2: block size

@@ -1467,8 +1467,8 @@ __device__ __forceinline__ void render_body(const KParams &P) {
                         chunk = Q.chunk_begin + Q.pass_big + (tc2 - t * ns);
                     }
                     const uint32_t ty = fast_div(t, fdiv(Q.fd_tiles_x));
-                    const uint32_t x = (t - ty * Q.tiles_x) * 8u + (lit & 7u);
-                    const uint32_t ly = ty * 8u + (lit >> 3);
+                    const uint32_t x = (t - ty * Q.tiles_x) * kTileW + (lit % kTileW);
+                    const uint32_t ly = ty * kTileH + (lit / kTileW);
                     if (x < Q.width && ly < Q.tile_rows) {
                         // tile-local row -> global image row (row bands dealt round-robin over ranks)
                         const uint32_t band = fast_div(ly, fdiv(Q.fd_band_rows));
