@@ -384,7 +384,7 @@ typedef struct RrtBookScene {
 
 int32_t rrt_build_next_week_scene(int32_t scene, const RrtOverrides *ov, uint64_t seed, RrtBookScene *out);
 
-/* The book-3 scene (the_rest_of_your_life/mod.rs:69-164): the Cornell box with one rotated box
+/* The book-3 scene (the_rest_of_your_life/mod.rs:69-161): the Cornell box with one rotated box
  * and a glass sphere, the light list {the light quad, the glass sphere} for MIS. The camera's
  * samples_per_pixel is rounded down to sqrt_spp^2 (Camera::initialize, camera.rs:115-117).
  * Render with out->flags (RRT_FLAG_RAY_TIME | RRT_FLAG_BOOK3) and an RrtSceneExt over the arrays

@@ -15,12 +15,12 @@
 //   Camera::get_ray / sample_square / defocus_disk_sample     books/in_one_weekend/camera.rs:152-180
 //   Camera::ray_color (recursive, RR from bounce 5)           books/in_one_weekend/camera.rs:182-209
 //   book-2 ray_color (emission, background), time draw        books/the_next_week/camera.rs:148-201
-//   get_sphere_uv, ImageTexture::value, RtwImage::pixel_data  the_next_week/sphere.rs:46-52, texture.rs:177-196,
+//   get_sphere_uv, ImageTexture::value, RtwImage::pixel_data  the_next_week/sphere.rs:46-52, texture.rs:89-109,
 //                                                             rtw_image.rs:46-78
 //   DiffuseLight::emitted                                     the_next_week/material.rs:116-135
 //   Sphere::new_moving / hit at ray time                      the_next_week/sphere.rs:24-45
 //   CheckerTexture / NoiseTexture::value                      the_next_week/texture.rs:39-77, 111-126
-//   Perlin::noise / turb / perlin_interp                      the_next_week/perlin.rs:25-102
+//   Perlin::noise / turb / perlin_interp                      the_next_week/perlin.rs:25-98
 //   write_color (f64 quantiser)                               books/in_one_weekend/color.rs:6-32
 //   write_ppm_from_accum (f32 quantiser)                      render_io.rs:3-31
 //   build_in_one_weekend_scene (seeded SmallRng scene)        gpu/mod.rs:124-301
@@ -1050,7 +1050,7 @@ Vec3<T> texture_value(const World<T> &w, uint32_t tex, Vec3<T> outward) {
     T u = phi / (T(2) * t_pi<T>());
     T v = theta / t_pi<T>();
     const Texture &t = w.texs[tex];
-    if (t.height <= 0) return mk(T(0), T(1), T(1));  // texture.rs:179-181
+    if (t.height <= 0) return mk(T(0), T(1), T(1));  // texture.rs:91-93
     const Interval<T> unit{T(0), T(1)};
     u = unit.clamp(u);
     v = T(1) - unit.clamp(v);
@@ -1062,8 +1062,8 @@ Vec3<T> texture_value(const World<T> &w, uint32_t tex, Vec3<T> outward) {
     };
     int32_t i = to_i32(u * (T)t.width);
     int32_t j = to_i32(v * (T)t.height);
-    auto clampi = [](int32_t x, int32_t lo, int32_t hi) { return x < lo ? lo : (x < hi ? x : hi - 1); };  // rtw_image.rs:326-334
-    if (!t.data) return mk(T(1), T(0), T(1));  // rtw_image.rs:303-305
+    auto clampi = [](int32_t x, int32_t lo, int32_t hi) { return x < lo ? lo : (x < hi ? x : hi - 1); };  // rtw_image.rs:51-52, 70-78
+    if (!t.data) return mk(T(1), T(0), T(1));  // rtw_image.rs:47-49
     i = clampi(i, 0, t.width);
     j = clampi(j, 0, t.height);
     const uint8_t *px = t.data + ((size_t)j * t.width + i) * 3;
@@ -1107,7 +1107,7 @@ template <class T> int32_t floor_as_i32(T x) {  // `x.floor() as i32`: saturatin
     return (int32_t)f;
 }
 
-template <class T> T perlin_noise(const PerlinT<T> &pt, Vec3<T> p) {  // perlin.rs:25-48, 84-102
+template <class T> T perlin_noise(const PerlinT<T> &pt, Vec3<T> p) {  // perlin.rs:25-48, 79-98
     const T u = p.x() - std::floor(p.x());
     const T v = p.y() - std::floor(p.y());
     const T w = p.z() - std::floor(p.z());
@@ -1131,7 +1131,7 @@ template <class T> T perlin_noise(const PerlinT<T> &pt, Vec3<T> p) {  // perlin.
     return accum;
 }
 
-template <class T> T noise_value(const PerlinT<T> &pt, T scale, Vec3<T> p) {  // texture.rs:119-123, perlin.rs:50-62
+template <class T> T noise_value(const PerlinT<T> &pt, T scale, Vec3<T> p) {  // texture.rs:122-126, perlin.rs:50-62
     T accum = T(0), weight = T(1);
     Vec3<T> tp = p;
     for (int o = 0; o < 7; ++o) {

@@ -1172,7 +1172,10 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
     p.scene_in_lds = fb.width == 2 ? fb.stride == (uint32_t)sizeof(rrt::GNode)
                                    : scene_lds_fit(fb.bytes.size(), n_prims, book2);
     {  // Perlin tables in LDS when the block's LDS (stack + staged scene + tables) stays within 64 KB
-        const size_t stack = ((size_t)p.stack_depth * rrt::kBlock * (fb.n_nodes > 65535u ? 4u : 2u) + 15u) / 16u * 16u;
+        // the block that launches (book-2 classes 1-3: 256 threads; book 3: 512), as launch_variant sizes it
+        const bool wide = fb.n_nodes > 65535u;
+        const size_t threads = (size_t)rrt::render_block_threads(book2 && !book3, wide);
+        const size_t stack = ((size_t)p.stack_depth * threads * (wide ? 4u : 2u) + 15u) / 16u * 16u;
         const size_t scene = p.scene_in_lds ? fb.bytes.size() + (size_t)n_prims * (rrt::kPrimBytes + (book2 ? rrt::kMotionBytes : 0)) : 0;
         p.perlin_in_lds = book2 && n_perlin > 0 &&
                           stack + scene + (size_t)n_perlin * sizeof(rrt::GPerlin) <= 64u * 1024u ? 1u : 0u;
@@ -1449,8 +1452,14 @@ static int32_t render_frame(const RrtCamera *cam, const RrtSphere *spheres, uint
                 hipHostMalloc((void **)&heads, rrt::kQueues * 128u, 0) == hipSuccess) {
                 uint32_t pass = 0, last_sum = 0;
                 int shown = -1;
+                // the end of the render is noticed within ~1 ms (a 100-ms sleep rounded a one-shot
+                // call up to the next tick: an 89-ms C2 frame took >= 100 ms); the heads are read
+                // every 100 ms
+                auto next_read = std::chrono::steady_clock::now() + std::chrono::milliseconds(100);
                 while (hipEventQuery(ev) == hipErrorNotReady) {
-                    std::this_thread::sleep_for(std::chrono::milliseconds(100));
+                    std::this_thread::sleep_for(std::chrono::milliseconds(1));
+                    if (std::chrono::steady_clock::now() < next_read) continue;
+                    next_read += std::chrono::milliseconds(100);
                     const double f = render_progress(scene, side, heads, pass, last_sum);
                     if (f < 0.0) break;
                     std::lock_guard<std::mutex> lk(mu);

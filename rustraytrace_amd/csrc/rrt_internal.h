@@ -221,6 +221,21 @@ constexpr int kBlock = RRT_BLOCK;          // threads per block (4 or 8 waves)
 constexpr int kWavesPerSimd = RRT_WAVES;   // launch-bounds occupancy target of the main variant
 constexpr int kGlobalBlock = 256;         // book-1 kernels whose scene is read from L2: block size
 constexpr int kGlobalWaves = 7;           // and waves per SIMD (72 VGPRs)
+#ifndef RRT_B2_WAVES
+#define RRT_B2_WAVES 5
+#endif
+#ifndef RRT_B2_BLOCK
+#define RRT_B2_BLOCK 256
+#endif
+constexpr int kBook2Waves = RRT_B2_WAVES;  // book-2 kernels (classes 1-3): launch bound (1 = none)
+constexpr int kBook2Block = RRT_B2_BLOCK;  // and block size; book 3 and unbounded launches use kBlock
+// Threads per block of the render launch for a scene (rrt_kernel.hip launch_width): the host sizes
+// the block's LDS (traversal stack, Perlin tables) with it. book2_class: a book-2 scene rendered by
+// kernel classes 1-3 (not book 3); wide_stack: more than 65535 nodes (32-bit stack, kBlock).
+inline int render_block_threads(bool book2_class, bool wide_stack) {
+    if (wide_stack) return kBlock;
+    return book2_class && kBook2Waves > 1 ? kBook2Block : kBlock;
+}
 // Per-block LDS budget for staging the scene (BVH nodes + spheres + per-sphere materials)
 // next to the stack. RTOW: 13.5 KB nodes + 486 x 48 B = 36.9 KB; + ~11 KB of stack per
 // 512-thread block keeps 3 blocks (6 waves/SIMD) within the CU's 160 KB.

@@ -15,7 +15,7 @@
 //   scatter          material.rs:28-40 / 53-64 / 83-102, vec3.rs:181-189, 201-210
 //   Russian roulette camera.rs:189-200 (this bounce's attenuation, clamp [.05,.95])
 //   sky / background camera.rs:206-208 / the_next_week/camera.rs:179-181
-//   emission, texture the_next_week/material.rs:41-53,131-135, texture.rs:177-196, sphere.rs:46-52
+//   emission, texture the_next_week/material.rs:41-53,131-135, texture.rs:89-109, sphere.rs:46-52
 // in f32 with every operation in the reference's order (built with -ffp-contract=off and
 // correctly rounded f32 div/sqrt; the only fused multiply-adds are explicit: dot products and
 // sums of squares, the sphere discriminant h*h - a*c, Ray::at of the hit point, the slab test)
@@ -38,33 +38,6 @@ namespace {
 //   4: shade entries x 64 / shading lanes / rejection-loop wave-iterations x 64
 #ifndef RRT_PHASE_TIMING
 #define RRT_PHASE_TIMING 0
-#endif
-#ifndef RRT_TRIM
-#define RRT_TRIM 1
-#endif
-#ifndef RRT_LEAN
-#define RRT_LEAN 1
-#endif
-#ifndef RRT_HOISTDIV
-#define RRT_HOISTDIV 1
-#endif
-#ifndef RRT_XQ
-#define RRT_XQ 1
-#endif
-#ifndef RRT_B2_WAVES  // book-2 kernels (classes 1-3): launch bound (1 = none) and block size
-#define RRT_B2_WAVES 5
-#endif
-#ifndef RRT_B2_BLOCK
-#define RRT_B2_BLOCK 256
-#endif
-#ifndef RRT_DIFFUSE_CLASS
-#define RRT_DIFFUSE_CLASS 1
-#endif
-#ifndef RRT_UNTEX_L2
-#define RRT_UNTEX_L2 0
-#endif
-#ifndef RRT_RUV_PAIR
-#define RRT_RUV_PAIR 0
 #endif
 // Wave issue priority per loop phase (s_setprio levels 0-3; see the work loop's head).
 #ifndef RRT_PRIO_REFILL
@@ -160,37 +133,6 @@ __device__ __forceinline__ float rnd_pm1(RngState &s) {
 template <typename C>
 __device__ __forceinline__ V3 random_unit_vector(RngState &s, C &cnt) {
     float px, py, pz, lensq;
-#if RRT_RUV_PAIR
-    // two candidates per iteration; the stream is rewound to just after the first when it is
-    // accepted, so the draws consumed are the same as one candidate per iteration
-#if RRT_RUV_PAIR == 2
-    px = rnd_pm1(s);  // (2: one candidate first, then pairs)
-    py = rnd_pm1(s);
-    pz = rnd_pm1(s);
-    lensq = __builtin_fmaf(pz, pz, __builtin_fmaf(py, py, px * px));
-    if (!(0.0f < lensq && lensq <= 1.0f))
-#endif
-    for (;;) {
-        px = rnd_pm1(s);
-        py = rnd_pm1(s);
-        pz = rnd_pm1(s);
-        lensq = __builtin_fmaf(pz, pz, __builtin_fmaf(py, py, px * px));
-        const RngState s1 = s;
-        const float qx = rnd_pm1(s), qy = rnd_pm1(s), qz = rnd_pm1(s);
-        const float l2 = __builtin_fmaf(qz, qz, __builtin_fmaf(qy, qy, qx * qx));
-        if (0.0f < lensq && lensq <= 1.0f) {
-            s = s1;
-            break;
-        }
-        if (0.0f < l2 && l2 <= 1.0f) {
-            px = qx;
-            py = qy;
-            pz = qz;
-            lensq = l2;
-            break;
-        }
-    }
-#else
     for (;;) {
         if constexpr (RRT_PHASE_TIMING == 4) cnt.d2 += wave_slot();
         px = rnd_pm1(s);
@@ -199,7 +141,6 @@ __device__ __forceinline__ V3 random_unit_vector(RngState &s, C &cnt) {
         lensq = __builtin_fmaf(pz, pz, __builtin_fmaf(py, py, px * px));
         if (0.0f < lensq && lensq <= 1.0f) break;
     }
-#endif
     const float inv = 1.0f / __builtin_sqrtf(lensq);
     return v3(px * inv, py * inv, pz * inv);
 }
@@ -525,23 +466,21 @@ __device__ __forceinline__ void test_prims(const PR &prim_cr, int first, int cou
 
 // Leaf primitives [first, first + count): the hit leaf children of one node visit, which are
 // adjacent in primitive order (sibling leaves split one range, rrt_host.cpp flatten2).
-// `skip` is the primitive the ray is leaving (exit_skip): tested and counted, never accepted.
-// The skip primitive is left out of the loop (it can never be accepted), so a lane whose range
-// holds it runs one iteration less. kFastDiv: every active lane's |d|^2 is in the range of the
-// per-ray reciprocal (the caller checked it wave-wide), so the root divisions take no branch.
+// `skip` is the primitive the ray is leaving (exit_skip): it can never be accepted, so it is left
+// out of the loop — a lane whose range holds it runs one iteration less — but the counting
+// variant still counts it as a test, like the oracle's hit_prim (tests count every primitive of
+// the range). kFastDiv: every active lane's |d|^2 is in the range of the per-ray reciprocal (the
+// caller checked it wave-wide), so the root divisions take no branch.
 template <bool kCount, bool kFastDiv, class PR>
 __device__ __forceinline__ void test_range(const PR &prim_cr, int first, int count, V3 o, V3 d, const RayK &rk,
                                            int skip, float &closest, int &hit_prim, Counters &cnt) {
     const float a = rk.a;
-#if RRT_TRIM
     const bool trim = (uint32_t)(skip - first) < (uint32_t)count;
     const int n = count - (trim ? 1 : 0);
     const int gap = trim ? skip : 0x7fffffff;
+    if (kCount && trim) cnt.spheres++;
     for (int k = 0; k < n; ++k) {
         const int i = first + k + (first + k >= gap ? 1 : 0);
-#else
-    for (int i = first; i < first + count; ++i) {
-#endif
         if (kCount) cnt.spheres++;
         if constexpr (RRT_PHASE_TIMING == 3) {
             cnt.d0 += wave_slot();
@@ -555,7 +494,7 @@ __device__ __forceinline__ void test_range(const PR &prim_cr, int first, int cou
                 bool hit;
                 if (PR::kHasMedia && j >= (int)prim_cr.n_quads) hit = medium_hit(prim_cr, j - (int)prim_cr.n_quads, o, d, rk, closest, tq);
                 else hit = quad_hit(prim_cr.qd[j], o, d, 0.001f, closest, tq);
-                if (hit && (RRT_TRIM || i != skip)) {
+                if (hit) {
                     closest = tq;
                     hit_prim = i;
                 }
@@ -566,7 +505,6 @@ __device__ __forceinline__ void test_range(const PR &prim_cr, int first, int cou
         const float h = dot(d, oc);
         const float c = dot(oc, oc) - (PR::kR2 ? cr.w : cr.w * cr.w);
         const float disc = __builtin_fmaf(h, h, -(a * c));
-#if RRT_LEAN
         // The far root (h + sq) / a is needed only when the near one is at or behind tmin (the
         // ray starts inside the sphere): r1 >= r0 always (sq >= 0, a > 0, correctly rounded
         // quotients are monotone), so r0 >= closest rejects both. A wave skips that rare branch
@@ -576,27 +514,10 @@ __device__ __forceinline__ void test_range(const PR &prim_cr, int first, int cou
         const float sq = __builtin_sqrtf(disc);
         float root = div_by_a<kFastDiv>(h - sq, rk);
         if (!(0.001f < root)) root = div_by_a<kFastDiv>(h + sq, rk);
-        if (0.001f < root && root < closest && (RRT_TRIM || i != skip)) {
+        if (0.001f < root && root < closest) {
             closest = root;
             hit_prim = i;
         }
-#else
-        if (disc < 0.0f) continue;
-        if constexpr (RRT_PHASE_TIMING == 3) cnt.d2 += 1;
-        // both roots, then selects: the far root is a pure function of (h, sq), so computing it
-        // whether or not the near one is accepted changes nothing, and the select form keeps the
-        // leaf loop free of exec-mask branches and phi copies
-        const float sq = __builtin_sqrtf(disc);
-        const float r0 = div_by_a<kFastDiv>(h - sq, rk);
-        const float r1 = div_by_a<kFastDiv>(h + sq, rk);
-        const bool ok0 = 0.001f < r0 && r0 < closest;
-        const bool ok1 = 0.001f < r1 && r1 < closest;
-        const float root = ok0 ? r0 : r1;
-        if ((ok0 || ok1) && (RRT_TRIM || i != skip)) {
-            closest = root;
-            hit_prim = i;
-        }
-#endif
     }
 }
 
@@ -703,12 +624,10 @@ template <bool kCount, class PR>
 __device__ __forceinline__ void trav_leaves(const PR &prims, Leaves lv, V3 o, V3 d, const RayK &rk, int skip, Trav &t,
                                             Counters &cnt) {
     const int first = (int)(lv & kLinkFirstMask), count = (int)(lv >> kLinkCountShift);
-#if RRT_HOISTDIV
     if (__ballot(rk.ra == 0.0f) == 0) {
         test_range<kCount, true>(prims, first, count, o, d, rk, skip, t.closest, t.hit_prim, cnt);
         return;
     }
-#endif
     test_range<kCount, false>(prims, first, count, o, d, rk, skip, t.closest, t.hit_prim, cnt);
 }
 
@@ -803,9 +722,6 @@ __device__ __forceinline__ int exit_skip(bool is_quad, bool is_medium, bool fron
 }
 
 // Camera::get_ray (camera.rs:152-180) for global pixel (x, y) and the path's RNG.
-#ifndef RRT_KARG_CAM
-#define RRT_KARG_CAM 1
-#endif
 // The camera block re-read from the kernarg segment at each use (scalar loads through the scalar
 // cache) rather than 19 values the compiler would hold in SGPRs across the whole work loop: the
 // asm makes the pointer opaque, so the loads cannot be hoisted out of the loop.
@@ -819,11 +735,7 @@ template <class FD>
 __device__ __forceinline__ FastDiv fdiv(const FD &f) { return FastDiv{f.m, f.s}; }
 template <bool kStrat>
 __device__ __forceinline__ void camera_ray(const KParams &P, uint32_t x, uint32_t y, uint32_t s, PathState &ps) {
-#if RRT_KARG_CAM
     const auto &C = *kernarg_params();
-#else
-    const KParams &C = P;
-#endif
     float ox, oy;
     if constexpr (kStrat) {  // sample_square_stratified (the_rest_of_your_life/camera.rs:173-177)
         const uint32_t sj = fast_div(s, P.fd_sqrt_spp), si = s - sj * P.sqrt_spp;
@@ -937,7 +849,7 @@ __device__ __forceinline__ int floor_i32(float x) {
     return (int)f;
 }
 
-// Perlin::noise (perlin.rs:25-48) + perlin_interp (perlin.rs:84-102), operation order kept:
+// Perlin::noise (perlin.rs:25-48) + perlin_interp (perlin.rs:79-98), operation order kept:
 // the (i*uu + (1-i)*(1-uu)) factors are exactly uu or 1-uu for i in {0,1}.
 __device__ __forceinline__ float perlin_noise(const GPerlin *__restrict__ pt, V3 p) {
     const float fx = __builtin_floorf(p.x), fy = __builtin_floorf(p.y), fz = __builtin_floorf(p.z);
@@ -964,7 +876,7 @@ __device__ __forceinline__ float perlin_noise(const GPerlin *__restrict__ pt, V3
     return accum;
 }
 
-// NoiseTexture::value (texture.rs:119-123): 0.5 * (1 + sin(scale * p.z + 10 * turb(p, 7))),
+// NoiseTexture::value (texture.rs:122-126): 0.5 * (1 + sin(scale * p.z + 10 * turb(p, 7))),
 // turb (perlin.rs:50-62): |sum of weight * noise(p * 2^i)|, weight halving. The octave and
 // corner loops stay rolled: unrolled (56 corner evaluations) they swamp the megakernel's
 // register allocation.
@@ -990,12 +902,12 @@ __device__ __forceinline__ bool checker_even(float inv_scale, V3 p) {
 
 __device__ __forceinline__ V3 texel(const KParams &P, int tex, float u, float v) {
     const GTexture t = P.texs[tex];
-    if (t.height <= 0) return v3(0.0f, 1.0f, 1.0f);  // texture.rs:179-181
+    if (t.height <= 0) return v3(0.0f, 1.0f, 1.0f);  // texture.rs:91-93
     u = (u < 0.0f) ? 0.0f : ((u > 1.0f) ? 1.0f : u);  // Interval::clamp
     v = 1.0f - ((v < 0.0f) ? 0.0f : ((v > 1.0f) ? 1.0f : v));
     int i = (int)(u * (float)t.width);
     int j = (int)(v * (float)t.height);
-    i = (i < 0) ? 0 : ((i < t.width) ? i : t.width - 1);  // rtw_image.rs:326-334
+    i = (i < 0) ? 0 : ((i < t.width) ? i : t.width - 1);  // rtw_image.rs:51-52, 70-78
     j = (j < 0) ? 0 : ((j < t.height) ? j : t.height - 1);
     const uint8_t *px = P.tex_pool + t.offset + ((size_t)j * t.width + i) * 3;
     const float cs = 1.0f / 255.0f;
@@ -1406,8 +1318,8 @@ __device__ __forceinline__ void render_body(const KParams &P) {
     // v_mov instead of the three exec-mask merges a bool held in an SGPR pair costs.
     tr.node = -1;
     uint32_t need_ray = 0;  // the lane must start the next segment of its path
-    // wave-uniform: claimed, not yet assigned units (RRT_XQ: pool_base starts in the block's queue)
-    uint32_t pool_base = RRT_XQ ? (blockIdx.x & (kQueues - 1u)) * 64u : 0u, pool_left = 0;
+    // wave-uniform: claimed, not yet assigned units; a wave's first claim goes to its block's queue
+    uint32_t pool_base = (blockIdx.x & (kQueues - 1u)) * 64u, pool_left = 0;
     [[maybe_unused]] uint64_t ph0 = 0, ph1 = 0, ph2 = 0, tp = 0;
     for (;;) {
         if constexpr (RRT_PHASE_TIMING == 1) tp = __builtin_amdgcn_s_memtime();
@@ -1419,23 +1331,25 @@ __device__ __forceinline__ void render_body(const KParams &P) {
         __builtin_amdgcn_s_setprio(RRT_PRIO_REFILL);
         uint64_t idle = __ballot(!has);
         if (idle != 0 && pool_left == 0 && q_open) {
-#if RRT_XQ
-            // kQueues interleaved queues with a counter each, 128 B apart: tile-chunk group g
-            // (64 units) is queue g % kQueues's (g / kQueues)-th claim, and the blocks are dealt to
-            // the queues as blockIdx % kQueues (on MI355X the blocks' XCDs). One counter took every
-            // wave's claims: device-scope atomics on one address serialise, which cost cheap-ray,
-            // low-spp frames a third of their time. The grid has >= kQueues blocks (launch_variant),
-            // and pool_base always lies in the wave's queue (it starts at the queue's first group).
+            // kQueues interleaved queues with a counter each, 128 B apart: tile-chunk group g (64
+            // units) is queue g % kQueues's (g / kQueues)-th claim. One counter took every wave's
+            // claims: device-scope atomics on one address serialise, which cost cheap-ray, low-spp
+            // frames a third of their time. A claim goes to the queue of pool_base's group: a
+            // wave's first claim to queue blockIdx % kQueues (the grid has >= kQueues blocks,
+            // launch_variant), and once a claimed group is used up pool_base points at the next
+            // group, so the wave's claims rotate q, q + 1, ... through all the queues (the claims
+            // are spread over the 8 counters; they do not stay on one XCD's queue). A partial last
+            // group leaves pool_base in its queue, whose next claim then fails. Drain: a wave stops
+            // claiming at its first failed claim, i.e. at an exhausted queue. Every successful claim
+            // on queue q is followed by a claim on q + 1, and queue sizes fall by at most one group
+            // from q to q + 1 (G_0 >= G_1 >= ... >= G_7 >= G_0 - 1, the groups dealt g % 8), while
+            // queue 0 also takes the first claims of its own blocks' waves: so once any queue is
+            // exhausted the next one is too, round the cycle, and every group is claimed
+            // (tests/test_gpu_parity.py::test_uneven_queues_drain checks every pixel's count).
             const uint32_t xq = (pool_base >> 6) & (kQueues - 1u);
             uint32_t k = 0;
             if (lane == 0) k = atomicAdd(P.unit_counter + 32u * xq, 1u);
             const uint32_t base = (__shfl(k, 0, 64) * kQueues + xq) * 64u;
-#else
-            // one atomic claims a whole tile-chunk (64 units) for this wave
-            uint32_t base = 0;
-            if (lane == 0) base = atomicAdd(P.unit_counter, 64u);
-            base = __shfl(base, 0, 64);
-#endif
             if (base >= P.n_units) {
                 q_open = false;
             } else {
@@ -1449,11 +1363,7 @@ __device__ __forceinline__ void render_body(const KParams &P) {
             if (!has && r < n) {
                 const uint32_t u = pool_base + r;
                 {
-#if RRT_KARG_CAM
                     const auto &Q = *kernarg_params();
-#else
-                    const KParams &Q = P;
-#endif
                     const uint32_t lit = u & 63u;
                     const uint32_t tc = u >> 6;
                     // big chunks of every tile first, then the tail chunks (small units last)
@@ -1598,11 +1508,7 @@ __device__ __forceinline__ void render_body(const KParams &P) {
                 ps.rng = path_rng_k(pkey, s);
                 camera_ray<kBook2 == 4>(P, x, y, s, ps);
             } else {  // unit complete: the chunk's sum, in sample order
-#if RRT_KARG_CAM
                 const auto &Q = *kernarg_params();
-#else
-                const KParams &Q = P;
-#endif
                 // chunk index and tile-local row, re-derived from (y, s_hi) once per unit
                 const uint32_t rel = s_hi - 1u - Q.sample_begin;
                 const uint32_t nbs = Q.n_big * Q.chunk;
@@ -1733,7 +1639,7 @@ hipError_t launch_variant(const KParams &p, bool count, hipStream_t stream) {
     if (per_cu < 1) per_cu = 1;
     const uint32_t want = (p.n_units + kBlk - 1) / kBlk;
     // at least kQueues blocks, so every work queue has a block (spare blocks find no work and exit)
-    const uint32_t blocks = std::max<uint32_t>(std::min<uint32_t>(want, (uint32_t)per_cu * p.n_cus), RRT_XQ ? kQueues : 1u);
+    const uint32_t blocks = std::max<uint32_t>(std::min<uint32_t>(want, (uint32_t)per_cu * p.n_cus), kQueues);
     e = hipMemsetAsync(p.unit_counter, 0, kQueues * 32u * sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(kernel, dim3(blocks), dim3(kBlk), lds, stream, p);
@@ -1756,9 +1662,9 @@ hipError_t launch_width(const KParams &p, bool count, hipStream_t stream) {
         // 1/4-spp scene table against 512 threads unbounded (~105 VGPRs, 4 waves): +2 ... +16 %
         // on every book-2 scene once the parameter spills were gone (256 x 4: +-1 %, 256 x 6:
         // -21 ... +9 %). Book 3 (class 4, the light-list pdfs) keeps the unbounded 512: -8 % at 5.
-        if constexpr (kBook2 != 4 && RRT_B2_WAVES > 1)
-            return p.scene_in_lds ? launch_variant<true, uint16_t, kWide, kBook2, RRT_B2_WAVES, RRT_B2_BLOCK>(p, count, stream)
-                                  : launch_variant<false, uint16_t, kWide, kBook2, RRT_B2_WAVES, RRT_B2_BLOCK>(p, count, stream);
+        if constexpr (kBook2 != 4 && kBook2Waves > 1)
+            return p.scene_in_lds ? launch_variant<true, uint16_t, kWide, kBook2, kBook2Waves, kBook2Block>(p, count, stream)
+                                  : launch_variant<false, uint16_t, kWide, kBook2, kBook2Waves, kBook2Block>(p, count, stream);
         return p.scene_in_lds ? launch_variant<true, uint16_t, kWide, kBook2>(p, count, stream)
                               : launch_variant<false, uint16_t, kWide, kBook2>(p, count, stream);
     } else {
@@ -1792,8 +1698,8 @@ hipError_t launch_render_pass(const KParams &p, bool count, hipStream_t stream) 
     if (p.bvh_width == 4) return launch_width<true, 0>(p, count, stream);
     // Scenes staged in LDS without image textures run the kernel with the texture path compiled
     // out (C2 +1.0 %); for scenes read from L2 it measured −0.4 % on C5, so they keep class 0.
-    if (RRT_DIFFUSE_CLASS && !p.specular && p.scene_in_lds) return launch_width<false, kBook1Diffuse>(p, count, stream);
-    if (!p.image_tex && (p.scene_in_lds || RRT_UNTEX_L2)) return launch_width<false, kBook1Untextured>(p, count, stream);
+    if (!p.specular && p.scene_in_lds) return launch_width<false, kBook1Diffuse>(p, count, stream);
+    if (!p.image_tex && p.scene_in_lds) return launch_width<false, kBook1Untextured>(p, count, stream);
     return launch_width<false, 0>(p, count, stream);
 }
 

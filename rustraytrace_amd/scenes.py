@@ -171,7 +171,7 @@ def next_week_scene(scene: int, overrides: Optional[dict] = None, seed: int = NE
 
 
 def rest_of_your_life_scene(overrides: Optional[dict] = None, seed: int = NEXT_WEEK_SEED) -> SceneData:
-    """The book-3 scene (the_rest_of_your_life/mod.rs:69-164): Cornell box, a rotated box and a
+    """The book-3 scene (the_rest_of_your_life/mod.rs:69-161): Cornell box, a rotated box and a
     glass sphere, with the MIS light list {light quad, glass sphere}; stratified sampling rounds
     samples_per_pixel down to a square. Renders with FLAG_RAY_TIME | FLAG_BOOK3."""
     lib = _lib.load()
