@@ -32,8 +32,10 @@ extern "C" {
  * 64-B global BVH2 nodes), xoshiro128+ path streams, tail-split accumulation chunks;
  * 5: exit_skip (f32 bounces never re-hit the primitive they leave), rrt_hip_render_rgb8_ex,
  * rrt_quantize_accum_books, chunk partials bounded by RRT_PARTIAL_MB (sample passes);
- * 6: RrtBvhInfo.n_unbounded (scene-enclosing media tested after the BVH walk; was _pad). */
-#define RRT_ABI_VERSION 6u
+ * 6: RrtBvhInfo.n_unbounded (scene-enclosing media tested after the BVH walk; was _pad);
+ * 7: RRT_FLAG_F64 (the books path's f64 arithmetic), rrt_hip_render_f64, rrt_render_tile_f64_async,
+ * rrt_quantize_accum_books_f64. */
+#define RRT_ABI_VERSION 7u
 
 /* ---- scene ABI (== src/gpu/mod.rs:13-42) ------------------------------------------ */
 
@@ -202,6 +204,14 @@ typedef struct RrtOverrides {
  * (cosine / sphere pdf) over RrtSceneExt.lights, Russian roulette folded into the weight.
  * Requires RRT_FLAG_RAY_TIME (the book-3 camera draws a time per ray). */
 #define RRT_FLAG_BOOK3 0x4u
+/* The books path's own arithmetic (ABI v7): the kernel computes in f64, in the reference CPU path's
+ * operation order (vec3.rs, sphere.rs:24-51, material.rs, camera.rs:152-209; no FP contraction),
+ * on the same per-path random stream as the f32 kernel, and sums in f64 — so every path takes the
+ * books path's decisions and the sums match it to a few f64 ulps (the north star's check "against
+ * the repo's own CPU books path"). Book-1 scenes: material kinds 0-4, sky or background, no
+ * RrtSceneExt data, not RRT_FLAG_BOOK3 (RRT_E_INVALID otherwise). Float entries return the f64 sums
+ * rounded to f32; rrt_hip_render_f64 / rrt_render_tile_f64_async return them unrounded. */
+#define RRT_FLAG_F64 0x8u
 
 /* ---- error codes ------------------------------------------------------------------ */
 #define RRT_OK 0
@@ -231,6 +241,17 @@ int32_t rrt_hip_render_ex(const RrtCamera *cam,
                           const RrtSceneExt *ext,
                           uint32_t total_spp, uint32_t n_gpus, uint32_t flags,
                           float *accum_out);
+
+/* rrt_hip_render with RRT_FLAG_F64 implied, returning the f64 sums unrounded: accum_out[W*H*4]
+ * doubles (RGB sums, [4i+3] = sample count). The books path's own arithmetic end to end (the
+ * reference's CPU ray_color sums pixel_color in f64, camera.rs:73-76); quantise with
+ * rrt_quantize_accum_books_f64 for the bytes camera.rs:87-94 prints. */
+int32_t rrt_hip_render_f64(const RrtCamera *cam,
+                           const RrtSphere *spheres, uint32_t n_spheres,
+                           const RrtMaterial *materials, uint32_t n_materials,
+                           const RrtTexture *textures, uint32_t n_textures,
+                           uint32_t total_spp, uint32_t n_gpus, uint32_t flags,
+                           double *accum_out);
 
 /* Thread-local message for the last failing call on this thread ("" if none). */
 const char *rrt_hip_last_error(void);
@@ -300,6 +321,9 @@ int32_t rrt_tile_row_index(uint32_t height, const RrtTile *tile, uint32_t local_
  * buffer, so renders of the same scene must be ordered on one stream (or synchronised);
  * concurrent renders on different streams need one RrtScene each. */
 int32_t rrt_render_tile_async(RrtScene *scene, const RrtTile *tile, float *d_accum, void *stream);
+/* The same for a scene created with RRT_FLAG_F64: d_accum = rows*W*4 doubles (f64 sums, w = count),
+ * overwritten. (rrt_render_tile_async on such a scene writes the f64 sums rounded to f32.) */
+int32_t rrt_render_tile_f64_async(RrtScene *scene, const RrtTile *tile, double *d_accum, void *stream);
 
 /* Counters (synchronises the scene's device). */
 int32_t rrt_scene_read_counters(RrtScene *scene, RrtCounters *out);
@@ -469,6 +493,10 @@ int32_t rrt_quantize_accum(uint32_t width, uint32_t height, const float *accum,
  * camera.rs:87-94 prints) with rrt_format_pnm_from_rgb8. spp >= 1. */
 int32_t rrt_quantize_accum_books(uint32_t width, uint32_t height, const float *accum,
                                  uint32_t samples_per_pixel, uint8_t *rgb8);
+/* The same quantiser over f64 sums (rrt_hip_render_f64): the books path's bytes for its own f64
+ * pixel_color, with no f32 rounding in between. */
+int32_t rrt_quantize_accum_books_f64(uint32_t width, uint32_t height, const double *accum,
+                                     uint32_t samples_per_pixel, uint8_t *rgb8);
 
 /* ---- output step after the boundary: device quantiser, P6 ---------------
  * render_io.rs writes P3 ASCII (~25 MB at 1080p) from a float accum copied to the host

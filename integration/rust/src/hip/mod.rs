@@ -48,8 +48,10 @@ mod imp {
 
     /// Suppress the library's own stderr progress lines (RRT_FLAG_QUIET).
     pub const RRT_FLAG_QUIET: u32 = 0x2;
+    /// The books path's f64 arithmetic (RRT_FLAG_F64): checked against `--backend cpu` output.
+    pub const RRT_FLAG_F64: u32 = 0x8;
     /// ABI this shim was written against (RRT_ABI_VERSION).
-    pub const RRT_ABI_VERSION: u32 = 6;
+    pub const RRT_ABI_VERSION: u32 = 7;
 
     #[link(name = "rrt_hip")]
     extern "C" {
@@ -67,6 +69,14 @@ mod imp {
                                materials: *const MaterialGpu, n_materials: u32,
                                textures: *const RrtTexture, n_textures: u32,
                                total_spp: u32, n_gpus: u32, flags: u32, rgb8_out: *mut u8) -> i32;
+        // the books path's own f64 arithmetic and sums (RRT_FLAG_F64), and its f64 quantiser
+        // (books/in_one_weekend/color.rs:6-32 write_color)
+        fn rrt_hip_render_f64(cam: *const CameraUniform, spheres: *const SphereGpu, n_spheres: u32,
+                              materials: *const MaterialGpu, n_materials: u32,
+                              textures: *const RrtTexture, n_textures: u32,
+                              total_spp: u32, n_gpus: u32, flags: u32, accum_out: *mut f64) -> i32;
+        fn rrt_quantize_accum_books_f64(width: u32, height: u32, accum: *const f64, samples_per_pixel: u32,
+                                        rgb8: *mut u8) -> i32;
         fn rrt_hip_last_error() -> *const c_char;
         fn rrt_hip_abi_version() -> u32;
         fn rrt_device_count(count: *mut i32) -> i32;
@@ -106,6 +116,8 @@ mod imp {
     /// Same contract as cuda::imp::render (cuda/mod.rs:342): render the scene and print the
     /// PPM to stdout through render_io. RRT_DEVICE_QUANTISE=1 quantises on the device instead
     /// (rrt_hip_render_rgb8 + the library's P3 writer: identical bytes, 3 B/pixel over PCIe).
+    /// RRT_BOOKS_F64=1 renders with the books path's f64 arithmetic (rrt_hip_render_f64) and
+    /// prints the bytes color.rs's write_color gives for the f64 sums.
     fn render(camera: CameraUniform, spheres: &[SphereGpu], materials: &[MaterialGpu]) -> Result<(), String> {
         let abi = unsafe { rrt_hip_abi_version() };
         if abi != RRT_ABI_VERSION {
@@ -116,6 +128,20 @@ mod imp {
         let total_spp = camera.params_f[3].max(1.0) as u32; // cuda/mod.rs:384
         let n_gpus = gpus()?;
         let pixels = width as usize * height as usize;
+        if std::env::var("RRT_BOOKS_F64").map(|v| v == "1").unwrap_or(false) {
+            let mut accum = vec![0.0f64; pixels * 4];
+            check(unsafe {
+                rrt_hip_render_f64(&camera, spheres.as_ptr(), spheres.len() as u32,
+                                   materials.as_ptr(), materials.len() as u32,
+                                   std::ptr::null(), 0, total_spp, n_gpus, RRT_FLAG_F64, accum.as_mut_ptr())
+            })?;
+            let mut rgb8 = vec![0u8; pixels * 3];
+            check(unsafe { rrt_quantize_accum_books_f64(width, height, accum.as_ptr(), total_spp, rgb8.as_mut_ptr()) })?;
+            let stdout = b"-\0";
+            return check(unsafe {
+                rrt_write_pnm_from_rgb8(width, height, rgb8.as_ptr(), 0, stdout.as_ptr() as *const c_char)
+            });
+        }
         if std::env::var("RRT_DEVICE_QUANTISE").map(|v| v == "1").unwrap_or(false) {
             let mut rgb8 = vec![0u8; pixels * 3];
             check(unsafe {

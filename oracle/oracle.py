@@ -70,6 +70,8 @@ def load() -> ctypes.CDLL:
     lib.oracle_reflect_refract.argtypes = [c_int, P, P, c_double, P, P, P]
     lib.oracle_path_stream.restype = None
     lib.oracle_path_stream.argtypes = [c_uint32, c_uint32, c_uint32, c_uint32, P]
+    lib.oracle_acos_atan2_f64.restype = None
+    lib.oracle_acos_atan2_f64.argtypes = [c_uint32, P, P, P, P]
     lib.oracle_acos_atan2_f32.restype = None
     lib.oracle_acos_atan2_f32.argtypes = [c_float, c_float, P, P]
     _LIB = lib
@@ -288,6 +290,16 @@ def acos_atan2_f32(x, y):
     a, b = c_float(0), c_float(0)
     lib.oracle_acos_atan2_f32(x, y, ctypes.byref(a), ctypes.byref(b))
     return a.value, b.value
+
+
+def acos_atan2_f64(x, y):
+    """BOOKS' f64 acos(x) and atan2(y, x) (fdlibm's algorithms restated) at each element."""
+    lib = load()
+    xs = np.ascontiguousarray(x, dtype=np.float64).ravel()
+    ys = np.ascontiguousarray(np.broadcast_to(y, xs.shape), dtype=np.float64).ravel()
+    a, b = np.zeros_like(xs), np.zeros_like(xs)
+    lib.oracle_acos_atan2_f64(xs.size, _p(xs), _p(ys), _p(a), _p(b))
+    return a, b
 
 
 def cos_f32(x):

@@ -37,7 +37,9 @@
 //     reproducible; both sides use a xoshiro128+ stream per (seed, pixel, sample) instead, and
 //     random_double() = (u32 >> 8) * 2^-24 (exact in f32 and f64).
 //   * f32 twin: 1e-160 (vec3.rs:185) underflows to 0; transcendentals of sphere UV and the
-//     noise texture's sin use the Cephes f32 polynomials the kernel uses (books mode: libm).
+//     noise texture's sin use the Cephes f32 polynomials the kernel uses (books mode: libm sin;
+//     the sphere UV's acos / atan2 are fdlibm's algorithms restated, <= 1 ulp from libm and
+//     shared bit for bit with the f64 kernel).
 #include "../include/rrt_hip.h"
 
 #include <algorithm>
@@ -165,7 +167,7 @@ template <class T> Vec3<T> random_in_unit_disk(PathRng &rng) {  // vec3.rs:172-1
     }
 }
 
-// ---- Cephes f32 acos / atan2 (twin) or libm (books) ------------------------------------------
+// ---- Cephes f32 acos / atan2 (twin) or fdlibm (books, below) -------------------------------
 float asin_core(float x) {
     const float z = x * x;
     return ((((4.2163199048e-2f * z + 2.4181311049e-2f) * z + 4.5470025998e-2f) * z + 7.4953002686e-2f) * z +
@@ -197,8 +199,156 @@ float cephes_atan2f(float y, float x) {
     if (x < 0.0f) z = (y < 0.0f) ? z - kPiF : z + kPiF;
     return z;
 }
-template <class T> T t_acos(T x) { if constexpr (std::is_same_v<T, float>) return cephes_acosf(x); else return std::acos(x); }
-template <class T> T t_atan2(T y, T x) { if constexpr (std::is_same_v<T, float>) return cephes_atan2f(y, x); else return std::atan2(y, x); }
+// ---- f64 acos / atan2 (books): fdlibm's e_acos.c, s_atan.c, e_atan2.c restated ----------------
+// The reference's f64::acos / atan2 call the platform libm, whose last-ulp choices this container
+// cannot pin against the Rust build. BOOKS uses fdlibm's published algorithms instead (only + - * /
+// sqrt and exponent-word tests), the same ones the f64 kernel (rrt_books64.hip) restates, so the two
+// agree bit for bit; tests/test_oracle.py bounds the restatement against glibc's libm (<= 1 ulp).
+uint32_t fd_hi(double x) {
+    uint64_t b;
+    std::memcpy(&b, &x, 8);
+    return (uint32_t)(b >> 32);
+}
+uint32_t fd_lo(double x) {
+    uint64_t b;
+    std::memcpy(&b, &x, 8);
+    return (uint32_t)b;
+}
+double fd_with_lo_zero(double x) {
+    uint64_t b;
+    std::memcpy(&b, &x, 8);
+    b &= 0xffffffff00000000ull;
+    std::memcpy(&x, &b, 8);
+    return x;
+}
+const double fd_pio2_hi = 1.57079632679489655800e+00, fd_pio2_lo = 6.12323399573676603587e-17;
+const double fd_pi = 3.14159265358979311600e+00, fd_pi_lo = 1.2246467991473531772e-16;
+double fd_acos_r(double z) {  // p(z) / q(z)
+    const double pS0 = 1.66666666666666657415e-01, pS1 = -3.25565818622400915405e-01,
+                 pS2 = 2.01212532134862925881e-01, pS3 = -4.00555345006794114027e-02,
+                 pS4 = 7.91534994289814532176e-04, pS5 = 3.47933107596021167570e-05;
+    const double qS1 = -2.40339491173441421878e+00, qS2 = 2.02094576023350569471e+00,
+                 qS3 = -6.88283971605453293030e-01, qS4 = 7.70381505559019352791e-02;
+    const double p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+    const double q = 1.0 + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+    return p / q;
+}
+double fdlibm_acos(double x) {
+    const int32_t hx = (int32_t)fd_hi(x);
+    const int32_t ix = hx & 0x7fffffff;
+    if (ix >= 0x3ff00000) {
+        if (((ix - 0x3ff00000) | (int32_t)fd_lo(x)) == 0) return hx > 0 ? 0.0 : fd_pi + 2.0 * fd_pio2_lo;
+        return (x - x) / (x - x);
+    }
+    if (ix < 0x3fe00000) {
+        if (ix <= 0x3c600000) return fd_pio2_hi + fd_pio2_lo;
+        const double z = x * x;
+        const double r = fd_acos_r(z);
+        return fd_pio2_hi - (x - (fd_pio2_lo - x * r));
+    } else if (hx < 0) {
+        const double z = (1.0 + x) * 0.5;
+        const double s = std::sqrt(z);
+        const double r = fd_acos_r(z);
+        const double w = r * s - fd_pio2_lo;
+        return fd_pi - 2.0 * (s + w);
+    } else {
+        const double z = (1.0 - x) * 0.5;
+        const double s = std::sqrt(z);
+        const double df = fd_with_lo_zero(s);
+        const double c = (z - df * df) / (s + df);
+        const double r = fd_acos_r(z);
+        const double w = r * s + c;
+        return 2.0 * (df + w);
+    }
+}
+double fdlibm_atan(double x) {
+    static const double atanhi[] = {4.63647609000806093515e-01, 7.85398163397448278999e-01,
+                                    9.82793723247329054082e-01, 1.57079632679489655800e+00};
+    static const double atanlo[] = {2.26987774529616870924e-17, 3.06161699786838301793e-17,
+                                    1.39033110312309984516e-17, 6.12323399573676603587e-17};
+    static const double aT[] = {3.33333333333329318027e-01, -1.99999999998764832476e-01, 1.42857142725034663711e-01,
+                                -1.11111104054623557880e-01, 9.09088713343650656196e-02, -7.69187620504482999495e-02,
+                                6.66107313738753120669e-02, -5.83357013379057348645e-02, 4.97687799461593236017e-02,
+                                -3.65315727442169155270e-02, 1.62858201153657823623e-02};
+    const int32_t hx = (int32_t)fd_hi(x);
+    const int32_t ix = hx & 0x7fffffff;
+    int id;
+    if (ix >= 0x44100000) {
+        if (ix > 0x7ff00000 || (ix == 0x7ff00000 && fd_lo(x) != 0)) return x + x;
+        return hx > 0 ? atanhi[3] + atanlo[3] : -atanhi[3] - atanlo[3];
+    }
+    if (ix < 0x3fdc0000) {
+        if (ix < 0x3e200000) return x;
+        id = -1;
+    } else {
+        x = std::fabs(x);
+        if (ix < 0x3ff30000) {
+            if (ix < 0x3fe60000) {
+                id = 0;
+                x = (2.0 * x - 1.0) / (2.0 + x);
+            } else {
+                id = 1;
+                x = (x - 1.0) / (x + 1.0);
+            }
+        } else {
+            if (ix < 0x40038000) {
+                id = 2;
+                x = (x - 1.5) / (1.0 + 1.5 * x);
+            } else {
+                id = 3;
+                x = -1.0 / x;
+            }
+        }
+    }
+    const double z = x * x;
+    const double w = z * z;
+    const double s1 = z * (aT[0] + w * (aT[2] + w * (aT[4] + w * (aT[6] + w * (aT[8] + w * aT[10])))));
+    const double s2 = w * (aT[1] + w * (aT[3] + w * (aT[5] + w * (aT[7] + w * aT[9]))));
+    if (id < 0) return x - x * (s1 + s2);
+    const double r = atanhi[id] - ((x * (s1 + s2) - atanlo[id]) - x);
+    return hx < 0 ? -r : r;
+}
+double fdlibm_atan2(double y, double x) {
+    const int32_t hx = (int32_t)fd_hi(x), hy = (int32_t)fd_hi(y);
+    const uint32_t lx = fd_lo(x), ly = fd_lo(y);
+    const int32_t ix = hx & 0x7fffffff, iy = hy & 0x7fffffff;
+    if (((uint32_t)ix | ((lx | (0u - lx)) >> 31)) > 0x7ff00000u || ((uint32_t)iy | ((ly | (0u - ly)) >> 31)) > 0x7ff00000u)
+        return x + y;
+    if ((((uint32_t)hx - 0x3ff00000u) | lx) == 0) return fdlibm_atan(y);
+    const int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);
+    if ((iy | (int32_t)ly) == 0) {
+        switch (m) {
+            case 0:
+            case 1: return y;
+            case 2: return fd_pi;
+            default: return -fd_pi;
+        }
+    }
+    if ((ix | (int32_t)lx) == 0) return hy < 0 ? -fd_pio2_hi : fd_pio2_hi;
+    if (ix == 0x7ff00000) {
+        const double pi_o_4 = 7.8539816339744827900e-01;
+        if (iy == 0x7ff00000) {
+            const double v[4] = {pi_o_4, -pi_o_4, 3.0 * pi_o_4, -3.0 * pi_o_4};
+            return v[m];
+        }
+        const double v[4] = {0.0, -0.0, fd_pi, -fd_pi};
+        return v[m];
+    }
+    if (iy == 0x7ff00000) return hy < 0 ? -fd_pio2_hi : fd_pio2_hi;
+    const int k = (iy - ix) >> 20;
+    double z;
+    if (k > 60) z = fd_pio2_hi + 0.5 * fd_pi_lo;
+    else if (hx < 0 && k < -60) z = 0.0;
+    else z = fdlibm_atan(std::fabs(y / x));
+    switch (m) {
+        case 0: return z;
+        case 1: return -z;
+        case 2: return fd_pi - (z - fd_pi_lo);
+        default: return (z - fd_pi_lo) - fd_pi;
+    }
+}
+template <class T> T t_acos(T x) { if constexpr (std::is_same_v<T, float>) return cephes_acosf(x); else return fdlibm_acos(x); }
+template <class T> T t_atan2(T y, T x) { if constexpr (std::is_same_v<T, float>) return cephes_atan2f(y, x); else return fdlibm_atan2(y, x); }
 template <class T> T t_pi() { return lit<T>(3.14159265358979323846, 3.14159265358979323846f); }
 
 // ---- interval.rs / aabb.rs -----------------------------------------------------------------
@@ -1826,6 +1976,14 @@ void oracle_path_stream(uint32_t seed, uint32_t pixel, uint32_t sample, uint32_t
     const uint64_t key = splitmix64(((uint64_t)seed << 32) ^ (uint64_t)pixel);
     PathRng rng(splitmix64(key + sample), key);
     for (uint32_t i = 0; i < count; ++i) out[i] = rng.next();
+}
+
+// fdlibm acos / atan2 as BOOKS (f64) evaluates them, over arrays (checked against libm by tests).
+void oracle_acos_atan2_f64(uint32_t n, const double *x, const double *y, double *acos_out, double *atan2_out) {
+    for (uint32_t i = 0; i < n; ++i) {
+        if (acos_out) acos_out[i] = fdlibm_acos(x[i]);
+        if (atan2_out) atan2_out[i] = fdlibm_atan2(y[i], x[i]);
+    }
 }
 
 void oracle_acos_atan2_f32(float x, float y, float *acos_out, float *atan2_out) {

@@ -38,6 +38,7 @@ MAT_LAMBERTIAN, MAT_METAL, MAT_DIELECTRIC, MAT_TEXTURED_LAMBERTIAN, MAT_DIFFUSE_
 FLAG_RAY_TIME = 0x1
 FLAG_QUIET = 0x2
 FLAG_BOOK3 = 0x4
+FLAG_F64 = 0x8  # the books path's f64 arithmetic (include/rrt_hip.h RRT_FLAG_F64)
 
 # Every symbol include/rrt_hip.h declares (checked by tests/test_abi.py).
 EXPORTED_SYMBOLS = (
@@ -74,6 +75,9 @@ EXPORTED_SYMBOLS = (
     "rrt_build_rest_of_your_life_scene",
     "rrt_flatten_scene",
     "rrt_device_count",
+    "rrt_hip_render_f64",
+    "rrt_render_tile_f64_async",
+    "rrt_quantize_accum_books_f64",
 )
 
 
@@ -245,6 +249,9 @@ def load() -> ctypes.CDLL:
         "rrt_build_rest_of_your_life_scene": (c_int32, [P, c_uint64, P]),
         "rrt_flatten_scene": (c_int32, [P, c_uint32, P, c_uint32, c_uint32, P]),
         "rrt_device_count": (c_int32, [P]),
+        "rrt_hip_render_f64": (c_int32, [P, P, c_uint32, P, c_uint32, P, c_uint32, c_uint32, c_uint32, c_uint32, P]),
+        "rrt_render_tile_f64_async": (c_int32, [P, P, P, P]),
+        "rrt_quantize_accum_books_f64": (c_int32, [c_uint32, c_uint32, P, c_uint32, P]),
     }
     experiment = "RRT_LIB_PATH" in os.environ  # A/B of older builds: tolerate symbols they lack
     for name, (res, args) in sig.items():

@@ -1,0 +1,714 @@
+// rrt_books64.hip — gfx950 kernel of the f64 books path (RRT_FLAG_F64).
+//
+// The reference's CPU books path computes in f64 (books/in_one_weekend/vec3.rs:5-8) and the
+// north star checks the GPU against it ("per-channel <= 1e-4 before u8 quantisation; bit-exact PPM
+// after"). The f32 megakernel (rrt_kernel.hip, the reference GPU slot's precision) is bit-exact
+// against the oracle's f32 restatement but only statistically close to f64: a rounding that
+// flips a discrete decision (a grazing hit, a rejection-loop acceptance, a Russian-roulette draw)
+// sends a path another way. This kernel runs the books path's own arithmetic instead:
+//   camera ray       camera.rs:152-180 (+ the time draw of the_next_week/camera.rs:160)
+//   closest hit      sphere.rs:24-51 over (0.001, inf): oc, a, h, c, h*h - a*c, both roots,
+//                    unfused and in the reference's operation order (Rust never contracts)
+//   hit record       sphere.rs:47-48 p = o + t*d, (p - center) / r; hittable.rs:20-32 front face
+//   scatter          material.rs:28-40 / 53-64 / 83-102, vec3.rs:181-189 (1e-160 < |p|^2 <= 1),
+//                    vec3.rs:201-210 reflect / refract, Schlick with powi(5) = x * ((x*x)*(x*x))
+//   Russian roulette camera.rs:189-200 (this bounce's attenuation, clamp [.05, .95])
+//   sky / background camera.rs:206-208 / the_next_week/camera.rs:179-181
+//   emission, image  the_next_week/material.rs:41-53, 116-135; sphere.rs:46-52 get_sphere_uv with
+//   texture          one f64 acos / atan2 (fdlibm's algorithms, restated op for op by the oracle's
+//                    BOOKS mode), texture.rs:89-109, rtw_image.rs:46-55
+// in f64 (-ffp-contract=off; IEEE division and square root), on the same per-path random stream as
+// the f32 kernel (rrt_device.h: every draw is a 24-bit value, exact in f32 and f64). Every path
+// decision — which sphere a ray hits, the rejection loops, the Russian-roulette draw against this
+// bounce's attenuation — depends only on ray geometry, the draws and the attenuation, so the f64
+// paths follow the books path's exactly; only the throughput product's association differs (the
+// reference multiplies back to front through its recursion, this kernel front to back), which moves
+// a pixel's f64 sum by a few ulps. No exit_skip: in f64 a ray leaving a surface never re-hits it.
+//
+// Scope: book-1 scenes (the BASELINE configs C1, C2, C4, C5: Lambertian, metal, dielectric,
+// image-textured Lambertian, diffuse light; sky or constant background). The host rejects book-2/3
+// scene data with RRT_FLAG_F64. Same work queue, chunked accumulation order and BVH (f32 boxes,
+// rounded outward and grown by the f32 slab bound, tested in f64: conservative) as the f32 kernel.
+#include "rrt_internal.h"
+
+#include <type_traits>
+
+namespace rrt {
+namespace {
+
+#include "rrt_device.h"
+
+// issue priority by loop phase (as rrt_kernel.hip: refill 2, node steps 1, leaf batches 2, shading 0)
+constexpr int kPrioRefill = 2, kPrioNode = 1, kPrioLeaf = 2, kPrioShade = 0;
+
+struct D3 {
+    double x, y, z;
+};
+__device__ __forceinline__ D3 d3(double x, double y, double z) { return D3{x, y, z}; }
+__device__ __forceinline__ D3 add(D3 a, D3 b) { return d3(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ D3 sub(D3 a, D3 b) { return d3(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ D3 mul(D3 a, D3 b) { return d3(a.x * b.x, a.y * b.y, a.z * b.z); }
+// vec3.rs:118-132: Vec3 * f64 and f64 * Vec3 both compute e[i] * s
+__device__ __forceinline__ D3 muls(D3 a, double s) { return d3(a.x * s, a.y * s, a.z * s); }
+// vec3.rs:156-158 dot = u0*v0 + u1*v1 + u2*v2 (left to right, unfused)
+__device__ __forceinline__ double dot(D3 a, D3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+// vec3.rs:168-170 unit_vector = v / |v|, Div<f64> = (1/rhs) * v (vec3.rs:142-148)
+__device__ __forceinline__ D3 unit_vector(D3 v) { return muls(v, 1.0 / __builtin_sqrt(dot(v, v))); }
+__device__ __forceinline__ D3 f2d(float x, float y, float z) { return d3((double)x, (double)y, (double)z); }
+// f64::min: a NaN operand yields the other
+__device__ __forceinline__ double rmin(double a, double b) { return a < b ? a : b; }
+
+// random_double(): the 24-bit draw, exact in f64; random_double_range(-1, 1) = u * 2 + -1 (exact)
+__device__ __forceinline__ double rnd64(RngState &s) { return (double)(rng_next(s) >> 8) * 0x1.0p-24; }
+__device__ __forceinline__ double rnd64_pm1(RngState &s) { return rnd64(s) * 2.0 + -1.0; }
+
+// vec3.rs:181-189 random_unit_vector (Vec3::random_range(-1, 1): x, y, z drawn in order)
+__device__ __forceinline__ D3 random_unit_vector(RngState &s) {
+    double x, y, z, lensq;
+    for (;;) {
+        x = rnd64_pm1(s);
+        y = rnd64_pm1(s);
+        z = rnd64_pm1(s);
+        lensq = x * x + y * y + z * z;
+        if (1e-160 < lensq && lensq <= 1.0) break;
+    }
+    return muls(d3(x, y, z), 1.0 / __builtin_sqrt(lensq));
+}
+
+// vec3.rs:201-203 reflect = v - (2 * dot(v, n)) * n
+__device__ __forceinline__ D3 reflect(D3 v, D3 n) { return sub(v, muls(n, 2.0 * dot(v, n))); }
+// vec3.rs:205-210 refract
+__device__ __forceinline__ D3 refract(D3 uv, D3 n, double e) {
+    const double c = rmin(-dot(uv, n), 1.0);
+    const D3 perp = muls(add(uv, muls(n, c)), e);
+    const D3 par = muls(n, -__builtin_sqrt(__builtin_fabs(1.0 - dot(perp, perp))));
+    return add(perp, par);
+}
+// material.rs:75-80 Schlick; powi(5) = x * ((x*x) * (x*x)) (LLVM's repeated squaring)
+__device__ __forceinline__ double reflectance(double cosine, double ri) {
+    double r0 = (1.0 - ri) / (1.0 + ri);
+    r0 = r0 * r0;
+    const double x = 1.0 - cosine;
+    const double x2 = x * x;
+    return r0 + (1.0 - r0) * (x * (x2 * x2));
+}
+
+// ---- f64 acos / atan2 for get_sphere_uv (the_next_week/sphere.rs:46-52) ----------------------
+// The reference calls Rust's f64::acos / atan2 (the platform libm). Both sides here restate one
+// algorithm — fdlibm's e_acos.c / s_atan.c / e_atan2.c (Sun Microsystems, freely distributable):
+// only + - * / sqrt and exponent-word tests, so the oracle's BOOKS mode reproduces every bit; within
+// 1 ulp of glibc's libm (tests/test_oracle.py checks 2e5 arguments).
+__device__ __forceinline__ uint32_t hi_word(double x) { return (uint32_t)((uint64_t)__double_as_longlong(x) >> 32); }
+__device__ __forceinline__ double clear_lo_word(double x) {
+    return __longlong_as_double((long long)((uint64_t)__double_as_longlong(x) & 0xffffffff00000000ull));
+}
+constexpr double kPio2Hi = 1.57079632679489655800e+00, kPio2Lo = 6.12323399573676603587e-17;
+constexpr double kPiD = 3.14159265358979311600e+00, kPiLo = 1.2246467991473531772e-16;
+__device__ __forceinline__ double acos_rat(double z) {  // R(z) = p(z) / q(z) of e_acos.c
+    const double p = z * (1.66666666666666657415e-01 +
+                          z * (-3.25565818622400915405e-01 +
+                               z * (2.01212532134862925881e-01 +
+                                    z * (-4.00555345006794114027e-02 +
+                                         z * (7.91534994289814532176e-04 + z * 3.47933107596021167570e-05)))));
+    const double q = 1.0 + z * (-2.40339491173441421878e+00 +
+                                z * (2.02094576023350569471e+00 +
+                                     z * (-6.88283971605453293030e-01 + z * 7.70381505559019352791e-02)));
+    return p / q;
+}
+__device__ double rrt_acos64(double x) {
+    const uint32_t hx = hi_word(x), ix = hx & 0x7fffffffu;
+    if (ix >= 0x3ff00000u) {  // |x| >= 1
+        const uint32_t lx = (uint32_t)__double_as_longlong(x);
+        if (((ix - 0x3ff00000u) | lx) == 0) return (hx >> 31) ? kPiD + 2.0 * kPio2Lo : 0.0;
+        return (x - x) / (x - x);  // NaN
+    }
+    if (ix < 0x3fe00000u) {  // |x| < 0.5
+        if (ix <= 0x3c600000u) return kPio2Hi + kPio2Lo;
+        const double r = acos_rat(x * x);
+        return kPio2Hi - (x - (kPio2Lo - x * r));
+    }
+    if (hx >> 31) {  // x < -0.5
+        const double z = (1.0 + x) * 0.5;
+        const double s = __builtin_sqrt(z);
+        const double w = acos_rat(z) * s - kPio2Lo;
+        return kPiD - 2.0 * (s + w);
+    }
+    const double z = (1.0 - x) * 0.5;  // x > 0.5
+    const double s = __builtin_sqrt(z);
+    const double df = clear_lo_word(s);
+    const double c = (z - df * df) / (s + df);
+    const double w = acos_rat(z) * s + c;
+    return 2.0 * (df + w);
+}
+__device__ double rrt_atan64(double x) {
+    constexpr double hi[4] = {4.63647609000806093515e-01, 7.85398163397448278999e-01, 9.82793723247329054082e-01,
+                              1.57079632679489655800e+00};
+    constexpr double lo[4] = {2.26987774529616870924e-17, 3.06161699786838301793e-17, 1.39033110312309984516e-17,
+                              6.12323399573676603587e-17};
+    const uint32_t hx = hi_word(x), ix = hx & 0x7fffffffu;
+    int id;
+    if (ix >= 0x44100000u) {  // |x| >= 2^66
+        if (ix > 0x7ff00000u || (ix == 0x7ff00000u && (uint32_t)__double_as_longlong(x) != 0)) return x + x;
+        return (hx >> 31) ? -hi[3] - lo[3] : hi[3] + lo[3];
+    }
+    if (ix < 0x3fdc0000u) {  // |x| < 0.4375
+        if (ix < 0x3e200000u) return x;
+        id = -1;
+    } else {
+        x = __builtin_fabs(x);
+        if (ix < 0x3ff30000u) {      // |x| < 1.1875
+            if (ix < 0x3fe60000u) {  // 7/16 <= |x| < 11/16
+                id = 0;
+                x = (2.0 * x - 1.0) / (2.0 + x);
+            } else {
+                id = 1;
+                x = (x - 1.0) / (x + 1.0);
+            }
+        } else if (ix < 0x40038000u) {  // |x| < 2.4375
+            id = 2;
+            x = (x - 1.5) / (1.0 + 1.5 * x);
+        } else {
+            id = 3;
+            x = -1.0 / x;
+        }
+    }
+    const double z = x * x;
+    const double w = z * z;
+    const double s1 = z * (3.33333333333329318027e-01 +
+                           w * (1.42857142725034663711e-01 +
+                                w * (9.09088713343650656196e-02 +
+                                     w * (6.66107313738753120669e-02 +
+                                          w * (4.97687799461593236017e-02 + w * 1.62858201153657823623e-02)))));
+    const double s2 = w * (-1.99999999998764832476e-01 +
+                           w * (-1.11111104054623557880e-01 +
+                                w * (-7.69187620504482999495e-02 +
+                                     w * (-5.83357013379057348645e-02 + w * -3.65315727442169155270e-02))));
+    if (id < 0) return x - x * (s1 + s2);
+    const double r = hi[id] - ((x * (s1 + s2) - lo[id]) - x);
+    return (hx >> 31) ? -r : r;
+}
+__device__ double rrt_atan2_64(double y, double x) {
+    const uint64_t bx = (uint64_t)__double_as_longlong(x), by = (uint64_t)__double_as_longlong(y);
+    const uint32_t hx = (uint32_t)(bx >> 32), lx = (uint32_t)bx, hy = (uint32_t)(by >> 32), ly = (uint32_t)by;
+    const uint32_t ix = hx & 0x7fffffffu, iy = hy & 0x7fffffffu;
+    if ((ix | ((lx | (0u - lx)) >> 31)) > 0x7ff00000u || (iy | ((ly | (0u - ly)) >> 31)) > 0x7ff00000u)
+        return x + y;  // NaN
+    if (((hx - 0x3ff00000u) | lx) == 0) return rrt_atan64(y);  // x = 1
+    const uint32_t m = ((hy >> 31) & 1u) | ((hx >> 30) & 2u);  // 2 * sign(x) + sign(y)
+    if ((iy | ly) == 0) {  // y = +-0
+        if (m < 2) return y;
+        return m == 2 ? kPiD : -kPiD;
+    }
+    if ((ix | lx) == 0) return (hy >> 31) ? -kPio2Hi : kPio2Hi;  // x = +-0
+    if (ix == 0x7ff00000u) {  // x = +-inf
+        if (iy == 0x7ff00000u) {
+            const double v[4] = {0.25 * kPiD, -0.25 * kPiD, 0.75 * kPiD, -0.75 * kPiD};
+            return v[m];
+        }
+        const double v[4] = {0.0, -0.0, kPiD, -kPiD};
+        return v[m];
+    }
+    if (iy == 0x7ff00000u) return (hy >> 31) ? -kPio2Hi : kPio2Hi;  // y = +-inf
+    const int k = ((int)iy - (int)ix) >> 20;
+    double z;
+    if (k > 60) z = kPio2Hi + 0.5 * kPiLo;
+    else if ((hx >> 31) && k < -60) z = 0.0;
+    else z = rrt_atan64(__builtin_fabs(y / x));
+    switch (m) {
+        case 0: return z;
+        case 1: return -z;
+        case 2: return kPiD - (z - kPiLo);
+        default: return (z - kPiLo) - kPiD;
+    }
+}
+
+// ImageTexture::value (texture.rs:89-109) at get_sphere_uv(outward) (the_next_week/sphere.rs:46-52):
+// theta = acos(-y), phi = atan2(-z, x) + pi, u = phi / (2 pi), v = theta / pi.
+__device__ __forceinline__ D3 texel64(const KParams &P, int tex, D3 outward) {
+    const double theta = rrt_acos64(-outward.y);
+    const double phi = rrt_atan2_64(-outward.z, outward.x) + kPiD;
+    double u = phi / (2.0 * kPiD);
+    double v = theta / kPiD;
+    const GTexture t = P.texs[tex];
+    if (t.height <= 0) return d3(0.0, 1.0, 1.0);              // texture.rs:91-93
+    u = u < 0.0 ? 0.0 : (u > 1.0 ? 1.0 : u);                   // Interval::clamp
+    v = 1.0 - (v < 0.0 ? 0.0 : (v > 1.0 ? 1.0 : v));
+    auto as_i32 = [](double x) -> int {                        // Rust `as i32`: saturating, NaN -> 0
+        if (!(x == x)) return 0;
+        if (x <= -2147483648.0) return (int)0x80000000;
+        if (x >= 2147483647.0) return 0x7fffffff;
+        return (int)x;
+    };
+    int i = as_i32(u * (double)t.width);
+    int j = as_i32(v * (double)t.height);
+    i = i < 0 ? 0 : (i < t.width ? i : t.width - 1);           // rtw_image.rs:51-52, 70-78
+    j = j < 0 ? 0 : (j < t.height ? j : t.height - 1);
+    const uint8_t *px = P.tex_pool + t.offset + ((size_t)j * t.width + i) * 3;
+    const double cs = 1.0 / 255.0;
+    return d3(cs * (double)px[0], cs * (double)px[1], cs * (double)px[2]);
+}
+
+// Per-ray constants of the f64 box test: 1/d clamped to +-2^500 (a zero component gives a huge
+// finite slope, so fma(P, inv, -o*inv) keeps the sign of P - o), and o * inv.
+struct RayK64 {
+    D3 inv, oi;
+};
+__device__ __forceinline__ double clamp_inv64(double v) { return __builtin_fmax(__builtin_fmin(v, 0x1.0p500), -0x1.0p500); }
+__device__ __forceinline__ RayK64 ray_consts64(D3 o, D3 d) {
+    RayK64 r;
+    r.inv = d3(clamp_inv64(1.0 / d.x), clamp_inv64(1.0 / d.y), clamp_inv64(1.0 / d.z));
+    r.oi = d3(o.x * r.inv.x, o.y * r.inv.y, o.z * r.inv.z);
+    return r;
+}
+// Slab test of a stored f32 box in f64 (role of Aabb::hit, aabb.rs:52-85: a box test only prunes).
+// The stored planes lie outside the f64 sphere box by the f32 slab bound (~2^-22 |P|, rrt_host.cpp
+// BoxSlack), far above this test's f64 rounding, so it never rejects a box whose sphere a ray hits.
+__device__ __forceinline__ bool box64(double lx, double hx, double ly, double hy, double lz, double hz, const RayK64 &rk,
+                                      double tmax, double &tnear) {
+    const double x0 = __builtin_fma(lx, rk.inv.x, -rk.oi.x), x1 = __builtin_fma(hx, rk.inv.x, -rk.oi.x);
+    const double y0 = __builtin_fma(ly, rk.inv.y, -rk.oi.y), y1 = __builtin_fma(hy, rk.inv.y, -rk.oi.y);
+    const double z0 = __builtin_fma(lz, rk.inv.z, -rk.oi.z), z1 = __builtin_fma(hz, rk.inv.z, -rk.oi.z);
+    const double nr = __builtin_fmax(__builtin_fmax(__builtin_fmin(x0, x1), __builtin_fmin(y0, y1)),
+                                     __builtin_fmax(__builtin_fmin(z0, z1), 0.001));
+    const double fr = __builtin_fmin(__builtin_fmin(__builtin_fmax(x0, x1), __builtin_fmax(y0, y1)),
+                                     __builtin_fmin(__builtin_fmax(z0, z1), tmax));
+    tnear = nr;
+    return nr < fr;
+}
+
+struct Trav64 {
+    double closest;
+    int hit_prim;
+    int node;
+    int sp;
+};
+
+// One BVH2 node visit (rrt_kernel.hip trav_node's schedule): both child boxes against the closest
+// hit so far, hit leaf children postponed as one primitive range, the nearer internal child next
+// and the farther one pushed. The visiting order only prunes: the closest hit is the smallest
+// accepted root whatever the order (exact ties aside), as with BvhNode::hit's left-first walk.
+template <bool kCount, typename Node, typename Stack>
+__device__ __forceinline__ bool trav_node64(const Node *__restrict__ nodes, Stack &stack, const RayK64 &rk,
+                                            Trav64 &t, Leaves &lv, Counters &cnt) {
+    if (kCount) { cnt.nodes++; cnt.boxes += 2; }
+    bool h0, h1;
+    uint32_t l0, l1;
+    double tn0 = 0.0, tn1 = 0.0;
+    if constexpr (std::is_same<Node, GNode>::value) {
+        const GNode &n = nodes[t.node];  // LDS: lo, hi, lo per axis
+        h0 = box64(n.box[0][0], n.box[0][1], n.box[0][3], n.box[0][4], n.box[0][6], n.box[0][7], rk, t.closest, tn0);
+        h1 = box64(n.box[1][0], n.box[1][1], n.box[1][3], n.box[1][4], n.box[1][6], n.box[1][7], rk, t.closest, tn1);
+        l0 = n.link[0];
+        l1 = n.link[1];
+    } else {
+        const GNodeG n = nodes[t.node];
+        h0 = box64(n.b0.x, n.b0.y, n.b0.z, n.b0.w, n.b1.x, n.b1.y, rk, t.closest, tn0);
+        h1 = box64(n.b1.z, n.b1.w, n.b2.x, n.b2.y, n.b2.z, n.b2.w, rk, t.closest, tn1);
+        l0 = n.link.x;
+        l1 = n.link.y;
+    }
+    const uint32_t c0 = h0 ? (l0 >> kLinkCountShift) : 0u;
+    const uint32_t c1 = h1 ? (l1 >> kLinkCountShift) : 0u;
+    lv = c0 ? l0 + (c1 << kLinkCountShift) : l1;
+    if (c0) h0 = false;
+    if (c1) h1 = false;
+    if (h0 && h1) {
+        const bool first1 = tn1 < tn0;
+        stack.store(t.sp, first1 ? (int)l0 : (int)l1);
+        ++t.sp;
+        t.node = first1 ? (int)l1 : (int)l0;
+    } else if (h0) {
+        t.node = (int)l0;
+    } else if (h1) {
+        t.node = (int)l1;
+    } else if (t.sp == 0) {
+        t.node = -1;
+    } else {
+        --t.sp;
+        t.node = stack.load(t.sp);
+    }
+    return (c0 | c1) != 0;
+}
+
+// Sphere::hit (sphere.rs:24-51) over the leaf range: oc = center - o, a = |d|^2, h = d.oc,
+// c = |oc|^2 - r*r, disc = h*h - a*c, roots (h -+ sqrt(disc)) / a in the open (0.001, closest).
+// (h + sq) / a >= (h - sq) / a, so the far root is tried only when the near one is <= 0.001 (or
+// NaN), exactly the roots the reference's surrounds() tests accept.
+template <bool kCount>
+__device__ __forceinline__ void leaves64(const float4 *__restrict__ prims, Leaves lv, D3 o, D3 d, double a, Trav64 &t,
+                                         Counters &cnt) {
+    const int first = (int)(lv & kLinkFirstMask), count = (int)(lv >> kLinkCountShift);
+    for (int i = first; i < first + count; ++i) {
+        if (kCount) cnt.spheres++;
+        const float4 cr = prims[i];
+        const D3 oc = sub(f2d(cr.x, cr.y, cr.z), o);
+        const double h = dot(d, oc);
+        const double r = (double)cr.w;
+        const double c = dot(oc, oc) - r * r;
+        const double disc = h * h - a * c;
+        if (disc < 0.0) continue;
+        const double sq = __builtin_sqrt(disc);
+        double root = (h - sq) / a;
+        if (!(0.001 < root)) root = (h + sq) / a;
+        if (0.001 < root && root < t.closest) {
+            t.closest = root;
+            t.hit_prim = i;
+        }
+    }
+}
+
+struct Path64 {
+    D3 o, d, T;
+    RngState rng;
+    uint32_t k;  // bounce index (camera ray = 0)
+};
+
+// Camera::get_ray (camera.rs:152-180) in f64 from the f32 camera block (gpu/mod.rs:278-298 casts).
+__device__ __forceinline__ void camera_ray64(uint32_t x, uint32_t y, Path64 &ps) {
+    const auto &C = *kernarg_params();
+    const double ox = rnd64(ps.rng) - 0.5, oy = rnd64(ps.rng) - 0.5;  // sample_square
+    const double fi = (double)x + ox, fj = (double)y + oy;
+    const D3 sample = d3(((double)C.p00[0] + (double)C.du[0] * fi) + (double)C.dv[0] * fj,
+                         ((double)C.p00[1] + (double)C.du[1] * fi) + (double)C.dv[1] * fj,
+                         ((double)C.p00[2] + (double)C.du[2] * fi) + (double)C.dv[2] * fj);
+    D3 origin = f2d(C.center[0], C.center[1], C.center[2]);
+    if (C.defocus_radius > 0.0f) {
+        double px, py;
+        for (;;) {  // vec3.rs:172-179 random_in_unit_disk
+            px = rnd64_pm1(ps.rng);
+            py = rnd64_pm1(ps.rng);
+            if (px * px + py * py < 1.0) break;
+        }
+        const double rad = (double)C.defocus_radius;  // defocus_disk_u = u * radius (camera.rs:136-138)
+        const D3 du = muls(f2d(C.cam_u[0], C.cam_u[1], C.cam_u[2]), rad);
+        const D3 dv = muls(f2d(C.cam_v[0], C.cam_v[1], C.cam_v[2]), rad);
+        origin = add(add(origin, muls(du, px)), muls(dv, py));
+    }
+    if (C.flags & 0x1u) (void)rnd64(ps.rng);  // RRT_FLAG_RAY_TIME: the time draw (the_next_week/camera.rs:160)
+    ps.o = origin;
+    ps.d = sub(sample, origin);
+    ps.T = d3(1.0, 1.0, 1.0);
+    ps.k = 0;
+}
+
+// After the closest-hit query: sky / background, or emission / scatter / RR (camera.rs:182-209).
+// Returns true when the path has ended; its radiance T * Le (if any) goes into `sum`.
+__device__ __forceinline__ bool shade64(const KParams &P, const float4 *prims, const GMaterial *mtl, Path64 &ps, double t,
+                                        int prim, D3 &sum) {
+    if (prim < 0) {
+        D3 bg;
+        if (P.bg_mode == 1u) {
+            bg = f2d(P.background[0], P.background[1], P.background[2]);
+        } else {  // (1 - a) * (1, 1, 1) + a * (0.5, 0.7, 1)
+            const D3 ud = unit_vector(ps.d);
+            const double a = 0.5 * (ud.y + 1.0);
+            bg = d3((1.0 - a) * 1.0 + a * 0.5, (1.0 - a) * 1.0 + a * 0.7, (1.0 - a) * 1.0 + a * 1.0);
+        }
+        sum = add(sum, mul(ps.T, bg));
+        return true;
+    }
+    const float4 cr = prims[prim];
+    const D3 p = add(ps.o, muls(ps.d, t));  // Ray::at = orig + t * dir
+    const D3 outward = muls(sub(p, f2d(cr.x, cr.y, cr.z)), 1.0 / (double)cr.w);  // (p - center) / r
+    const bool front = dot(ps.d, outward) < 0.0;
+    const D3 nrm = front ? outward : d3(-outward.x, -outward.y, -outward.z);
+    const GMaterial m = mtl[prim];
+    const int kind = m.b.x;
+    const D3 albedo = f2d(m.a.x, m.a.y, m.a.z);
+    if (kind == 4) {  // DiffuseLight: emitted, scatter None
+        sum = add(sum, mul(ps.T, albedo));
+        return true;
+    }
+    D3 att, dir;
+    if (kind == 1) {  // Metal (material.rs:53-64): unit(reflect) + fuzz * random_unit_vector
+        const D3 refl = unit_vector(reflect(ps.d, nrm));
+        dir = add(refl, muls(random_unit_vector(ps.rng), (double)m.a.w));
+        if (!(dot(dir, nrm) > 0.0)) return true;  // absorbed
+        att = albedo;
+    } else if (kind == 2) {  // Dielectric (material.rs:83-102)
+        const double eta = (double)__int_as_float(m.b.y);
+        const double ri = front ? 1.0 / eta : eta;
+        const D3 ud = unit_vector(ps.d);
+        const double c = rmin(-dot(ud, nrm), 1.0);
+        const double sn = __builtin_sqrt(1.0 - c * c);
+        const bool cannot = ri * sn > 1.0;
+        if (cannot || reflectance(c, ri) > rnd64(ps.rng)) dir = reflect(ud, nrm);
+        else dir = refract(ud, nrm, ri);
+        att = d3(1.0, 1.0, 1.0);
+    } else {  // Lambertian, plain or image-textured (material.rs:28-40; the_next_week/material.rs:41-53)
+        dir = add(nrm, random_unit_vector(ps.rng));
+        if (__builtin_fabs(dir.x) < 1e-8 && __builtin_fabs(dir.y) < 1e-8 && __builtin_fabs(dir.z) < 1e-8) dir = nrm;
+        att = kind == 3 ? texel64(P, m.b.z, outward) : albedo;
+    }
+    if (ps.k >= 5u) {  // camera.rs:189-200
+        double pr = att.x;
+        if (att.y > pr) pr = att.y;
+        if (att.z > pr) pr = att.z;
+        if (pr < 0.05) pr = 0.05;
+        if (pr > 0.95) pr = 0.95;
+        if (rnd64(ps.rng) > pr) return true;
+        ps.T = muls(mul(ps.T, att), 1.0 / pr);
+    } else {
+        ps.T = mul(ps.T, att);
+    }
+    ps.o = p;
+    ps.d = dir;
+    ps.k++;
+    return false;
+}
+
+// The persistent work loop of rrt_kernel.hip's render_body (same queue, units, chunk order,
+// postponed leaves and wave-uniform exits) over Path64 state.
+template <bool kLds, bool kCount, int kBlk>
+__device__ __forceinline__ void render64_body(const KParams &P) {
+    extern __shared__ uint4 lds_dyn[];
+    uint16_t *lds_stack = reinterpret_cast<uint16_t *>(lds_dyn);
+    using Node = typename std::conditional<kLds, GNode, GNodeG>::type;
+    const Node *nodes = reinterpret_cast<const Node *>(P.nodes);
+    const float4 *prims = P.prim_cr;
+    const GMaterial *mtl = P.prim_mtl;
+    if constexpr (kLds) {  // stage nodes + spheres + their materials once per block
+        uint4 *dst = lds_dyn + (P.stack_depth * kBlk * sizeof(uint16_t) + 15u) / 16u;
+        const uint4 *src_n = reinterpret_cast<const uint4 *>(P.nodes);
+        const uint32_t nn = P.n_nodes * (uint32_t)(sizeof(Node) / 16);
+        for (uint32_t i = threadIdx.x; i < nn; i += kBlk) dst[i] = src_n[i];
+        const uint4 *src_p = reinterpret_cast<const uint4 *>(P.prim_cr);
+        for (uint32_t i = threadIdx.x; i < P.n_prims; i += kBlk) dst[nn + i] = src_p[i];
+        const uint4 *src_m = reinterpret_cast<const uint4 *>(P.prim_mtl);
+        const uint32_t nm = P.n_prims * (uint32_t)(sizeof(GMaterial) / 16);
+        for (uint32_t i = threadIdx.x; i < nm; i += kBlk) dst[nn + P.n_prims + i] = src_m[i];
+        __syncthreads();
+        nodes = reinterpret_cast<const Node *>(dst);
+        prims = reinterpret_cast<const float4 *>(dst + nn);
+        mtl = reinterpret_cast<const GMaterial *>(dst + nn + P.n_prims);
+    }
+    LdsStack<uint16_t, kBlk> stack;
+    stack.init(lds_stack, threadIdx.x);
+
+    const uint32_t lane = threadIdx.x & 63u;
+    Counters cnt = {0, 0, 0, 0, 0, 0};
+    uint32_t w_rays = 0, w_paths = 0;
+    uint32_t has = 0, need_ray = 0;
+    bool q_open = true;
+    uint32_t xy = 0, s = 0, s_hi = 0;
+    uint64_t pkey = 0;
+    D3 sum = d3(0.0, 0.0, 0.0);
+    Path64 ps;
+    Trav64 tr;
+    tr.node = -1;
+    uint32_t pool_base = (blockIdx.x & (kQueues - 1u)) * 64u, pool_left = 0;  // queue claims: rrt_kernel.hip
+    for (;;) {
+        __builtin_amdgcn_s_setprio(kPrioRefill);
+        const uint64_t idle = __ballot(!has);
+        if (idle != 0 && pool_left == 0 && q_open) {
+            const uint32_t xq = (pool_base >> 6) & (kQueues - 1u);
+            uint32_t k = 0;
+            if (lane == 0) k = atomicAdd(P.unit_counter + 32u * xq, 1u);
+            const uint32_t base = (__shfl(k, 0, 64) * kQueues + xq) * 64u;
+            if (base >= P.n_units) {
+                q_open = false;
+            } else {
+                pool_base = base;
+                pool_left = min(64u, P.n_units - base);
+            }
+        }
+        if (idle != 0 && pool_left != 0) {
+            const uint32_t n = min((uint32_t)__popcll(idle), pool_left);
+            const uint32_t r = (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
+            if (!has && r < n) {
+                const auto &Q = *kernarg_params();
+                const uint32_t u = pool_base + r;
+                const uint32_t lit = u & 63u, tc = u >> 6;
+                uint32_t t, chunk;  // big chunks of every tile first, then the tail chunks
+                if (u < Q.n_big_units) {
+                    t = fast_div(tc, fdiv(Q.fd_pass_big));
+                    chunk = Q.chunk_begin + (tc - t * Q.pass_big);
+                } else {
+                    const uint32_t ns = Q.pass_n - Q.pass_big, tc2 = tc - (Q.n_big_units >> 6);
+                    t = fast_div(tc2, fdiv(Q.fd_pass_tail));
+                    chunk = Q.chunk_begin + Q.pass_big + (tc2 - t * ns);
+                }
+                const uint32_t ty = fast_div(t, fdiv(Q.fd_tiles_x));
+                const uint32_t x = (t - ty * Q.tiles_x) * kTileW + (lit % kTileW);
+                const uint32_t ly = ty * kTileH + (lit / kTileW);
+                if (x < Q.width && ly < Q.tile_rows) {
+                    const uint32_t band = fast_div(ly, fdiv(Q.fd_band_rows));
+                    const uint32_t y = (band * Q.n_ranks + Q.rank) * Q.band_rows + (ly - band * Q.band_rows);
+                    xy = x | (y << 16);
+                    s = Q.sample_begin + chunk_first(Q, chunk);
+                    s_hi = min(s + (chunk < Q.n_big ? Q.chunk : Q.chunk_small), Q.sample_end);
+                    sum = d3(0.0, 0.0, 0.0);
+                    pkey = pixel_key(Q, x, y);
+                    ps.rng = path_rng_k(pkey, s);
+                    camera_ray64(x, y, ps);
+                    need_ray = 1;
+                    has = 1;
+                }
+            }
+            pool_base += n;
+            pool_left -= n;
+        }
+        if (__ballot(has) == 0) break;
+
+        uint32_t seg_done = 0, started = 0;
+        if (has && need_ray) {
+            if (ps.k >= P.max_depth) {  // ray_color: depth <= 0 -> 0 (no query)
+                seg_done = 1;
+            } else {
+                tr.closest = __builtin_inf();  // Interval(0.001, INFINITY)
+                tr.hit_prim = -1;
+                tr.node = 0;
+                tr.sp = 0;
+                need_ray = 0;
+                started = 1;
+            }
+        }
+        w_rays += (uint32_t)__popcll(__ballot(started));
+        const uint32_t live = (uint32_t)__popcll(__ballot(has));
+        const uint32_t min_active = (live * P.trav_frac) >> 8;
+        const uint32_t leaf_min = (live * P.leaf_frac) >> 8;
+        RayK64 rk;
+        double a = 0.0;
+        if (tr.node >= 0) {
+            rk = ray_consts64(ps.o, ps.d);
+            a = dot(ps.d, ps.d);  // sphere.rs:27 r.direction().length_squared()
+        }
+        __builtin_amdgcn_s_setprio(kPrioNode);
+        Leaves lv = 0;
+        for (;;) {
+            if (tr.node >= 0 && lv == 0) {
+                Leaves l;
+                if (trav_node64<kCount>(nodes, stack, rk, tr, l, cnt)) lv = l;
+            }
+            const uint64_t pm = __ballot(lv != 0);
+            const uint64_t tm = __ballot(tr.node >= 0) | pm;
+            const bool leave = (uint32_t)__popcll(tm) <= min_active;
+            const bool batch = ((uint32_t)__popcll(pm) > leaf_min) | leave | (tm == pm);
+            if ((pm != 0) & batch) {
+                __builtin_amdgcn_s_setprio(kPrioLeaf);
+                if (lv != 0) {
+                    leaves64<kCount>(prims, lv, ps.o, ps.d, a, tr, cnt);
+                    lv = 0;
+                }
+                __builtin_amdgcn_s_setprio(kPrioNode);
+            }
+            if (leave) break;
+        }
+        __builtin_amdgcn_s_setprio(kPrioShade);
+        if (has && !need_ray && tr.node < 0) {
+            need_ray = 1;
+            seg_done = shade64(P, prims, mtl, ps, tr.closest, tr.hit_prim, sum) ? 1u : 0u;
+        }
+        w_paths += (uint32_t)__popcll(__ballot(seg_done));
+        if (seg_done) {  // pixel_color += ray_color(..): already in `sum`
+            ++s;
+            const uint32_t x = xy & 0xffffu, y = xy >> 16;
+            if (s < s_hi) {
+                ps.rng = path_rng_k(pkey, s);
+                camera_ray64(x, y, ps);
+            } else {  // unit complete: the chunk's f64 sum, in sample order
+                const auto &Q = *kernarg_params();
+                const uint32_t rel = s_hi - 1u - Q.sample_begin;
+                const uint32_t nbs = Q.n_big * Q.chunk;
+                const uint32_t chunk =
+                    rel < nbs ? fast_div(rel, fdiv(Q.fd_chunk)) : Q.n_big + fast_div(rel - nbs, fdiv(Q.fd_chunk_small));
+                const uint32_t gb = fast_div(y, fdiv(Q.fd_band_rows));
+                const uint32_t ly = fast_div(gb - Q.rank, fdiv(Q.fd_n_ranks)) * Q.band_rows + (y - gb * Q.band_rows);
+                const size_t px = (size_t)ly * Q.width + x;
+                const D4 out{sum.x, sum.y, sum.z, (double)(s_hi - (Q.sample_begin + chunk_first(Q, chunk)))};
+                if (Q.n_chunks == 1) Q.accum64[px] = out;
+                else Q.partial64[(size_t)(chunk - Q.chunk_begin) * ((size_t)Q.tile_rows * Q.width) + px] = out;
+                has = 0;
+            }
+        }
+    }
+    uint32_t nv = 0, bt = 0, st = 0;
+    if (kCount) {
+        nv = wave_sum_u32(cnt.nodes);
+        bt = wave_sum_u32(cnt.boxes);
+        st = wave_sum_u32(cnt.spheres);
+    }
+    if (lane == 0) {
+        if (w_rays) atomicAdd(&P.counters[0], (unsigned long long)w_rays);
+        if (w_paths) atomicAdd(&P.counters[1], (unsigned long long)w_paths);
+        if (kCount) {
+            atomicAdd(&P.counters[2], (unsigned long long)nv);
+            atomicAdd(&P.counters[3], (unsigned long long)bt);
+            atomicAdd(&P.counters[4], (unsigned long long)st);
+        }
+    }
+}
+
+constexpr int kBlock64 = 256;  // threads per block of the f64 kernel
+
+template <bool kLds, bool kCount>
+__global__ __launch_bounds__(kBlock64) void rrt_render64(KParams P) {
+    render64_body<kLds, kCount, kBlock64>(P);
+}
+
+// The pass's f64 chunk sums into accum64, continuing the left fold over chunks in order (as
+// rrt_combine_chunks); w = the tile's sample count.
+__global__ __launch_bounds__(256) void rrt_combine_chunks64(const D4 *__restrict__ partial, D4 *__restrict__ accum,
+                                                            uint32_t n_pixels, uint32_t n_chunks, uint32_t first,
+                                                            double count) {
+    const uint32_t p = blockIdx.x * 256u + threadIdx.x;
+    if (p >= n_pixels) return;
+    D4 acc = first ? partial[p] : accum[p];
+    for (uint32_t c = first ? 1u : 0u; c < n_chunks; ++c) {
+        const D4 v = partial[(size_t)c * n_pixels + p];
+        acc.x = acc.x + v.x;
+        acc.y = acc.y + v.y;
+        acc.z = acc.z + v.z;
+    }
+    accum[p] = D4{acc.x, acc.y, acc.z, count};
+}
+
+// f64 sums rounded to the ABI's f32 RGBA accum (round to nearest: the closest f32 to each sum).
+__global__ __launch_bounds__(256) void rrt_accum64_to_f32(const D4 *__restrict__ a64, float4 *__restrict__ a32,
+                                                          uint32_t n_pixels) {
+    const uint32_t p = blockIdx.x * 256u + threadIdx.x;
+    if (p >= n_pixels) return;
+    const D4 v = a64[p];
+    a32[p] = make_float4((float)v.x, (float)v.y, (float)v.z, (float)v.w);
+}
+
+template <bool kLds>
+hipError_t launch64(const KParams &p, bool count, hipStream_t stream) {
+    size_t lds = ((size_t)p.stack_depth * kBlock64 * sizeof(uint16_t) + 15u) / 16u * 16u;
+    if (kLds) lds += (size_t)p.n_nodes * sizeof(GNode) + (size_t)p.n_prims * kPrimBytes;
+    auto kernel = count ? rrt_render64<kLds, true> : rrt_render64<kLds, false>;
+    int per_cu = 0;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock64, lds);
+    if (e != hipSuccess) return e;
+    if (per_cu < 1) per_cu = 1;
+    const uint32_t want = (p.n_units + kBlock64 - 1) / kBlock64;
+    const uint32_t blocks = std::max<uint32_t>(std::min<uint32_t>(want, (uint32_t)per_cu * p.n_cus), kQueues);
+    e = hipMemsetAsync(p.unit_counter, 0, kQueues * 32u * sizeof(uint32_t), stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(kernel, dim3(blocks), dim3(kBlock64), lds, stream, p);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_render_pass_f64(const KParams &p, bool count, hipStream_t stream) {
+    if (p.n_units == 0) return hipSuccess;
+    if (p.bvh_width != 2 || p.prim_motion || p.stack_depth > (uint32_t)kMaxStackDepth || p.n_nodes > 65535u)
+        return hipErrorInvalidValue;  // the host builds a 16-bit-stack BVH2 for book-1 scenes
+    hipError_t e = p.scene_in_lds ? launch64<true>(p, count, stream) : launch64<false>(p, count, stream);
+    if (e != hipSuccess || p.n_chunks <= 1) return e;
+    const uint32_t n_pixels = p.tile_rows * p.width;
+    hipLaunchKernelGGL(rrt_combine_chunks64, dim3((n_pixels + 255) / 256), dim3(256), 0, stream, p.partial64,
+                       p.accum64, n_pixels, p.pass_n, p.chunk_begin == 0 ? 1u : 0u,
+                       (double)(p.sample_end - p.sample_begin));
+    return hipGetLastError();
+}
+
+hipError_t launch_accum64_to_f32(const D4 *d_accum64, float4 *d_accum, uint32_t n_pixels, hipStream_t stream) {
+    if (n_pixels == 0) return hipSuccess;
+    hipLaunchKernelGGL(rrt_accum64_to_f32, dim3((n_pixels + 255) / 256), dim3(256), 0, stream, d_accum64, d_accum,
+                       n_pixels);
+    return hipGetLastError();
+}
+
+}  // namespace rrt

@@ -738,6 +738,11 @@ struct RrtScene {
     uint32_t *d_unit_counter = nullptr;             // persistent-queue head
     float4 *d_partial = nullptr;                    // chunk partial sums
     size_t partial_cap = 0;                         // float4 elements
+    bool f64 = false;                               // RRT_FLAG_F64: the books-arithmetic kernel
+    rrt::D4 *d_partial64 = nullptr;                 // its chunk partial sums
+    size_t partial64_cap = 0;                       // D4 elements
+    rrt::D4 *d_accum64 = nullptr;                   // its f64 sums behind the float entry points
+    size_t accum64_cap = 0;                         // D4 elements
     uint32_t last_groups = 0, last_passes = 0;      // the last launch: 64-unit groups per pass, passes
     rrt::KParams base{};
     RrtBvhInfo info{};
@@ -762,6 +767,8 @@ void free_scene(RrtScene *s) {
     (void)hipFree(s->d_work_counters);
     (void)hipFree(s->d_unit_counter);
     (void)hipFree(s->d_partial);
+    (void)hipFree(s->d_partial64);
+    (void)hipFree(s->d_accum64);
     delete s;
 }
 
@@ -840,18 +847,23 @@ int fill_params(RrtScene *s, const RrtTile *t, float *d_accum, rrt::KParams &p) 
     p.pass_chunks = p.n_chunks;
     if (p.n_chunks > 1) {  // partial sums [pass chunk][pixel], within the partial budget; grow on demand
         const size_t n_px = std::max<size_t>((size_t)p.tile_rows * p.width, 1);
-        p.pass_chunks = (uint32_t)std::min<size_t>(p.n_chunks, std::max<size_t>(1, partial_budget() / (n_px * sizeof(float4))));
+        const size_t elem = s->f64 ? sizeof(rrt::D4) : sizeof(float4);
+        p.pass_chunks = (uint32_t)std::min<size_t>(p.n_chunks, std::max<size_t>(1, partial_budget() / (n_px * elem)));
         const size_t need = n_px * p.pass_chunks;
-        if (need > s->partial_cap) {
+        size_t &cap = s->f64 ? s->partial64_cap : s->partial_cap;
+        void **buf = s->f64 ? (void **)&s->d_partial64 : (void **)&s->d_partial;
+        if (need > cap) {
             HIP_TRY(hipSetDevice(s->device), "hipSetDevice");
-            (void)hipFree(s->d_partial);
-            s->d_partial = nullptr;
-            s->partial_cap = 0;
-            HIP_TRY(hipMalloc((void **)&s->d_partial, need * sizeof(float4)), "hipMalloc chunk partials");
-            s->partial_cap = need;
+            (void)hipFree(*buf);
+            *buf = nullptr;
+            cap = 0;
+            HIP_TRY(hipMalloc(buf, need * elem), "hipMalloc chunk partials");
+            cap = need;
         }
     }
     p.partial = s->d_partial;
+    p.partial64 = s->d_partial64;
+    p.accum64 = nullptr;
     return RRT_OK;
 }
 
@@ -937,6 +949,11 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
     for (uint32_t i = 0; i < n_materials && materials; ++i)
         book2 = book2 || materials[i].kind == RRT_MAT_CHECKER_LAMBERTIAN || materials[i].kind == RRT_MAT_NOISE_LAMBERTIAN ||
                 materials[i].kind == RRT_MAT_ISOTROPIC;
+    static_assert(RRT_FLAG_F64 == rrt::kFlagF64, "RRT_FLAG_F64");
+    const bool f64 = (flags & RRT_FLAG_F64) != 0;
+    if (f64 && (book2 || n_perlin || ex.n_lights))
+        return fail(RRT_E_INVALID, "RRT_FLAG_F64 renders book-1 scenes (material kinds 0-4, no RrtSceneExt data, "
+                                   "not RRT_FLAG_BOOK3)");
     if (!has_motion) motion = nullptr;
     if (n_spheres && !spheres) return fail(RRT_E_INVALID, "null spheres");
     if (n_materials && !materials) return fail(RRT_E_INVALID, "null materials");
@@ -963,7 +980,7 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
     // ---- BVH over the sphere bounding boxes ----
     uint32_t width, max_leaf;
     bvh_defaults(width, max_leaf);
-    if (book2) width = 2;  // the book-2 kernel variants are BVH2 only
+    if (book2 || f64) width = 2;  // the book-2 and f64 kernels are BVH2 only
     std::vector<uint32_t> order;
     if ((uint64_t)n_spheres + n_quads + n_media >= (1u << 24) ||
         (uint64_t)n_quads + ex.n_bquads + ex.n_lights >= (1u << 24))
@@ -974,6 +991,7 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
                                  [&](size_t nb) { return scene_lds_fit(nb, n_prims_all, book2); });
     if (fb.stack_need > (uint32_t)rrt::kMaxStackDepth)
         return fail(RRT_E_INVALID, "BVH depth " + std::to_string(fb.max_depth) + " exceeds the LDS stack");
+    if (f64 && fb.n_nodes > 65535u) return fail(RRT_E_INVALID, "RRT_FLAG_F64: more than 65535 BVH nodes");
     // postponed leaf tests pack (first primitive, count) as first | count << 28
     if (fb.max_leaf > (fb.width == 2 ? rrt::kMaxLeafPrims : 15u)) return fail(RRT_E_INVALID, "leaf size too large");
     if (!fb.sibling_leaves_adjacent) return fail(RRT_E_INVALID, "internal: BVH2 sibling leaves not adjacent");
@@ -1043,7 +1061,7 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
         const RrtSphere &sp = spheres[order[i]];
         const float r = std::max(sp.center_radius[3], 0.0f);
         prim_mtl[i] = mats[sp.material_index];
-        if (book2) {
+        if (book2 || f64) {  // the f64 kernel forms r * r in f64 (sphere.rs:29)
             prim_cr[i] = make_float4(sp.center_radius[0], sp.center_radius[1], sp.center_radius[2], r);
         } else {  // book-1 kernel layout: r * r in the record (one multiply less per test), r in b.w
             const volatile float r2 = r * r;  // f32, rounded once like the kernel's r * r
@@ -1093,6 +1111,7 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
 
     RrtScene *s = new RrtScene();
     s->device = device;
+    s->f64 = f64;
     int rc = RRT_OK;
     do {
         if (hipSetDevice(device) != hipSuccess) { rc = fail(RRT_E_HIP, "hipSetDevice failed"); break; }
@@ -1154,6 +1173,8 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
         p.center[i] = cam->origin[i];
         p.disk_u[i] = cam->u[i] * radius;  // defocus_disk_u = u * defocus_radius (camera.rs:136-138)
         p.disk_v[i] = cam->v[i] * radius;
+        p.cam_u[i] = cam->u[i];
+        p.cam_v[i] = cam->v[i];
         p.background[i] = cam->background[i];
     }
     p.defocus_radius = radius;
@@ -1310,22 +1331,51 @@ int32_t rrt_tile_row_index(uint32_t height, const RrtTile *tile, uint32_t local_
     return RRT_OK;
 }
 
-int32_t rrt_render_tile_async(RrtScene *scene, const RrtTile *tile, float *d_accum, void *stream) {
+// The tile's render into d_accum (float4 rows) or, for an f64 scene, d_accum64 (D4 rows; a float
+// d_accum then receives the f64 sums rounded to f32 from the scene's own f64 buffer).
+static int32_t render_tile(RrtScene *scene, const RrtTile *tile, float *d_accum, rrt::D4 *d_accum64, void *stream) {
     if (int rc = check_tile(scene, tile)) return rc;
     rrt::KParams p;
     if (int rc = fill_params(scene, tile, d_accum, p)) return rc;
-    if (p.tile_rows && !d_accum) return fail(RRT_E_INVALID, "null d_accum");
+    if (p.tile_rows && !d_accum && !d_accum64) return fail(RRT_E_INVALID, "null d_accum");
     HIP_TRY(hipSetDevice(scene->device), "hipSetDevice");
+    const size_t n_px = (size_t)p.tile_rows * p.width;
+    if (scene->f64) {
+        p.accum64 = d_accum64;
+        if (!d_accum64 && n_px > scene->accum64_cap) {  // float output: the f64 sums go to the scene's buffer first
+            (void)hipFree(scene->d_accum64);
+            scene->d_accum64 = nullptr;
+            scene->accum64_cap = 0;
+            HIP_TRY(hipMalloc((void **)&scene->d_accum64, n_px * sizeof(rrt::D4)), "hipMalloc f64 accum");
+            scene->accum64_cap = n_px;
+        }
+        if (!d_accum64) p.accum64 = scene->d_accum64;
+    }
     if (p.n_chunks == 0) {  // no samples: accum = 0 (sums and count)
-        HIP_TRY(hipMemsetAsync(d_accum, 0, (size_t)p.tile_rows * p.width * sizeof(float4), (hipStream_t)stream),
-                "hipMemsetAsync accum");
+        if (d_accum)
+            HIP_TRY(hipMemsetAsync(d_accum, 0, n_px * sizeof(float4), (hipStream_t)stream), "hipMemsetAsync accum");
+        if (d_accum64)
+            HIP_TRY(hipMemsetAsync(d_accum64, 0, n_px * sizeof(rrt::D4), (hipStream_t)stream), "hipMemsetAsync accum");
         return RRT_OK;
     }
     HIP_TRY(rrt::launch_render(p, (hipStream_t)stream), "render kernel launch");
+    if (scene->f64 && d_accum)
+        HIP_TRY(rrt::launch_accum64_to_f32(p.accum64, reinterpret_cast<float4 *>(d_accum), (uint32_t)n_px,
+                                           (hipStream_t)stream),
+                "f64 accum conversion launch");
     const uint32_t per_pass = (p.pass_chunks == 0 || p.pass_chunks >= p.n_chunks) ? p.n_chunks : p.pass_chunks;
     scene->last_passes = (p.n_chunks + per_pass - 1) / per_pass;
     scene->last_groups = p.n_work_tiles * per_pass;
     return RRT_OK;
+}
+
+int32_t rrt_render_tile_async(RrtScene *scene, const RrtTile *tile, float *d_accum, void *stream) {
+    return render_tile(scene, tile, d_accum, nullptr, stream);
+}
+
+int32_t rrt_render_tile_f64_async(RrtScene *scene, const RrtTile *tile, double *d_accum, void *stream) {
+    if (scene && !scene->f64) return fail(RRT_E_INVALID, "rrt_render_tile_f64_async: scene not created with RRT_FLAG_F64");
+    return render_tile(scene, tile, nullptr, reinterpret_cast<rrt::D4 *>(d_accum), stream);
 }
 
 namespace {
@@ -1375,9 +1425,11 @@ int32_t rrt_scene_count_work(RrtScene *scene, const RrtTile *tile, RrtCounters *
     if (int rc = fill_params(scene, tile, nullptr, p)) return rc;
     HIP_TRY(hipSetDevice(scene->device), "hipSetDevice");
     float4 *scratch = nullptr;
-    HIP_TRY(hipMalloc((void **)&scratch, std::max<size_t>((size_t)p.tile_rows * p.width, 1) * sizeof(float4)),
+    const size_t elem = scene->f64 ? sizeof(rrt::D4) : sizeof(float4);
+    HIP_TRY(hipMalloc((void **)&scratch, std::max<size_t>((size_t)p.tile_rows * p.width, 1) * elem),
             "hipMalloc scratch accum");
     p.accum = scratch;
+    p.accum64 = reinterpret_cast<rrt::D4 *>(scratch);
     p.counters = scene->d_work_counters;
     hipError_t e = hipMemset(scene->d_work_counters, 0, 8 * sizeof(unsigned long long));
     if (e == hipSuccess) e = rrt::launch_render_counting(p, nullptr);
@@ -1393,19 +1445,32 @@ int32_t rrt_scene_count_work(RrtScene *scene, const RrtTile *tile, RrtCounters *
 // ---- one-shot drop-in (cuda/mod.rs:342-439) ---------------------------------------------
 }  // extern "C"
 
-// One-shot frame on n_gpus devices: float accum rows (accum_out) or render_io-quantised rows
-// (rgb8_out, quantised on the device) assembled into the caller's image.
+// Test mode RRT_DEVICE_WRAP=1: worker g of a one-shot render runs on device g % device_count, so
+// the multi-device path (threads, row bands, the strided copies into the caller's image) runs with
+// n_gpus > 1 on a one-GPU box (tests/test_gpu_multidevice.py). Off by default: n_gpus must not
+// exceed the visible devices.
+static bool device_wrap() {
+    const char *e = std::getenv("RRT_DEVICE_WRAP");
+    return e && std::atoi(e) != 0;
+}
+
+// One-shot frame on n_gpus devices: float accum rows (accum_out), f64 accum rows (accum64_out, the
+// RRT_FLAG_F64 kernel) or render_io-quantised rows (rgb8_out, quantised on the device) assembled
+// into the caller's image.
 static int32_t render_frame(const RrtCamera *cam, const RrtSphere *spheres, uint32_t n_spheres,
                             const RrtMaterial *materials, uint32_t n_materials, const RrtTexture *textures,
                             uint32_t n_textures, const RrtSceneExt *ext, uint32_t total_spp, uint32_t n_gpus,
-                            uint32_t flags, float *accum_out, uint8_t *rgb8_out) {
-    if (!cam || (!accum_out && !rgb8_out)) return fail(RRT_E_INVALID, "null camera or output buffer");
+                            uint32_t flags, float *accum_out, uint8_t *rgb8_out, double *accum64_out = nullptr) {
+    if (!cam || (!accum_out && !rgb8_out && !accum64_out)) return fail(RRT_E_INVALID, "null camera or output buffer");
+    if (accum64_out) flags |= RRT_FLAG_F64;
     if (total_spp == 0) total_spp = (uint32_t)std::max(cam->params_f[3], 1.0f);  // cuda/mod.rs:384
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(RRT_E_NODEV, "no HIP device available");
     if (n_gpus == 0) n_gpus = 1;
-    if ((int)n_gpus > ndev)
+    const bool wrap = device_wrap();
+    if ((int)n_gpus > ndev && !wrap)
         return fail(RRT_E_INVALID, "n_gpus=" + std::to_string(n_gpus) + " > visible devices " + std::to_string(ndev));
+    if (n_gpus > 64) return fail(RRT_E_INVALID, "n_gpus > 64");
     const uint32_t width = (uint32_t)cam->params_f[1];
     const uint32_t height = (uint32_t)cam->params_f[2];
 
@@ -1424,15 +1489,16 @@ static int32_t render_frame(const RrtCamera *cam, const RrtSphere *spheres, uint
         };
         RrtScene *scene = nullptr;
         int rc = scene_create(cam, spheres, n_spheres, materials, n_materials, textures, n_textures, ext, flags,
-                              (int32_t)g, &scene);
+                              (int32_t)(g % (uint32_t)ndev), &scene);
         if (rc) return set_err(rc);
         const RrtTile tile{16u, g, n_gpus, 0u, total_spp};
         const uint32_t rows = tile_rows_of(height, tile);
         const size_t n_px = (size_t)rows * width;
-        const size_t row_bytes = rgb8_out ? (size_t)width * 3 : (size_t)width * 16;
+        const size_t px_bytes = accum64_out ? sizeof(rrt::D4) : sizeof(float4);
+        const size_t row_bytes = rgb8_out ? (size_t)width * 3 : (size_t)width * px_bytes;
         float *d_accum = nullptr;
         uint8_t *d_rgb8 = nullptr;
-        hipError_t e = hipMalloc((void **)&d_accum, std::max<size_t>(n_px, 1) * 16);
+        hipError_t e = hipMalloc((void **)&d_accum, std::max<size_t>(n_px, 1) * px_bytes);
         if (e == hipSuccess && rgb8_out) e = hipMalloc((void **)&d_rgb8, std::max<size_t>(n_px, 1) * 3);
         if (e != hipSuccess) {
             (void)hipFree(d_accum);
@@ -1440,7 +1506,8 @@ static int32_t render_frame(const RrtCamera *cam, const RrtSphere *spheres, uint
             g_err = std::string("hipMalloc output failed: ") + hipGetErrorString(e);
             return set_err(RRT_E_NOMEM);
         }
-        rc = rrt_render_tile_async(scene, &tile, d_accum, nullptr);
+        rc = accum64_out ? rrt_render_tile_f64_async(scene, &tile, reinterpret_cast<double *>(d_accum), nullptr)
+                         : rrt_render_tile_async(scene, &tile, d_accum, nullptr);
         if (!rc && !(flags & RRT_FLAG_QUIET)) {
             // within-GPU progress (the reference prints one line per sample pass, cuda/mod.rs:426-431):
             // poll the work-queue heads every 100 ms while the kernel runs
@@ -1490,7 +1557,8 @@ static int32_t render_frame(const RrtCamera *cam, const RrtSphere *spheres, uint
             // contiguous on both sides, so one strided 2-D copy places every whole band (its
             // image rows are band * n_ranks + rank) and one plain copy the partial last band
             const uint8_t *src = rgb8_out ? (const uint8_t *)d_rgb8 : (const uint8_t *)d_accum;
-            uint8_t *dst = rgb8_out ? rgb8_out : reinterpret_cast<uint8_t *>(accum_out);
+            uint8_t *dst = rgb8_out ? rgb8_out
+                                    : accum64_out ? reinterpret_cast<uint8_t *>(accum64_out) : reinterpret_cast<uint8_t *>(accum_out);
             const size_t band_bytes = (size_t)tile.band_rows * row_bytes;
             const uint32_t whole = rows / tile.band_rows, rest = rows % tile.band_rows;
             e = hipDeviceSynchronize();
@@ -1548,6 +1616,15 @@ int32_t rrt_hip_render_ex(const RrtCamera *cam, const RrtSphere *spheres, uint32
     if (!accum_out) return fail(RRT_E_INVALID, "null camera or accum_out");
     return render_frame(cam, spheres, n_spheres, materials, n_materials, textures, n_textures, ext, total_spp,
                         n_gpus, flags, accum_out, nullptr);
+}
+
+int32_t rrt_hip_render_f64(const RrtCamera *cam, const RrtSphere *spheres, uint32_t n_spheres,
+                           const RrtMaterial *materials, uint32_t n_materials, const RrtTexture *textures,
+                           uint32_t n_textures, uint32_t total_spp, uint32_t n_gpus, uint32_t flags,
+                           double *accum_out) {
+    if (!accum_out) return fail(RRT_E_INVALID, "null camera or accum_out");
+    return render_frame(cam, spheres, n_spheres, materials, n_materials, textures, n_textures, nullptr, total_spp,
+                        n_gpus, flags | RRT_FLAG_F64, nullptr, nullptr, accum_out);
 }
 
 int32_t rrt_hip_render_rgb8(const RrtCamera *cam, const RrtSphere *spheres, uint32_t n_spheres,
@@ -2268,7 +2345,8 @@ static inline uint8_t books_channel(double x) {
     return v != v ? (uint8_t)0 : (uint8_t)(int32_t)v;
 }
 
-static void quantize_rgb8_books(size_t n_px, const float *accum, uint32_t spp, uint8_t *rgb8) {
+template <class T>
+static void quantize_rgb8_books(size_t n_px, const T *accum, uint32_t spp, uint8_t *rgb8) {
     const double scale = 1.0 / (double)spp;  // camera.rs:107 pixel_samples_scale (spp >= 1)
     parallel_chunks(n_px, 1u << 16, [&](size_t b, size_t e, unsigned) {
         for (size_t i = b; i < e; ++i)
@@ -2360,6 +2438,14 @@ int32_t rrt_quantize_accum(uint32_t width, uint32_t height, const float *accum, 
 }
 
 int32_t rrt_quantize_accum_books(uint32_t width, uint32_t height, const float *accum, uint32_t spp, uint8_t *rgb8) {
+    if ((!accum || !rgb8) && (size_t)width * height) return fail(RRT_E_INVALID, "null accum or rgb8");
+    if (spp == 0) return fail(RRT_E_INVALID, "samples_per_pixel must be >= 1 (camera.rs pixel_samples_scale)");
+    quantize_rgb8_books((size_t)width * height, accum, spp, rgb8);
+    return RRT_OK;
+}
+
+int32_t rrt_quantize_accum_books_f64(uint32_t width, uint32_t height, const double *accum, uint32_t spp,
+                                     uint8_t *rgb8) {
     if ((!accum || !rgb8) && (size_t)width * height) return fail(RRT_E_INVALID, "null accum or rgb8");
     if (spp == 0) return fail(RRT_E_INVALID, "samples_per_pixel must be >= 1 (camera.rs pixel_samples_scale)");
     quantize_rgb8_books((size_t)width * height, accum, spp, rgb8);

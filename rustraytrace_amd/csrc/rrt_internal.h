@@ -117,6 +117,12 @@ __host__ __device__ inline uint32_t fast_div(uint32_t n, FastDiv f) {
     return (uint32_t)((((uint64_t)n * f.m) >> 32) + n) >> f.s;
 }
 
+// f64 sums of the books path: RGB + sample count (32 B; two 16-B stores)
+struct alignas(16) D4 {
+    double x, y, z, w;
+};
+static_assert(sizeof(D4) == 32, "D4 must be 32 B");
+
 struct KParams {
     const void *nodes;           // GNode[] (bvh_width 2) or GNode4[] (bvh_width 4)
     const float4 *prim_cr;       // sphere center.xyz, radius — in BVH leaf order
@@ -201,7 +207,19 @@ struct KParams {
     uint32_t *unit_counter;   // device queue heads: kQueues counters 128 B apart (zeroed per launch)
     float4 *partial;          // [pass chunk][tile pixel] partial sums when n_chunks > 1: a chunk's
                               // pixels are contiguous, so an 8x8 tile's rows fill whole 128-B lines
+
+    // The f64 books path (flags & kFlagF64, rrt_books64.hip); appended so the f32 kernels' field
+    // offsets stay unchanged. Sums and chunk partials as D4 (RGB sums, w = count) in the same
+    // layouts as accum / partial; the camera's raw u, v (defocus_disk_u = u * defocus_radius is
+    // formed in f64, camera.rs:136-138).
+    D4 *accum64;
+    D4 *partial64;
+    float cam_u[3];
+    float cam_v[3];
 };
+
+// RRT_FLAG_F64 (include/rrt_hip.h): the f64 books-arithmetic kernel (rrt_books64.hip)
+constexpr uint32_t kFlagF64 = 0x8u;
 
 // Traversal stack entries held in LDS per lane: up to 64 (BVH depth <= 63).
 constexpr int kMaxStackDepth = 64;
@@ -248,5 +266,9 @@ hipError_t launch_render(const KParams &p, hipStream_t stream);
 hipError_t launch_render_counting(const KParams &p, hipStream_t stream);
 // render_io quantiser on the device (d_accum: n_pixels x float4; d_rgb8: n_pixels x 3 B).
 hipError_t launch_quantize(const float *d_accum, uint8_t *d_rgb8, uint32_t n_pixels, float scale, hipStream_t stream);
+// Implemented in rrt_books64.hip: one sample pass of the f64 books kernel (+ its chunk combine)
+// into p.accum64, and the f64 sums rounded to the f32 RGBA accum of the ABI.
+hipError_t launch_render_pass_f64(const KParams &p, bool count, hipStream_t stream);
+hipError_t launch_accum64_to_f32(const D4 *d_accum64, float4 *d_accum, uint32_t n_pixels, hipStream_t stream);
 
 }  // namespace rrt

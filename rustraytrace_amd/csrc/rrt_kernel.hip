@@ -53,10 +53,8 @@ namespace {
 #define RRT_PRIO_SHADE 0
 #endif
 
-// 64 if the calling lane is the wave's first active lane, else 0 (wave-level event count).
-__device__ __forceinline__ uint32_t wave_slot() {
-    return (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x) == threadIdx.x ? 64u : 0u;
-}
+#include "rrt_device.h"
+
 
 
 struct V3 {
@@ -81,50 +79,6 @@ __device__ __forceinline__ V3 unit(V3 v) {
     return muls(v, inv);
 }
 
-// ---- RNG: xoshiro128+ per path, keyed by (seed, pixel, sample) ------------------------------
-// Counter-based in effect: the i-th draw of a path is a pure function of
-// (seed, global pixel index, sample index, i); nothing depends on lane or launch shape.
-// xoshiro128+ (Blackman & Vigna) is all full-rate 32-bit VALU (add, shift, xor, alignbit):
-// 8 instructions per draw against ~17 with three quarter-rate multiplies for the 64-bit LCG
-// of a PCG32 (+4.3 % on C2, same-box A/B). Only the top 24 bits of each output are used
-// (random_double), the bits the authors recommend for floating-point generation.
-__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
-    z += 0x9e3779b97f4a7c15ull;
-    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
-    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
-    return z ^ (z >> 31);
-}
-struct RngState {
-    uint32_t a, b, c, d;
-};
-__device__ __forceinline__ uint32_t rotl32(uint32_t x, int k) { return (x << k) | (x >> (32 - k)); }
-__device__ __forceinline__ uint32_t rng_next(RngState &s) {
-    const uint32_t r = s.a + s.d;
-    const uint32_t t = s.b << 9;
-    s.c ^= s.a;
-    s.d ^= s.b;
-    s.b ^= s.c;
-    s.a ^= s.d;
-    s.c ^= t;
-    s.d = rotl32(s.d, 11);
-    return r;
-}
-// state = (z, pixel key); the low bit of the last word is forced so the state is never zero
-__device__ __forceinline__ RngState rng_seed(uint64_t z, uint64_t key) {
-    return RngState{(uint32_t)z, (uint32_t)(z >> 32), (uint32_t)key, (uint32_t)(key >> 32) | 1u};
-}
-// 64 bits of the state (the media draws' key at a segment start)
-__device__ __forceinline__ uint64_t rng_key(const RngState &s) { return (uint64_t)s.a | ((uint64_t)s.b << 32); }
-// random_double(): 24-bit uniform in [0,1) (exact in f32 and f64).
-__device__ __forceinline__ float rnd(RngState &s) { return (float)(rng_next(s) >> 8) * 0x1.0p-24f; }
-// random_double_range(lo,hi) = u*(hi-lo) + lo  (rand 0.8 UniformFloat::sample_single order)
-__device__ __forceinline__ float rnd_range(RngState &s, float lo, float hi) { return rnd(s) * (hi - lo) + lo; }
-// rnd_range(s, -1, 1) in one rounding less work: u * 2^-24 * 2 is exact (power-of-two scalings
-// of a 24-bit integer), so u * 2^-23 - 1 rounds once, at the add — and fma(u, 2^-23, -1) rounds
-// the same exact product once: identical bits in one instruction.
-__device__ __forceinline__ float rnd_pm1(RngState &s) {
-    return __builtin_fmaf((float)(rng_next(s) >> 8), 0x1.0p-23f, -1.0f);
-}
 
 // vec3.rs:181-189 random_unit_vector: rejection in [-1,1)^3, accept 1e-160 < |p|^2 <= 1
 // (1e-160 underflows to 0 in f32: the one intentional f32 deviation).
@@ -244,11 +198,6 @@ __device__ __forceinline__ bool box_hit_ordered(float nx, float fx, float ny, fl
     return nr < fr;
 }
 
-// Per-lane work counts of the instrumented (counting) kernel variant (+ debug statistics).
-struct Counters {
-    uint32_t nodes, boxes, spheres;
-    uint32_t d0, d1, d2;
-};
 
 // Per-ray constants of the box and sphere tests. Recomputed from (o, d) each time a wave
 // enters its traversal loop rather than kept alive across shading (same IEEE ops, so the
@@ -521,22 +470,6 @@ __device__ __forceinline__ void test_range(const PR &prim_cr, int first, int cou
     }
 }
 
-// Traversal stack in LDS. 16-bit entries: the dword at (depth, wave, k) holds lanes k and
-// k+32, which the LDS serves in different cycles (2 x 32-lane groups), so no bank conflicts.
-template <typename StackT, int kBlk>
-struct LdsStack {
-    StackT *base;
-    __device__ __forceinline__ void init(StackT *lds, uint32_t tid) {
-        if constexpr (sizeof(StackT) == 2) {
-            const uint32_t lane = tid & 63u;
-            base = lds + (tid & ~63u) + ((lane & 31u) << 1) + (lane >> 5);
-        } else {
-            base = lds + tid;
-        }
-    }
-    __device__ __forceinline__ void store(int sp, int v) { base[sp * kBlk] = (StackT)v; }
-    __device__ __forceinline__ int load(int sp) const { return (int)base[sp * kBlk]; }
-};
 
 // Resumable BVH traversal: one call = one node. The state lives in registers (+ the LDS stack)
 // so a wave can leave the traversal loop while some lanes are still mid-tree.
@@ -554,9 +487,6 @@ __device__ __forceinline__ void trav_begin(Trav &t) {
     t.sp = 0;
 }
 
-// A lane's postponed leaf tests: primitives [first, first + count), packed first | count << 28
-// like a GNode leaf link (count <= 2 x kMaxLeafPrims = 14, primitive indices < 2^28).
-using Leaves = uint32_t;
 
 // BVH2 node visit with postponed leaf tests: tests both child boxes against the current
 // closest hit, records leaf children in `lv` (tested later, before this lane's next node
@@ -722,17 +652,6 @@ __device__ __forceinline__ int exit_skip(bool is_quad, bool is_medium, bool fron
 }
 
 // Camera::get_ray (camera.rs:152-180) for global pixel (x, y) and the path's RNG.
-// The camera block re-read from the kernarg segment at each use (scalar loads through the scalar
-// cache) rather than 19 values the compiler would hold in SGPRs across the whole work loop: the
-// asm makes the pointer opaque, so the loads cannot be hoisted out of the loop.
-__device__ __forceinline__ const __attribute__((address_space(4))) KParams *kernarg_params() {
-    auto q = (const __attribute__((address_space(4))) KParams *)__builtin_amdgcn_kernarg_segment_ptr();
-    asm volatile("" : "+s"(q));
-    return q;
-}
-// a FastDiv member read through either view of the parameters
-template <class FD>
-__device__ __forceinline__ FastDiv fdiv(const FD &f) { return FastDiv{f.m, f.s}; }
 template <bool kStrat>
 __device__ __forceinline__ void camera_ray(const KParams &P, uint32_t x, uint32_t y, uint32_t s, PathState &ps) {
     const auto &C = *kernarg_params();
@@ -772,14 +691,6 @@ __device__ __forceinline__ void camera_ray(const KParams &P, uint32_t x, uint32_
     ps.k = 0;
 }
 
-// The path's RNG stream for sample s of global pixel (x, y): xoshiro128+ state
-// (z, key | 1 << 32) with key = splitmix64((seed << 32) ^ pixel) and z = splitmix64(key + s).
-// The key is computed once per work unit (pixel, sample chunk) and held (+0.6 % on C2).
-template <class KP>
-__device__ __forceinline__ uint64_t pixel_key(const KP &P, uint32_t x, uint32_t y) {
-    return splitmix64(((uint64_t)P.seed << 32) ^ (uint64_t)(y * P.width + x));
-}
-__device__ __forceinline__ RngState path_rng_k(uint64_t key, uint32_t s) { return rng_seed(splitmix64(key + s), key); }
 __device__ __forceinline__ RngState path_rng(const KParams &P, uint32_t x, uint32_t y, uint32_t s) {
     const uint64_t key = pixel_key(P, x, y);
     return rng_seed(splitmix64(key + s), key);
@@ -1233,17 +1144,6 @@ __device__ __forceinline__ bool shade_b3(const KParams &P, const PR &prims, cons
     return false;
 }
 
-// First sample (relative to sample_begin) of chunk c of a pixel (rrt_accum_chunk's schedule).
-template <class KP>
-__device__ __forceinline__ uint32_t chunk_first(const KP &P, uint32_t c) {
-    return c < P.n_big ? c * P.chunk : P.n_big * P.chunk + (c - P.n_big) * P.chunk_small;
-}
-
-__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    return v;
-}
 
 template <bool kLds, bool kCount, typename StackT, bool kWide, int kBook2, int kBlk>
 __device__ __forceinline__ void render_body(const KParams &P) {
@@ -1685,6 +1585,7 @@ hipError_t launch_width(const KParams &p, bool count, hipStream_t stream) {
 }  // namespace
 
 hipError_t launch_render_pass(const KParams &p, bool count, hipStream_t stream) {
+    if (p.flags & kFlagF64) return launch_render_pass_f64(p, count, stream);  // the f64 books path
     // Variant choice: BVH width, smallest LDS stack that holds the traversal, and the scene
     // staged in LDS when the BVH + spheres fit the per-block budget (RTOW: ~20-26 KB).
     // Book-2 scenes (moving spheres, checker / noise textures): BVH2 only (the host builds a

@@ -88,6 +88,23 @@ def render(scene: SceneData, spp: Optional[int] = None, n_gpus: int = 1, quiet: 
     return accum
 
 
+def render_f64(scene: SceneData, spp: Optional[int] = None, n_gpus: int = 1, quiet: bool = True) -> np.ndarray:
+    """rrt_hip_render_f64: the books path's own f64 arithmetic (RRT_FLAG_F64, book-1 scenes);
+    returns the RGBA float64 accum (H, W, 4) of f64 sums, w = sample count."""
+    lib = _lib.load()
+    if getattr(scene, "motion", None) is not None or getattr(scene, "quads", None) is not None:
+        raise ValueError("render_f64: book-1 scenes only (RRT_FLAG_F64)")
+    accum = np.zeros((scene.height, scene.width, 4), dtype=np.float64)
+    tex, ntex, keep = _textures(scene)
+    flags = scene.flags | _lib.FLAG_F64 | (_lib.FLAG_QUIET if quiet else 0)
+    _lib.check(lib.rrt_hip_render_f64(_lib.ptr(scene.camera), _lib.ptr(scene.spheres), len(scene.spheres),
+                                      _lib.ptr(scene.materials), len(scene.materials),
+                                      ctypes.cast(tex, ctypes.c_void_p) if tex is not None else None, ntex,
+                                      int(spp or 0), int(n_gpus), flags, _lib.ptr(accum)))
+    del keep
+    return accum
+
+
 def render_rgb8(scene: SceneData, spp: Optional[int] = None, n_gpus: int = 1, quiet: bool = True) -> np.ndarray:
     """rrt_hip_render_rgb8_ex: render and quantise on the device (render_io.rs quantiser);
     returns (H, W, 3) uint8, identical to quantize_accum(render(scene)) at the same spp, for
@@ -176,6 +193,15 @@ def quantize_accum_books(width: int, height: int, accum: np.ndarray, samples_per
     return out
 
 
+def quantize_accum_books_f64(width: int, height: int, accum: np.ndarray, samples_per_pixel: int) -> np.ndarray:
+    """color.rs:6-32 write_color over f64 sums (render_f64): the books path's bytes, (H, W, 3) uint8."""
+    accum = np.ascontiguousarray(accum, dtype=np.float64)
+    out = np.zeros((height, width, 3), dtype=np.uint8)
+    _lib.check(_lib.load().rrt_quantize_accum_books_f64(width, height, _lib.ptr(accum), samples_per_pixel,
+                                                        _lib.ptr(out)))
+    return out
+
+
 def device_count() -> int:
     n = ctypes.c_int32(0)
     _lib.check(_lib.load().rrt_device_count(ctypes.byref(n)))
@@ -251,9 +277,11 @@ def make_tile(band_rows=16, rank=0, n_ranks=1, sample_begin=0, sample_end=0) -> 
 class DeviceScene:
     """RrtScene*: scene + BVH resident on one device; renders tiles asynchronously on a stream."""
 
-    def __init__(self, scene: SceneData, device: int = 0):
+    def __init__(self, scene: SceneData, device: int = 0, f64: bool = False):
+        """f64=True: the books path's f64 kernel (RRT_FLAG_F64, book-1 scenes)."""
         lib = _lib.load()
         self.scene = scene
+        flags = scene.flags | (_lib.FLAG_F64 if f64 else 0)
         self._lib = lib
         self._h = ctypes.c_void_p()
         tex, ntex, keep = _textures(scene)
@@ -262,11 +290,11 @@ class DeviceScene:
         if ext is None:
             _lib.check(lib.rrt_scene_create(_lib.ptr(scene.camera), _lib.ptr(scene.spheres), len(scene.spheres),
                                             _lib.ptr(scene.materials), len(scene.materials), texp, ntex,
-                                            scene.flags, int(device), ctypes.byref(self._h)))
+                                            flags, int(device), ctypes.byref(self._h)))
         else:
             _lib.check(lib.rrt_scene_create_ex(_lib.ptr(scene.camera), _lib.ptr(scene.spheres), len(scene.spheres),
                                                _lib.ptr(scene.materials), len(scene.materials), texp, ntex,
-                                               ctypes.byref(ext), scene.flags, int(device), ctypes.byref(self._h)))
+                                               ctypes.byref(ext), flags, int(device), ctypes.byref(self._h)))
         del keep, keep_ext
 
     def close(self):
@@ -297,6 +325,11 @@ class DeviceScene:
     def render_tile_async(self, tile, d_accum_ptr: int, stream_ptr: int = 0) -> None:
         _lib.check(self._lib.rrt_render_tile_async(self._h, ctypes.byref(tile), ctypes.c_void_p(d_accum_ptr),
                                                    ctypes.c_void_p(stream_ptr)))
+
+    def render_tile_f64_async(self, tile, d_accum_ptr: int, stream_ptr: int = 0) -> None:
+        """rrt_render_tile_f64_async: f64 sums (rows x W x 4 doubles) of a DeviceScene(f64=True)."""
+        _lib.check(self._lib.rrt_render_tile_f64_async(self._h, ctypes.byref(tile), ctypes.c_void_p(d_accum_ptr),
+                                                       ctypes.c_void_p(stream_ptr)))
 
     def counters(self) -> dict:
         c = _lib.RrtCounters()

@@ -1,0 +1,109 @@
+"""The f64 books path (RRT_FLAG_F64, rrt_books64.hip) against the oracle's f64 BOOKS restatement:
+the north star's correctness check "against the repo's own CPU books path on identical scene + RNG
+seed (per-channel float tolerance <= 1e-4 before u8 quantisation; bit-exact PPM after)".
+
+The kernel runs the books path's arithmetic (vec3.rs, sphere.rs:24-51, material.rs, camera.rs:
+152-209 in f64, unfused, the reference's operation order) on the same per-path random stream, so
+every path takes the same decisions as BOOKS: the closest-hit query counts are equal, and the only
+difference left is the throughput product's association (BOOKS multiplies back to front through
+its recursion, the kernel front to back) — a few f64 ulps per pixel sum. Bars, with the tolerance
+written here: every channel |gpu - books| / S <= 1e-4 (the north star's; measured max ~1e-15), the
+query counts equal, and the bytes of color.rs's f64 quantiser equal for every pixel.
+"""
+import numpy as np
+import pytest
+
+import rustraytrace_amd as rrt
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-4  # north star: per-channel float tolerance before u8 quantisation
+
+
+def _gpu_f64(scene, rows=None):
+    import torch
+
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    ds = rrt.DeviceScene(scene, device=0, f64=True)
+    tile = ds.tile(16, 0, 1, 0, scene.spp)
+    n_rows = ds.tile_rows(tile)
+    buf = torch.full((n_rows, scene.width, 4), float("nan"), dtype=torch.float64, device="cuda:0")
+    ds.reset_counters()
+    ds.render_tile_f64_async(tile, buf.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    rays = int(ds.counters()["rays"])
+    # the float entry on the same scene: the f64 sums rounded to f32
+    buf32 = torch.full((n_rows, scene.width, 4), float("nan"), dtype=torch.float32, device="cuda:0")
+    ds.render_tile_async(tile, buf32.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    out, out32 = buf.cpu().numpy(), buf32.cpu().numpy()
+    ds.close()
+    return out, out32, rays
+
+
+def _check(scene, gpu, books, label):
+    S = scene.spp
+    assert np.array_equal(gpu[..., 3], books[..., 3])  # w = sample count
+    err = np.abs(gpu[..., :3] - books[..., :3]) / S
+    within = float((err <= TOL).mean())
+    rel = float((np.abs(gpu[..., :3] - books[..., :3]) / np.maximum(np.abs(books[..., :3]), 1e-300)).max())
+    q_gpu = rrt.quantize_accum_books_f64(scene.width, gpu.shape[0], np.ascontiguousarray(gpu), S)
+    q_books = rrt.quantize_accum_books_f64(scene.width, books.shape[0], np.ascontiguousarray(books), S)
+    u8_equal = float((q_gpu == q_books).mean())
+    print(f"{label}: max |diff|/S {err.max():.3e} max rel {rel:.3e} within 1e-4 {within:.6f} u8 equal {u8_equal:.6f}")
+    assert within == 1.0, f"{label}: {1 - within:.2e} of channels outside {TOL}"
+    assert u8_equal == 1.0, f"{label}: {int((q_gpu != q_books).sum())} PPM bytes differ"
+    return rel
+
+
+@pytest.mark.parametrize("cfg", ["C1", "C2", "C4", "C5"])
+def test_f64_kernel_matches_books_path(cfg):
+    scene = rrt.config_scene(cfg, image_width=64, samples_per_pixel=256)
+    gpu, gpu32, gpu_rays = _gpu_f64(scene)
+    books, books_rays, _ = oracle.render(scene, oracle.BOOKS, threads=16)
+    assert gpu_rays == books_rays, f"{cfg}: {gpu_rays} closest-hit queries vs BOOKS {books_rays}"
+    rel = _check(scene, gpu, books, cfg)
+    assert rel < 1e-12  # a few f64 ulps of throughput association, nothing else
+    assert np.array_equal(gpu32, gpu.astype(np.float32))
+    # the PPM the books path prints (camera.rs:87-94) and the one from the GPU's f64 sums
+    q = rrt.quantize_accum_books_f64(scene.width, scene.height, gpu, scene.spp)
+    qb = rrt.quantize_accum_books_f64(scene.width, scene.height, books, scene.spp)
+    assert rrt.format_pnm_from_rgb8(scene.width, scene.height, q) == rrt.format_pnm_from_rgb8(scene.width,
+                                                                                              scene.height, qb)
+
+
+def test_f64_one_shot_render_and_ppm():
+    scene = rrt.config_scene("C2", image_width=48, samples_per_pixel=64)
+    accum = rrt.render_f64(scene)
+    books, _, _ = oracle.render(scene, oracle.BOOKS, threads=16)
+    _check(scene, accum, books, "C2 one-shot")
+
+
+@pytest.mark.parametrize("cfg,rows", [("C2", (536, 552)), ("C4", (536, 544)), ("C5", (600, 608))])
+def test_f64_full_size_rows_match_books(cfg, rows):
+    """Full BASELINE resolution and spp (C2 1920x1080x512, C4 x1024, C5 x256): the GPU renders the
+    whole frame in f64; the oracle renders a band of rows of it in f64 (seconds on 16 threads)."""
+    scene = rrt.config_scene(cfg)
+    gpu, _, _ = _gpu_f64(scene)
+    y0, y1 = rows
+    books, _, _ = oracle.render(scene, oracle.BOOKS, rows=rows, threads=16)
+    _check(scene, gpu[y0:y1], books, f"{cfg} rows {y0}-{y1}")
+    assert np.all(gpu[..., 3] == scene.spp)
+    assert np.isfinite(gpu).all()
+
+
+def test_f64_rejects_book2_scenes():
+    sc = rrt.next_week_scene(1, dict(image_width=32, samples_per_pixel=4, max_depth=4))
+    with pytest.raises(rrt.RrtError, match="RRT_FLAG_F64"):
+        rrt.DeviceScene(sc, device=0, f64=True)
+
+
+def test_f64_sample_passes_are_bit_identical(monkeypatch):
+    """The chunk partials in bounded sample passes continue one f64 fold: the bits do not depend
+    on the partial budget (RRT_PARTIAL_MB)."""
+    scene = rrt.config_scene("C2", image_width=64, samples_per_pixel=600)
+    a, _, _ = _gpu_f64(scene)
+    monkeypatch.setenv("RRT_PARTIAL_MB", "1")
+    b, _, _ = _gpu_f64(scene)
+    assert np.array_equal(a, b)

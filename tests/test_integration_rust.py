@@ -34,6 +34,8 @@ RUST_TO_C = {
     "f32": "float",
     "*mut f32": "float *",
     "*const f32": "const float *",
+    "*mut f64": "double *",
+    "*const f64": "const double *",
     "*mut u8": "uint8_t *",
     "*const u8": "const uint8_t *",
     "*mut i32": "int32_t *",
