@@ -64,6 +64,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-breakdown", action="store_true", help="skip the wall-clock split (one extra frame)")
     ap.add_argument("--no-extra", action="store_true", help="skip the 1-GPU C3 frame and the C1 timings")
+    ap.add_argument("--no-f64", action="store_true", help="skip the f64 books-arithmetic frame (f64_books)")
+    ap.add_argument("--issue-json", default=None,
+                    help="issue-side PMC record (tools/pmc_issue.py); default profiles/issue_<config>.json")
     ap.add_argument("--traffic-json", default=None,
                     help="per-launch HBM bytes from rocprofv3 PMC passes (tools/pmc_traffic.py); "
                          "default profiles/traffic_<config>.json")
@@ -194,6 +197,43 @@ def c3_one_gpu():
             "mrays_s": round(rays / wall / 1e6, 2)}
 
 
+def f64_books_frame(config, frames=2):
+    """The same workload through the f64 books-arithmetic kernel (RRT_FLAG_F64, rrt_books64.hip):
+    the reference CPU path's own arithmetic on the GPU, which tests/test_gpu_books64.py checks
+    against the f64 books restatement (every channel within 1e-4, identical PPM bytes). One warmup
+    frame, then `frames` frames timed with HIP events on the render stream; rays counted on the
+    device. Not the headline (the headline is the f32 kernel, the reference GPU slot's precision)."""
+    import numpy as np
+    import torch
+
+    import rustraytrace_amd as rrt
+
+    scene = rrt.config_scene(config)
+    ds = rrt.DeviceScene(scene, f64=True)
+    tile = ds.tile(BAND_ROWS, 0, 1, 0, scene.spp)
+    buf = torch.empty((scene.height, scene.width, 4), dtype=torch.float64, device="cuda")
+    stream = torch.cuda.current_stream()
+    ds.render_tile_f64_async(tile, buf.data_ptr(), stream.cuda_stream)
+    torch.cuda.synchronize()
+    ds.reset_counters()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(frames + 1)]
+    t = time.perf_counter()
+    for i in range(frames):
+        ev[i].record(stream)
+        ds.render_tile_f64_async(tile, buf.data_ptr(), stream.cuda_stream)
+    ev[frames].record(stream)
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t) / frames
+    ms = float(np.mean([ev[i].elapsed_time(ev[i + 1]) for i in range(frames)]))
+    rays = ds.counters()["rays"] // frames
+    ds.close()
+    return {"workload": f"{config} {scene.width}x{scene.height}x{scene.spp}spp, f64 books arithmetic (RRT_FLAG_F64)",
+            "dtype": "f64", "value": round(rays / wall / 1e6, 2), "unit": "Mrays/s", "ms_per_frame": round(wall * 1e3, 3),
+            "kernel_ms": round(ms, 3), "rays_per_frame": rays, "frames": frames,
+            "parity": "tests/test_gpu_books64.py: closest-hit counts equal to the f64 books restatement, every "
+                      "channel within 1e-4 (max |diff|/S ~1e-16), every PPM byte equal"}
+
+
 def wall_clock_breakdown(scene, accum, kernel_ms):
     """SURVEY 8(d) split of one frame through the library, measured outside the timed region on
     rank 0: host BVH build, scene creation (BVH build + H2D upload), kernel (the timed loop's
@@ -256,6 +296,29 @@ def load_traffic(path, config, W, S, lib_path):
            f"FETCH_SIZE x2 (gfx950 correction, MI355X_MICROARCH.md HBM section) + WRITE_SIZE, "
            f"{'this' if same else 'an earlier'} librrt_hip.so build ({tj.get('lib_sha256', '')[:12]})")
     return tj.get("hbm_bytes_per_launch_fetch_corrected", tj.get("hbm_bytes_per_launch")), src
+
+
+def load_issue(path, config, W, S, lib_path):
+    """valu_busy / lanes_per_valu / valu_insts_per_ray of this config from a tools/pmc_issue.py
+    record (one PMC pass over a full-size launch), or None."""
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            rec = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if not (rec.get("config") == config and rec.get("width") == W and rec.get("spp") == S and not rec.get("f64")):
+        return None
+    import hashlib
+
+    with open(lib_path, "rb") as f:
+        same = hashlib.sha256(f.read()).hexdigest() == rec.get("lib_sha256")
+    return {k: rec[k] for k in ("valu_busy", "lanes_per_valu", "valu_insts_per_ray")} | {
+        "issue_source": f"{os.path.relpath(path, ROOT)}: rocprofv3 --pmc SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU "
+                        f"GRBM_GUI_ACTIVE ... over one {config} launch, {'this' if same else 'an earlier'} "
+                        f"librrt_hip.so build ({rec.get('lib_sha256', '')[:12]}); valu_busy = 2 cycles x "
+                        f"VALU wave-instructions / (1024 SIMDs x cycles)"}
 
 
 def main():
@@ -362,8 +425,11 @@ def main():
         alg_bytes = BYTES_PER_SPHERE_TEST * work["sphere_tests"] + BYTES_PER_NODE_VISIT * work["node_visits"]
         traffic_json = args.traffic_json or os.path.join(ROOT, "profiles", f"traffic_{config}.json")
         traffic, traffic_src = (None, None)
-        if rows == H:  # the PMC record is of a whole-frame launch
+        issue = None
+        if rows == H:  # the PMC records are of a whole-frame launch
             traffic, traffic_src = load_traffic(traffic_json, config, W, S, rrt._lib.LIB_PATH)
+            issue = load_issue(args.issue_json or os.path.join(ROOT, "profiles", f"issue_{config}.json"), config, W, S,
+                               rrt._lib.LIB_PATH)
         if bands:
             split = (f"{band}-row bands dealt round-robin over {world} rank(s), RCCL gather of the float tiles "
                      f"to rank 0 inside the timed step" if world > 1 else
@@ -393,6 +459,8 @@ def main():
                     "(SURVEY 8d's 78.6 assumed 16-lane SIMDs). lds_l2_scene_read_GBps_algorithmic = "
                     "(16 B/sphere test + 56 B/node visit) / kernel time: scene reads served by LDS/L2, not HBM",
         }
+        if issue:  # the binding limit: VALU issue slots and lanes per instruction (FLOP frac is low by construction)
+            roofline.update(issue)
         out = {
             "metric": METRIC,
             "value": round(rays / elapsed / 1e6, 2),
@@ -436,6 +504,8 @@ def main():
             if config != "C3":
                 out["c3_one_gpu"] = c3_one_gpu()
             out["c1"] = c1_timings(cpus)
+        if world == 1 and not args.no_f64 and config in ("C1", "C2", "C4", "C5"):
+            out["f64_books"] = f64_books_frame(config)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(scene, args.cpu_seconds, cpus)
         print(json.dumps(out), flush=True)
