@@ -10,6 +10,8 @@
 // the CPU renderer) and no silent fallback.
 #include "../../include/rrt_hip.h"
 
+#include <unistd.h>
+
 #include <cctype>
 #include <chrono>
 #include <cstdio>
@@ -17,6 +19,71 @@
 #include <cstring>
 #include <string>
 #include <vector>
+
+// A binary P6 PPM (maxval 255) into RGB8 rows; false if the file is missing or not such a PPM.
+static bool read_p6(const std::string &path, std::vector<uint8_t> &rgb, int32_t &w, int32_t &h) {
+    FILE *f = std::fopen(path.c_str(), "rb");
+    if (!f) return false;
+    auto token = [&](std::string &t) {
+        t.clear();
+        int ch = std::fgetc(f);
+        while (ch != EOF && (std::isspace(ch) || ch == '#')) {
+            if (ch == '#')
+                while (ch != EOF && ch != '\n') ch = std::fgetc(f);
+            ch = std::fgetc(f);
+        }
+        while (ch != EOF && !std::isspace(ch)) {
+            t += (char)ch;
+            ch = std::fgetc(f);
+        }
+        return !t.empty();  // the one whitespace byte after the token is consumed
+    };
+    std::string magic, ws, hs, maxv;
+    bool ok = token(magic) && magic == "P6" && token(ws) && token(hs) && token(maxv) && maxv == "255";
+    if (ok) {
+        w = std::atoi(ws.c_str());
+        h = std::atoi(hs.c_str());
+        ok = w > 0 && h > 0 && (size_t)w * h <= ((size_t)1 << 28);
+    }
+    if (ok) {
+        rgb.resize((size_t)w * h * 3);
+        ok = std::fread(rgb.data(), 1, rgb.size(), f) == rgb.size();
+    }
+    std::fclose(f);
+    return ok;
+}
+
+// RtwImage::new (the_next_week/rtw_image.rs:11-36) for this backend's texture files: the reference
+// decodes `name` (a JPEG) with the image crate; this CLI reads the RGB8 decode of it shipped as a
+// binary P6 (`name` with the extension .ppm; rustraytrace_amd/assets/earthmap.ppm, written by
+// build() from the committed decode). Search order as the reference's: $RTW_IMAGES/<file>, <file>,
+// then images/<file> in the working directory and up to six parents; then the assets directory
+// next to this executable. Not found: the reference's error line and an empty image, which
+// ImageTexture::value renders cyan (texture.rs:91-93).
+static bool load_rtw_image(const std::string &name, std::vector<uint8_t> &rgb, int32_t &w, int32_t &h) {
+    const std::string file = name.substr(0, name.rfind('.')) + ".ppm";
+    std::vector<std::string> cands;
+    if (const char *dir = std::getenv("RTW_IMAGES")) cands.push_back(std::string(dir) + "/" + file);
+    cands.push_back(file);
+    std::string prefix;
+    for (int i = 0; i < 7; ++i) {
+        cands.push_back(prefix + "images/" + file);
+        prefix += "../";
+    }
+    char exe[4096];
+    const ssize_t n = readlink("/proc/self/exe", exe, sizeof(exe) - 1);
+    if (n > 0) {
+        exe[n] = 0;
+        std::string d(exe);
+        cands.push_back(d.substr(0, d.rfind('/')) + "/assets/" + file);
+    }
+    for (const auto &p : cands)
+        if (read_p6(p, rgb, w, h)) return true;
+    std::fprintf(stderr, "ERROR: Could not load image file '%s'.\n", name.c_str());
+    rgb.clear();
+    w = h = 0;
+    return false;
+}
 
 static std::string normalize_book_name(const std::string &name) {  // main.rs:7-12
     std::string out;
@@ -35,7 +102,8 @@ static void usage() {
                  "           [--gpus N] [--seed S] [--grid_half G] [--p6] [--host-quantise] [-o out.ppm]\n"
                  "  --p6             binary P6 instead of render_io.rs's P3 text\n"
                  "  --host-quantise  copy the float accum and quantise on the host (same bytes)\n"
-                 "books: in_one_weekend\n");
+                 "books: in_one_weekend, the_next_week [1-9, other = final_scene(400, 250, 4)], "
+                 "the_rest_of_your_life\n");
 }
 
 int main(int argc, char **argv) {
@@ -107,17 +175,19 @@ int main(int argc, char **argv) {
     const bool book2 = book == "thenextweek" || book == "nextweek" || book == "next";  // main.rs:89
     const bool book3 = book == "therestofyourlife" || book == "restofyourlife" || book == "rest" ||
                        book == "restoflife";  // main.rs:90-92
-    const int scene = positional.size() > 1 ? std::atoi(positional[1].c_str()) : 0;  // main.rs:55
-    if (book2 && !(scene >= 1 && scene <= 8 && scene != 3)) {
-        std::fprintf(stderr, "HIP backend supports the_next_week scenes 1 (bouncing_spheres), 2 (checkered_spheres), "
-                             "4 (perlin_spheres), 5 (quads), 6 (simple_light), 7 (cornell_box) and 8 "
-                             "(cornell_smoke); scenes 3 (earth) and 9/other (final_scene) need the earth texture: "
-                             "use the Python API.\n");
-        return 2;
+    // main.rs:55 `positional_args.get(1).and_then(|a| a.parse::<i32>().ok())`, the_next_week/mod.rs:68-81
+    // `match scene.unwrap_or(0)`: 1-9 name a scene, anything else (missing, unparsable, 0, 10, -1)
+    // is the default arm final_scene(400, 250, 4) = rrt_build_next_week_scene's scene 10
+    int scene = 0;
+    if (positional.size() > 1) {
+        char *end = nullptr;
+        const long v = std::strtol(positional[1].c_str(), &end, 10);
+        if (end && *end == 0 && end != positional[1].c_str()) scene = (int)v;
     }
+    const int nw_scene = (scene >= 1 && scene <= 9) ? scene : 10;
     if (!book1 && !book2 && !book3) {  // main.rs:59-70, 93-97
-        std::fprintf(stderr, "HIP backend supports in_one_weekend, the_next_week scenes 1, 2, 4-8 and "
-                             "the_rest_of_your_life.\n");
+        std::fprintf(stderr, "Usage: rrt [--backend hip] <book> [scene]\n"
+                             "books: in_one_weekend, the_next_week, the_rest_of_your_life\n");
         return 2;
     }
 
@@ -131,6 +201,9 @@ int main(int argc, char **argv) {
     std::vector<float> motion;
     std::vector<RrtPerlin> perlin;
     uint32_t flags = 0;
+    std::vector<uint8_t> earth_rgb;
+    RrtTexture earth{nullptr, 0, 0};
+    uint32_t n_tex = 0;
     if (book1) {
         if (rrt_build_in_one_weekend_scene(&ov, seed, grid_half, &cam, nullptr, nullptr, 0, &n)) {
             std::fprintf(stderr, "HIP render failed: %s\n", rrt_hip_last_error());
@@ -146,7 +219,7 @@ int main(int argc, char **argv) {
     } else {
         const uint64_t s2 = seed_set ? seed : 0xB00C0002ull;
         auto build = [&](RrtBookScene *o) {
-            return book3 ? rrt_build_rest_of_your_life_scene(&ov, s2, o) : rrt_build_next_week_scene(scene, &ov, s2, o);
+            return book3 ? rrt_build_rest_of_your_life_scene(&ov, s2, o) : rrt_build_next_week_scene(nw_scene, &ov, s2, o);
         };
         RrtBookScene nw{};
         if (build(&nw)) {  // sizing pass
@@ -175,6 +248,11 @@ int main(int argc, char **argv) {
         cam = nw.camera;
         n = nw.n_spheres, n_mat = nw.n_materials, n_quads = nw.n_quads, n_perlin = nw.n_perlin;
         flags = nw.flags;  // RAY_TIME (book-2/3 cameras), BOOK3 (MIS integrator)
+        if (nw.uses_texture0) {  // ImageTexture::new("earthmap.jpg") (the_next_week/mod.rs earth, final_scene)
+            load_rtw_image("earthmap.jpg", earth_rgb, earth.width, earth.height);
+            earth.rgb8 = earth_rgb.empty() ? nullptr : earth_rgb.data();
+            n_tex = 1;
+        }
     }
     RrtSceneExt ext{};
     ext.sphere_motion = motion.empty() ? nullptr : motion.data();
@@ -196,12 +274,12 @@ int main(int argc, char **argv) {
     int rc;
     if (host_quantise && !p6) {  // float accum -> render_io on the host (rrt_hip_render_ex)
         accum.resize((size_t)w * h * 4);
-        rc = rrt_hip_render_ex(&cam, spheres.data(), n, materials.data(), n_mat, nullptr, 0, &ext, spp, gpus, flags,
-                               accum.data());
+        rc = rrt_hip_render_ex(&cam, spheres.data(), n, materials.data(), n_mat, n_tex ? &earth : nullptr, n_tex, &ext,
+                               spp, gpus, flags, accum.data());
     } else {  // render_io quantiser on the device (identical bytes), 3 B/pixel to the host, every book
         rgb8.resize((size_t)w * h * 3);
-        rc = rrt_hip_render_rgb8_ex(&cam, spheres.data(), n, materials.data(), n_mat, nullptr, 0, &ext, spp, gpus,
-                                    flags, rgb8.data());
+        rc = rrt_hip_render_rgb8_ex(&cam, spheres.data(), n, materials.data(), n_mat, n_tex ? &earth : nullptr, n_tex,
+                                    &ext, spp, gpus, flags, rgb8.data());
     }
     if (rc) {
         std::fprintf(stderr, "HIP render failed: %s\n", rrt_hip_last_error());  // main.rs:60-65

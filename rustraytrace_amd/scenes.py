@@ -148,6 +148,30 @@ def earth_texture() -> np.ndarray:
         return np.ascontiguousarray(z["rgb8"])
 
 
+def earth_ppm_path() -> str:
+    """The binary P6 copy of the earth texture the C++ CLI resolves like rtw_image.rs:11-36
+    (rustraytrace_amd/assets/earthmap.ppm, next to the rrt executable's directory)."""
+    return os.path.join(os.path.dirname(os.path.abspath(__file__)), "assets", "earthmap.ppm")
+
+
+def ensure_earth_ppm() -> str:
+    """Write earthmap.ppm (P6, the committed RGB8 decode of images/earthmap.jpg) if it is missing
+    or differs; build() calls this. Returns its path."""
+    rgb = earth_texture()
+    data = b"P6\n%d %d\n255\n" % (rgb.shape[1], rgb.shape[0]) + rgb.tobytes()
+    path = earth_ppm_path()
+    try:
+        with open(path, "rb") as f:
+            if f.read() == data:
+                return path
+    except OSError:
+        pass
+    with open(path + ".tmp", "wb") as f:
+        f.write(data)
+    os.replace(path + ".tmp", path)
+    return path
+
+
 def earth_light(image_width=1920, samples_per_pixel=1024, max_depth=100, seed=C4_SEED) -> SceneData:
     """C4: the_next_week earth() (mod.rs:196-220) + DiffuseLight(4,4,4) sphere at (0,7,0) r=2
     (simple_light, mod.rs:330-331), background black (mod.rs:344). Book-2 camera (time draw)."""

@@ -129,8 +129,10 @@ def test_cli_mirrors_main_rs():
     cli = os.path.join(ROOT, "rustraytrace_amd", "rrt")
     r = subprocess.run([cli, "--backend", "cpu"], capture_output=True, text=True)
     assert r.returncode == 2 and "CPU books renderer" in r.stderr
-    r = subprocess.run([cli, "--backend=hip", "the_next_week"], capture_output=True, text=True)
-    assert r.returncode == 2 and "the_next_week scenes 1" in r.stderr  # final_scene (0) not supported
+    if rrt.device_count() == 0:  # the default arm final_scene(400, 250, 4) renders (tests/test_gpu_cli.py)
+        r = subprocess.run([cli, "--backend=hip", "the_next_week", "--image_width", "16", "--samples_per_pixel", "1"],
+                           capture_output=True, text=True)
+        assert r.returncode == 1 and "no HIP device" in r.stderr and "Could not load image" not in r.stderr
     r = subprocess.run([cli, "--backend=hip", "no_such_book"], capture_output=True, text=True)
     assert r.returncode == 2 and "the_rest_of_your_life" in r.stderr
     r = subprocess.run([cli, "--backend", "wgpu"], capture_output=True, text=True)

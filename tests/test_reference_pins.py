@@ -35,14 +35,15 @@ def test_earth_asset_matches_survey_sha_and_texels():
         assert tuple(int(c) for c in rgb[y, x]) == want, (x, y)
 
 
-def test_earth_asset_raw_file_matches_npz():
-    """The raw RGB8 copy the C++ CLI reads (rtw_image resolution) holds the same bytes."""
-    raw = os.path.join(ROOT, "rustraytrace_amd", "assets", "earthmap.rgb8")
-    if not os.path.exists(raw):
-        pytest.skip("no raw asset")
-    data = open(raw, "rb").read()
-    assert data[:16] == b"RRTRGB8\0" + (1024).to_bytes(4, "little") + (512).to_bytes(4, "little")
-    assert data[16:] == _asset().tobytes()
+def test_earth_asset_p6_matches_npz():
+    """The P6 copy the C++ CLI reads (rtw_image.rs resolution; written by build()) holds the same bytes."""
+    import rustraytrace_amd as rrt
+    from rustraytrace_amd.scenes import ensure_earth_ppm
+
+    rrt.load()
+    data = open(ensure_earth_ppm(), "rb").read()
+    head = b"P6\n1024 512\n255\n"
+    assert data[: len(head)] == head and data[len(head):] == _asset().tobytes()
 
 
 def test_earth_asset_equals_fresh_decode_of_reference_jpeg():
