@@ -36,6 +36,9 @@ namespace {
 //   2: traversal wave-iterations x 64 / sum of tracing lanes per iteration / outer iterations
 //   3: leaf-loop wave-iterations x 64 / active lanes per leaf iteration / lanes taking the root branch
 //   4: shade entries x 64 / shading lanes / rejection-loop wave-iterations x 64
+//   5: dielectric-branch wave entries x 64 / dielectric lanes / metal-branch wave entries x 64
+//   6: metal lanes / miss (sky) wave entries x 64 / miss lanes
+//   7: camera-ray wave entries x 64 (after a path ends) / their lanes / disk-loop wave-iterations x 64
 #ifndef RRT_PHASE_TIMING
 #define RRT_PHASE_TIMING 0
 #endif
@@ -653,7 +656,8 @@ __device__ __forceinline__ int exit_skip(bool is_quad, bool is_medium, bool fron
 
 // Camera::get_ray (camera.rs:152-180) for global pixel (x, y) and the path's RNG.
 template <bool kStrat>
-__device__ __forceinline__ void camera_ray(const KParams &P, uint32_t x, uint32_t y, uint32_t s, PathState &ps) {
+__device__ __forceinline__ void camera_ray(const KParams &P, uint32_t x, uint32_t y, uint32_t s, PathState &ps,
+                                           Counters &cnt) {
     const auto &C = *kernarg_params();
     float ox, oy;
     if constexpr (kStrat) {  // sample_square_stratified (the_rest_of_your_life/camera.rs:173-177)
@@ -674,6 +678,7 @@ __device__ __forceinline__ void camera_ray(const KParams &P, uint32_t x, uint32_
     if (C.defocus_radius > 0.0f) {
         float px, py;
         for (;;) {  // vec3.rs:172-179 random_in_unit_disk
+            if constexpr (RRT_PHASE_TIMING == 7) cnt.d2 += wave_slot();
             px = rnd_pm1(ps.rng);
             py = rnd_pm1(ps.rng);
             if (__builtin_fmaf(py, py, px * px) < 1.0f) break;
@@ -836,6 +841,10 @@ __device__ __forceinline__ bool shade(const KParams &P, const PR &prims, const G
         cnt.d1 += 1;
     }
     if (prim < 0) {
+        if constexpr (RRT_PHASE_TIMING == 6) {
+            cnt.d1 += wave_slot();
+            cnt.d2 += 1;
+        }
         V3 bg;
         if (P.bg_mode == 1u) {
             bg = v3(P.background[0], P.background[1], P.background[2]);
@@ -901,11 +910,17 @@ __device__ __forceinline__ bool shade(const KParams &P, const PR &prims, const G
             att = v3(m.a.x, m.a.y, m.a.z);
         }
     } else if (kind == 1) {  // Metal (material.rs:53-64)
+        if constexpr (RRT_PHASE_TIMING == 5) cnt.d2 += wave_slot();
+        if constexpr (RRT_PHASE_TIMING == 6) cnt.d0 += 1;
         const V3 refl = unit(reflect(ps.d, nrm));
         dir = add(refl, muls(r, m.a.w));
         if (!(dot(dir, nrm) > 0.0f)) return true;  // absorbed
         att = v3(m.a.x, m.a.y, m.a.z);
     } else {  // Dielectric (material.rs:83-102)
+        if constexpr (RRT_PHASE_TIMING == 5) {
+            cnt.d0 += wave_slot();
+            cnt.d1 += 1;
+        }
         const float eta = __int_as_float(m.b.y);
         const float ri = front ? (1.0f / eta) : eta;
         const V3 ud = unit(ps.d);
@@ -1289,7 +1304,7 @@ __device__ __forceinline__ void render_body(const KParams &P) {
                         sum = v3(0.0f, 0.0f, 0.0f);
                         pkey = pixel_key(Q, x, y);
                         ps.rng = path_rng_k(pkey, s);
-                        camera_ray<kBook2 == 4>(P, x, y, s, ps);
+                        camera_ray<kBook2 == 4>(P, x, y, s, ps, cnt);
                         need_ray = 1;
                         has = 1;
                     }
@@ -1406,7 +1421,11 @@ __device__ __forceinline__ void render_body(const KParams &P) {
             const uint32_t x = xy & 0xffffu, y = xy >> 16;
             if (s < s_hi) {
                 ps.rng = path_rng_k(pkey, s);
-                camera_ray<kBook2 == 4>(P, x, y, s, ps);
+                if constexpr (RRT_PHASE_TIMING == 7) {
+                    cnt.d0 += wave_slot();
+                    cnt.d1 += 1;
+                }
+                camera_ray<kBook2 == 4>(P, x, y, s, ps, cnt);
             } else {  // unit complete: the chunk's sum, in sample order
                 const auto &Q = *kernarg_params();
                 // chunk index and tile-local row, re-derived from (y, s_hi) once per unit

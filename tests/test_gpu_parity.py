@@ -202,3 +202,30 @@ def test_book1_kernel_classes_match_oracle(monkeypatch, kinds, textured, in_lds)
     gpu = rrt.render(scene)
     ref, _, _ = oracle.render(scene, oracle.TWIN)
     assert_bit_exact(gpu, ref, scene.spp)
+
+
+@pytest.mark.parametrize("width,spp", [(24, 3), (40, 300), (200, 9)])
+def test_uneven_queues_drain(width, spp):
+    """Every work unit is claimed whatever the queues' sizes (rrt_kernel.hip work-queue comment):
+    frames whose 64-unit groups do not fill the 8 queues evenly (3 groups: queues 3-7 start empty;
+    a partial last group), with tiles of very different cost (sky-only rows against ground rows),
+    so the queues drain at different rates; every pixel's count w must equal the samples and the
+    image must equal the oracle's."""
+    scene = rrt.rtow(image_width=width, samples_per_pixel=spp, max_depth=8)
+    gpu, idx, _, _ = gpu_tile(scene)
+    assert np.all(gpu[..., 3] == spp)
+    if width * spp <= 40 * 300:
+        ref, _, _ = oracle.render(scene, oracle.TWIN, threads=16)
+        assert_bit_exact(gpu, ref[idx], spp)
+
+
+def test_counting_kernel_matches_oracle_test_counts():
+    """The instrumented kernel's sphere-test count (bench.py's roofline numerator) equals the
+    oracle's count over the kernel's own tree (KBVH): every primitive of a visited leaf range is
+    a test, the exit_skip primitive included (left out of the loop, counted once)."""
+    scene = rrt.rtow(image_width=48, samples_per_pixel=4, max_depth=8)
+    _, _, ctr, work = gpu_tile(scene, count=True)
+    nodes, order, info = build_bvh(scene)
+    _, rays, tests = oracle.render_kbvh(scene, nodes, order, info, threads=16)
+    assert work["rays"] == rays == ctr["rays"]
+    assert work["sphere_tests"] == tests

@@ -459,3 +459,25 @@ def test_accum_chunk_schedule(S, chunk):
             cs = cs + per[s]
         total = cs if total is None else total + cs
     assert np.array_equal(got[..., :3].astype(np.float32), total) and np.all(got[..., 3] == S)
+
+
+def test_fdlibm_acos_atan2_within_one_ulp_of_libm():
+    """BOOKS' f64 acos / atan2 (the earth texture's get_sphere_uv, the_next_week/sphere.rs:46-52)
+    restate fdlibm's algorithms, shared op for op with the f64 kernel (rrt_books64.hip). The
+    reference calls the platform libm through Rust's f64::acos / atan2: the restatement stays
+    within 1 ulp of glibc's over the unit sphere's normals and a wide atan2 range."""
+    rng = np.random.default_rng(7)
+    x = np.concatenate([rng.uniform(-1, 1, 200_000), rng.uniform(-1e-3, 1e-3, 2000),
+                        [-1.0, 1.0, 0.0, -0.0, -0.5, 0.5, 0.4375, -0.4375, 1 - 2**-53]])
+    y = rng.standard_normal(x.size) * np.exp(rng.uniform(-8, 8, x.size))
+    a, b = oracle.acos_atan2_f64(x, y)
+
+    def ulps(u, v):
+        return np.abs(u.view(np.int64) - v.view(np.int64))
+
+    assert ulps(a, np.arccos(x)).max() <= 1
+    assert ulps(b, np.arctan2(y, x)).max() <= 1
+    assert (a == np.arccos(x)).mean() > 0.9 and (b == np.arctan2(y, x)).mean() > 0.75
+    # exact special values of fdlibm
+    sa, sb = oracle.acos_atan2_f64(np.array([1.0, -1.0, 0.0]), np.array([0.0, 0.0, 1.0]))
+    assert sa[0] == 0.0 and sa[1] == np.pi and sb[0] == 0.0 and sb[1] == np.pi and sb[2] == np.pi / 2
