@@ -54,7 +54,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default=None,
-                    help="workload (BASELINE config name); default C2 (the metric's config) on 1 rank, C3 on N > 1")
+                    help="workload (BASELINE config C1-C5, or a scene-table name NW1-NW10 / B3); default C2 (the metric's config) on 1 rank, C3 on N > 1")
     ap.add_argument("--split", choices=["bands", "samples"], default="bands",
                     help="bands: C3's row-band tiles, strong scaling (default); samples: whole frame per rank, "
                          "weak scaling")
@@ -351,7 +351,7 @@ def main():
         kw["image_width"] = args.width
     if args.spp:
         kw["samples_per_pixel"] = args.spp
-    scene = rrt.config_scene(config, **kw)
+    scene = rrt.named_scene(config, **kw)
     W, H, S = scene.width, scene.height, scene.spp
     ds = rrt.DeviceScene(scene, device=device)
     # bands of equal count per rank when the height allows it (C3: 15 rows at 2/4/8 ranks)
@@ -459,6 +459,9 @@ def main():
                     "(SURVEY 8d's 78.6 assumed 16-lane SIMDs). lds_l2_scene_read_GBps_algorithmic = "
                     "(16 B/sphere test + 56 B/node visit) / kernel time: scene reads served by LDS/L2, not HBM",
         }
+        if scene.quads is not None or scene.media is not None:
+            roofline["note"] += (" Book-2 scene: the kernel's primitive-test count (spheres, quads, medium boundaries) "
+                                 "is priced at the sphere test's 23 FLOP / 16 B.")
         if issue:  # the binding limit: VALU issue slots and lanes per instruction (FLOP frac is low by construction)
             roofline.update(issue)
         out = {
@@ -475,8 +478,9 @@ def main():
             "dtype": "f32",
             "data": "synthetic",
             "config": {
-                "workload": f"{config} {SCENES.get(config, scene.name)}, {W}x{H}x{S}spp, max_depth {scene.max_depth}, "
-                            f"{len(scene.spheres)} spheres",
+                "workload": f"{config + ' ' + SCENES[config] if config in SCENES else scene.name}, {W}x{H}x{S}spp, max_depth {scene.max_depth}, "
+                            f"{len(scene.spheres)} spheres" + (f", {len(scene.quads)} quads" if scene.quads is not None else "")
+                            + (f", {len(scene.media)} media" if scene.media is not None else ""),
                 "image": [W, H],
                 "spp": S,
                 "max_depth": scene.max_depth,

@@ -27,6 +27,7 @@ from .scenes import (
     SceneData,
     build_in_one_weekend_scene,
     config_scene,
+    named_scene,
     earth_light,
     earth_texture,
     next_week_scene,
@@ -40,5 +41,5 @@ __all__ = [
     "_lib", "RrtError", "load", "DeviceScene", "device_count", "format_ppm_from_accum", "quantize_accum", "quantize_accum_books", "quantize_accum_books_f64", "render", "render_f64",
     "render_in_one_weekend", "write_ppm_from_accum", "render_rgb8", "quantize_accum_async", "format_pnm_from_rgb8",
     "write_pnm_from_rgb8", "CONFIGS", "SceneData", "build_in_one_weekend_scene",
-    "config_scene", "earth_light", "earth_texture", "next_week_scene", "rest_of_your_life_scene", "make_camera", "rtow", "three_spheres",
+    "config_scene", "named_scene", "earth_light", "earth_texture", "next_week_scene", "rest_of_your_life_scene", "make_camera", "rtow", "three_spheres",
 ]

@@ -257,3 +257,24 @@ def config_scene(name: str, **override) -> SceneData:
     sc = fn(**kw)
     sc.name = name
     return sc
+
+
+# The scene table's workloads (tools/bench_scenes.py at spp scale 1/4): book-2
+# scenes at 1920x1080 (square scenes 1080x1080), 64 spp, max_depth 50 (final_scene keeps its 40).
+_SQUARE = (5, 7, 8, 9, 10)
+NAMED = {f"NW{k}": dict(image_width=1080 if k in _SQUARE else 1920, samples_per_pixel=64,
+                        **({} if k in (9, 10) else dict(max_depth=50))) for k in range(1, 11)}
+NAMED["B3"] = dict(image_width=1080, samples_per_pixel=64, max_depth=50)
+
+
+def named_scene(name: str, **override) -> SceneData:
+    """A BASELINE config (C1-C5) or a scene-table workload by name: NW1-NW10 (the_next_week
+    scenes, `next_week_scene`) and B3 (`rest_of_your_life_scene`) at the NAMED sizes."""
+    if name in CONFIGS:
+        return config_scene(name, **override)
+    if name not in NAMED:
+        raise KeyError(f"unknown workload {name!r}: {sorted(CONFIGS) + sorted(NAMED)}")
+    kw = dict(NAMED[name], **override)
+    sc = rest_of_your_life_scene(kw) if name == "B3" else next_week_scene(int(name[2:]), kw)
+    sc.name = f"{name} {sc.name}"
+    return sc

@@ -1,0 +1,24 @@
+#!/bin/bash
+# Memory-latency PMC of one render launch per workload: two --pmc passes (SQ issue/latency
+# accumulators; L1/L2 hit counts), each its own run. WORKLOADS = config:spp[:width] list.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+for spec in ${WORKLOADS:-C2:64 NW9:64:1080}; do
+  c=${spec%%:*}; rest=${spec#*:}; s=${rest%%:*}; wa=""
+  [ "$rest" != "$s" ] && wa="--width ${rest#*:}"
+  timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_INST_LEVEL_VMEM SQ_INSTS_SMEM SQ_INST_LEVEL_SMEM SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_LDS SQ_INST_LEVEL_LDS -d gpurun_out/lat_$c -o p --output-format csv -- python3 tools/prof_render.py --config $c --spp $s $wa --iters 1 > gpurun_out/lat_$c.log 2>&1 || { echo "lat $c failed"; tail -3 gpurun_out/lat_$c.log; exit 1; }
+  timeout -s KILL 120 rocprofv3 --pmc TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum -d gpurun_out/hit_$c -o p --output-format csv -- python3 tools/prof_render.py --config $c --spp $s $wa --iters 1 > gpurun_out/hit_$c.log 2>&1 || { echo "hit $c failed"; tail -3 gpurun_out/hit_$c.log; exit 1; }
+  python3 - "$c" <<'PY'
+import sys, os
+sys.path.insert(0, "tools")
+from pmc_issue import per_dispatch
+c = sys.argv[1]
+a, _ = per_dispatch(f"gpurun_out/lat_{c}")
+b, _ = per_dispatch(f"gpurun_out/hit_{c}")
+a.update(b)
+print(c, {k: f"{v:.4g}" for k, v in sorted(a.items())})
+print(c, "vmem latency %.0f cyc, smem %.0f, lds %.0f" % (a["SQ_INST_LEVEL_VMEM"] / a["SQ_INSTS_VMEM_RD"],
+      a["SQ_INST_LEVEL_SMEM"] / max(a["SQ_INSTS_SMEM"], 1), a["SQ_INST_LEVEL_LDS"] / max(a["SQ_INSTS_LDS"], 1)))
+PY
+done

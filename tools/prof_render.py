@@ -22,7 +22,7 @@ def main():
     kw = dict(samples_per_pixel=a.spp)
     if a.width:
         kw["image_width"] = a.width
-    scene = rrt.config_scene(a.config, **kw)
+    scene = rrt.named_scene(a.config, **kw)
     ds = rrt.DeviceScene(scene, f64=a.f64)
     tile = ds.tile(16, 0, 1, 0, scene.spp)
     buf = torch.empty((scene.height, scene.width, 4), dtype=torch.float32, device="cuda:0")
