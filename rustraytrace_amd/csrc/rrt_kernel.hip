@@ -274,15 +274,21 @@ struct Prims {
     uint32_t n_quads;
     uint64_t seg;  // the path's RNG state at this segment ^ (bounce << 32): key of the media draws
     const GPerlin *perlin;  // Perlin tables (LDS copy when staged, else KParams.perlin)
+    const float4 *quv;      // a quad's u, v, w at 3 x its primitive index (KParams.prim_quv)
     static constexpr bool kHasQuads = kBook2 >= 2;
     static constexpr bool kHasMedia = kBook2 >= 3;
     // Book-1 scenes store r * r (f32, rounded as the test would round it) in the record's w and
     // the radius in the material record's b.w (rrt_host.cpp): one multiply less per sphere test.
     static constexpr bool kR2 = kBook2 <= 0;
     __device__ __forceinline__ float4 at(int i) const {
+        float4 m;
+        return at(i, m);
+    }
+    // also returns the motion record: a quad's (normal, D)
+    __device__ __forceinline__ float4 at(int i, float4 &m) const {
         float4 c = cr[i];
         if constexpr (kBook2 > 0) {
-            const float4 m = mo[i];
+            m = mo[i];
             c.x = c.x + time * m.x;
             c.y = c.y + time * m.y;
             c.z = c.z + time * m.z;
@@ -305,6 +311,26 @@ __device__ __forceinline__ bool quad_hit(const GQuad &g, V3 o, V3 d, float tmin,
     const V3 w = v3(g.w.x, g.w.y, g.w.z);
     const float alpha = dot(w, cross(hp, v3(g.v.x, g.v.y, g.v.z)));
     const float beta = dot(w, cross(v3(g.u.x, g.u.y, g.u.z), hp));
+    if (!(0.0f <= alpha && alpha <= 1.0f && 0.0f <= beta && beta <= 1.0f)) return false;  // is_interior
+    t_out = t;
+    return true;
+}
+
+// quad_hit on the leaf-order record: q and the tag in the primitive slot, (normal, D) in the motion
+// slot, so the plane test needs no further fetch; u, v, w are read only for a t inside the range.
+__device__ __forceinline__ bool quad_hit_leaf(const float4 *quv, float4 c, float4 m, V3 o, V3 d, float closest,
+                                              float &t_out) {
+    const V3 n = v3(m.x, m.y, m.z);
+    const float denom = dot(n, d);
+    if (__builtin_fabsf(denom) < 1e-8f) return false;
+    const float t = (m.w - dot(n, o)) / denom;
+    if (!(0.001f <= t && t <= closest)) return false;
+    const float4 u = quv[0], v = quv[1], w4 = quv[2];
+    const V3 p = v3(o.x + t * d.x, o.y + t * d.y, o.z + t * d.z);  // Ray::at
+    const V3 hp = v3(p.x - c.x, p.y - c.y, p.z - c.z);
+    const V3 w = v3(w4.x, w4.y, w4.z);
+    const float alpha = dot(w, cross(hp, v3(v.x, v.y, v.z)));
+    const float beta = dot(w, cross(v3(u.x, u.y, u.z), hp));
     if (!(0.0f <= alpha && alpha <= 1.0f && 0.0f <= beta && beta <= 1.0f)) return false;  // is_interior
     t_out = t;
     return true;
@@ -438,20 +464,27 @@ __device__ __forceinline__ void test_range(const PR &prim_cr, int first, int cou
             cnt.d0 += wave_slot();
             cnt.d1 += 1;
         }
-        const float4 cr = prim_cr.at(i);
+        float4 cr;
         if constexpr (PR::kHasQuads) {
+            cr = prim_cr.cr[i];
+            const float4 m = prim_cr.mo[i];
             if (cr.w < 0.0f) {
                 const int j = (int)(-cr.w) - 1;
                 float tq;
                 bool hit;
                 if (PR::kHasMedia && j >= (int)prim_cr.n_quads) hit = medium_hit(prim_cr, j - (int)prim_cr.n_quads, o, d, rk, closest, tq);
-                else hit = quad_hit(prim_cr.qd[j], o, d, 0.001f, closest, tq);
+                else hit = quad_hit_leaf(prim_cr.quv + 3 * i, cr, m, o, d, closest, tq);
                 if (hit) {
                     closest = tq;
                     hit_prim = i;
                 }
                 continue;
             }
+            cr.x = cr.x + prim_cr.time * m.x;  // Prims::at
+            cr.y = cr.y + prim_cr.time * m.y;
+            cr.z = cr.z + prim_cr.time * m.z;
+        } else {
+            cr = prim_cr.at(i);
         }
         const V3 oc = v3(cr.x - o.x, cr.y - o.y, cr.z - o.z);
         const float h = dot(d, oc);
@@ -857,7 +890,8 @@ __device__ __forceinline__ bool shade(const KParams &P, const PR &prims, const G
         return true;
     }
     // HitRecord (sphere.rs:47-50, hittable.rs:20-32)
-    const float4 cr = prims.at(prim);  // the sphere's center at the ray's time (sphere.rs:48)
+    float4 qn;  // a quad's (normal, D): its motion slot
+    const float4 cr = prims.at(prim, qn);  // the sphere's center at the ray's time (sphere.rs:48)
     const V3 p = v3(__builtin_fmaf(ps.d.x, t, ps.o.x), __builtin_fmaf(ps.d.y, t, ps.o.y), __builtin_fmaf(ps.d.z, t, ps.o.z));  // Ray::at, fused
     V3 outward;
     bool is_quad = false, is_medium = false;
@@ -868,7 +902,6 @@ __device__ __forceinline__ bool shade(const KParams &P, const PR &prims, const G
             outward = v3(1.0f, 0.0f, 0.0f);  // constant_medium.rs:76-82 (front_face true)
         } else {
             is_quad = true;
-            const float4 qn = prims.qd[j].n;
             outward = v3(qn.x, qn.y, qn.z);
         }
     } else {
@@ -1037,7 +1070,8 @@ __device__ __forceinline__ bool shade_b3(const KParams &P, const PR &prims, cons
         sum = add(sum, mul(ps.T, v3(P.background[0], P.background[1], P.background[2])));
         return true;
     }
-    const float4 cr = prims.at(prim);
+    float4 qn;  // a quad's (normal, D): its motion slot
+    const float4 cr = prims.at(prim, qn);
     const V3 p = v3(__builtin_fmaf(ps.d.x, t, ps.o.x), __builtin_fmaf(ps.d.y, t, ps.o.y), __builtin_fmaf(ps.d.z, t, ps.o.z));  // Ray::at, fused
     V3 outward;
     bool is_quad = false, is_medium = false;
@@ -1048,7 +1082,6 @@ __device__ __forceinline__ bool shade_b3(const KParams &P, const PR &prims, cons
             outward = v3(1.0f, 0.0f, 0.0f);
         } else {
             is_quad = true;
-            const float4 qn = prims.qd[j].n;
             outward = v3(qn.x, qn.y, qn.z);
         }
     } else {
@@ -1338,7 +1371,7 @@ __device__ __forceinline__ void render_body(const KParams &P) {
         }
         RayK rk;
         if (tr.node >= 0) rk = ray_consts(ps.o, ps.d);
-        const Prims<kBook2> pr{prims, motion, ps.time, P.quads, P.media, P.n_quads, rng_key(ps.rng) ^ ((uint64_t)ps.k << 32), perlin};
+        const Prims<kBook2> pr{prims, motion, ps.time, P.quads, P.media, P.n_quads, rng_key(ps.rng) ^ ((uint64_t)ps.k << 32), perlin, P.prim_quv};
         if constexpr (kWide) {
             for (;;) {
                 if constexpr (RRT_PHASE_TIMING == 2) {
@@ -1389,7 +1422,7 @@ __device__ __forceinline__ void render_body(const KParams &P) {
         }
         if (has && !need_ray && tr.node < 0) {
             need_ray = 1;
-            const Prims<kBook2> spr{prims, motion, ps.time, P.quads, P.media, P.n_quads, rng_key(ps.rng) ^ ((uint64_t)ps.k << 32), perlin};
+            const Prims<kBook2> spr{prims, motion, ps.time, P.quads, P.media, P.n_quads, rng_key(ps.rng) ^ ((uint64_t)ps.k << 32), perlin, P.prim_quv};
             if constexpr (Prims<kBook2>::kHasMedia) {
                 // The unbounded media (a fog around the whole scene; rrt_host.cpp unbounded_media):
                 // not in the tree, tested here against the closest hit of the walk, every lane whose
