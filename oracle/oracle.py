@@ -180,7 +180,7 @@ def render_kbvh(scene, nodes, order, layout, rows=None, samples=None, threads=1,
     80 / 64 BVH2, 128 BVH4, for trees without unbounded media). Same return as render()."""
     stride = int(layout["node_stride"]) if isinstance(layout, dict) else int(layout)
     n_unbounded = int(layout.get("n_unbounded", 0)) if isinstance(layout, dict) else 0
-    if stride not in (64, 80, 128):
+    if stride not in (32, 80, 128):
         raise ValueError(f"render_kbvh: node stride {stride} (pass build_bvh's info dict)")
     lib = load()
     W, H = int(scene.camera["params_f"][0, 1]), int(scene.camera["params_f"][0, 2])

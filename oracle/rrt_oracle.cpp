@@ -803,7 +803,7 @@ template <class T> struct World {
 // where the closest-hit winner depends on BVH topology (near-ties and grazing rays).
 struct KTree {
     uint32_t width = 0;
-    uint32_t stride = 0;  // bytes per node: 80 or 64 (BVH2), 128 (BVH4)
+    uint32_t stride = 0;  // bytes per node: 80 or 32 (BVH2), 128 (BVH4)
     const uint8_t *nodes = nullptr;
     uint32_t n_nodes = 0;
     const uint32_t *order = nullptr;  // leaf-order primitive -> original sphere index
@@ -825,6 +825,20 @@ struct KRay {
 // against tmin = 0.001 or orders strictly, so they cannot change a decision.
 static inline float min_num(float a, float b) { return (b != b) ? a : ((a != a) ? b : (a < b ? a : b)); }
 static inline float max_num(float a, float b) { return (b != b) ? a : ((a != a) ? b : (a > b ? a : b)); }
+
+// IEEE binary16 bits -> float (exact)
+static inline float half_to_float(uint16_t h) {
+    const uint32_t s = (uint32_t)(h & 0x8000u) << 16, e = (h >> 10) & 0x1fu, m = h & 0x3ffu;
+    uint32_t b;
+    if (e == 0) {
+        const float v = std::ldexp((float)m, -24);  // zero or subnormal
+        return s ? -v : v;
+    }
+    b = e == 31 ? (s | 0x7f800000u | (m << 13)) : (s | ((e + 112u) << 23) | (m << 13));
+    float out;
+    std::memcpy(&out, &b, 4);
+    return out;
+}
 
 // Kernel slab test (rrt_kernel.hip box_hit). A macro so the FMAs are emitted inside each
 // target clone of kbvh_hit (as vfmadd where the host has FMA3, else the libm call).
@@ -874,11 +888,21 @@ bool kbvh_hit(const World<float> &w, const KTree &kt, Vec3<float> o, Vec3<float>
             //   80 B (LDS): per child lo, hi, lo for x, y, z (9 floats), then the two links; the
             //        kernel reads each axis' (entry, exit) pair by the sign of 1/d, which takes
             //        the same decisions as min/max over (lo, hi) here;
-            //   64 B (global): c0 lo.x hi.x lo.y hi.y lo.z hi.z, c1 the same, links, 2 unused.
+            //   32 B (global): per child and axis lo | hi << 16 as f16 bits, then the links
+            //        (rrt_internal.h GNodeH); decoded exactly, as the kernel's v_fma_mix_f32 reads them.
             const uint8_t *nb = kt.nodes + (size_t)node * kt.stride;
             const float *f = reinterpret_cast<const float *>(nb);
             const bool ordered = kt.stride == 80;
-            const uint32_t *lk = reinterpret_cast<const uint32_t *>(nb + (ordered ? 72 : 48));
+            float hf[12];
+            if (!ordered) {
+                const uint32_t *w = reinterpret_cast<const uint32_t *>(nb);
+                for (int k = 0; k < 6; ++k) {
+                    hf[2 * k] = half_to_float((uint16_t)(w[k] & 0xffffu));
+                    hf[2 * k + 1] = half_to_float((uint16_t)(w[k] >> 16));
+                }
+                f = hf;
+            }
+            const uint32_t *lk = reinterpret_cast<const uint32_t *>(nb + (ordered ? 72 : 24));
             const int32_t l[4] = {(int32_t)(lk[0] & 0x0fffffffu), (int32_t)(lk[1] & 0x0fffffffu), (int32_t)(lk[0] >> 28),
                                   (int32_t)(lk[1] >> 28)};
             float tn0 = 0.0f, tn1 = 0.0f;
@@ -886,7 +910,7 @@ bool kbvh_hit(const World<float> &w, const KTree &kt, Vec3<float> o, Vec3<float>
             if (ordered) {
                 KBOX(f[0], f[1], f[3], f[4], f[6], f[7], r, kTmin, closest, tn0, h0);
                 KBOX(f[9], f[10], f[12], f[13], f[15], f[16], r, kTmin, closest, tn1, h1);
-            } else {
+            } else {  // f16 planes, decoded: c0 lo.x hi.x lo.y hi.y lo.z hi.z, c1 the same
                 KBOX(f[0], f[1], f[2], f[3], f[4], f[5], r, kTmin, closest, tn0, h0);
                 KBOX(f[6], f[7], f[8], f[9], f[10], f[11], r, kTmin, closest, tn1, h1);
             }
@@ -1789,15 +1813,15 @@ int oracle_render(const RrtCamera *cam, const RrtSphere *s, uint32_t n, const Rr
 }
 
 // mode 2 = KBVH: TWIN arithmetic, but closest hits found by walking the kernel's BVH
-// (rrt_build_bvh output: `nodes` of n_nodes x node_stride B (80 or 64: BVH2, 128: BVH4), `order`).
+// (rrt_build_bvh output: `nodes` of n_nodes x node_stride B (80 or 32: BVH2, 128: BVH4), `order`).
 int oracle_render_kbvh(const RrtCamera *cam, const RrtSphere *s, uint32_t n, const RrtMaterial *m, uint32_t nm,
                        const RrtTexture *tex, uint32_t ntex, const RrtSceneExt *ext, uint32_t flags, const void *nodes,
                        uint32_t n_nodes,
                        uint32_t width, const uint32_t *order, uint32_t n_unbounded, uint32_t y0, uint32_t y1,
                        uint32_t s0, uint32_t s1, int threads, double *accum, uint64_t *rays, uint64_t *sphere_tests,
                        uint32_t chunk) {
-    // `width` is the node stride in bytes: 80 / 64 (BVH2 layouts), 128 (BVH4)
-    if (!cam || !accum || !nodes || (width != 64 && width != 80 && width != 128)) return -1;
+    // `width` is the node stride in bytes: 80 / 32 (BVH2 layouts), 128 (BVH4)
+    if (!cam || !accum || !nodes || (width != 32 && width != 80 && width != 128)) return -1;
     const uint32_t np = n + (ext && ext->quads ? ext->n_quads : 0u) + (ext && ext->media ? ext->n_media : 0u);
     if (n_unbounded > np) return -1;
     KTree kt;

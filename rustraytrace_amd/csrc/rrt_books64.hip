@@ -300,12 +300,13 @@ __device__ __forceinline__ bool trav_node64(const Node *__restrict__ nodes, Stac
         h1 = box64(n.box[1][0], n.box[1][1], n.box[1][3], n.box[1][4], n.box[1][6], n.box[1][7], rk, t.closest, tn1);
         l0 = n.link[0];
         l1 = n.link[1];
-    } else {
-        const GNodeG n = nodes[t.node];
-        h0 = box64(n.b0.x, n.b0.y, n.b0.z, n.b0.w, n.b1.x, n.b1.y, rk, t.closest, tn0);
-        h1 = box64(n.b1.z, n.b1.w, n.b2.x, n.b2.y, n.b2.z, n.b2.w, rk, t.closest, tn1);
-        l0 = n.link.x;
-        l1 = n.link.y;
+    } else {  // global memory: the 32-B f16 node (GNodeH)
+        const uint4 *q = reinterpret_cast<const uint4 *>(nodes + t.node);
+        const uint4 a = q[0], b = q[1];
+        h0 = box64(lo16(a.x), hi16(a.x), lo16(a.y), hi16(a.y), lo16(a.z), hi16(a.z), rk, t.closest, tn0);
+        h1 = box64(lo16(a.w), hi16(a.w), lo16(b.x), hi16(b.x), lo16(b.y), hi16(b.y), rk, t.closest, tn1);
+        l0 = b.z;
+        l1 = b.w;
     }
     const uint32_t c0 = h0 ? (l0 >> kLinkCountShift) : 0u;
     const uint32_t c1 = h1 ? (l1 >> kLinkCountShift) : 0u;
@@ -463,7 +464,7 @@ template <bool kLds, bool kCount, int kBlk>
 __device__ __forceinline__ void render64_body(const KParams &P) {
     extern __shared__ uint4 lds_dyn[];
     uint16_t *lds_stack = reinterpret_cast<uint16_t *>(lds_dyn);
-    using Node = typename std::conditional<kLds, GNode, GNodeG>::type;
+    using Node = typename std::conditional<kLds, GNode, GNodeH>::type;
     const Node *nodes = reinterpret_cast<const Node *>(P.nodes);
     const float4 *prims = P.prim_cr;
     const GMaterial *mtl = P.prim_mtl;

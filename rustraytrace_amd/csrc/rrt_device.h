@@ -17,6 +17,10 @@ __device__ __forceinline__ uint32_t wave_slot() {
 // 8 instructions per draw against ~17 with three quarter-rate multiplies for the 64-bit LCG
 // of a PCG32 (+4.3 % on C2, same-box A/B). Only the top 24 bits of each output are used
 // (random_double), the bits the authors recommend for floating-point generation.
+// f16 planes of a GNodeH (exact conversions; in an FMA operand they become v_fma_mix_f32)
+__device__ __forceinline__ float lo16(uint32_t v) { return (float)__builtin_bit_cast(_Float16, (uint16_t)(v & 0xffffu)); }
+__device__ __forceinline__ float hi16(uint32_t v) { return (float)__builtin_bit_cast(_Float16, (uint16_t)(v >> 16)); }
+
 __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
     z += 0x9e3779b97f4a7c15ull;
     z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;

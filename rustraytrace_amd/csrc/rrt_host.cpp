@@ -119,7 +119,7 @@ void put4(float *dst, float a, float b, float c, float d) {
 // sweep SAH on all three axes (Builder::sweep); RRT_BVH_SPLIT=binned selects the reference's
 // own criterion — binned SAH exactly as bvh.rs:21-156 chooses splits (12 buckets, longest axis
 // of the node bbox, stable-sort+median fallbacks). Leaves hold <= max_leaf spheres; the tree
-// is flattened into 64-B GNodes with both child boxes in the parent. The tree only changes
+// is flattened into GNodes (80 B in LDS, 32 B in global memory) with both child boxes in the parent. The tree only changes
 // which boxes are tested, never a sphere's result.
 // ------------------------------------------------------------------------------------
 struct Interval {
@@ -342,7 +342,7 @@ struct Builder {
 struct FlatBvh {
     std::vector<uint8_t> bytes;
     uint32_t n_nodes = 0, n_leaves = 0, max_depth = 0, max_leaf = 0, stack_need = 0, width = 2;
-    uint32_t stride = 0;  // bytes per node: 80 (BVH2, sign-ordered, LDS), 64 (BVH2, global), 128 (BVH4)
+    uint32_t stride = 0;  // bytes per node: 80 (BVH2, sign-ordered, LDS), 32 (BVH2, f16, global), 128 (BVH4)
     // BVH2: every node whose children are both leaves has them adjacent in primitive order
     // (right.first == left.first + left.count), so the kernel tests the hit ones as one range
     bool sibling_leaves_adjacent = true;
@@ -404,17 +404,52 @@ void put_node2(rrt::GNode &n, const float *lo0, const float *hi0, const float *l
     n.link[0] = (uint32_t)ref0 | ((uint32_t)cnt0 << rrt::kLinkCountShift);
     n.link[1] = (uint32_t)ref1 | ((uint32_t)cnt1 << rrt::kLinkCountShift);
 }
-void put_node2(rrt::GNodeG &n, const float *lo0, const float *hi0, const float *lo1, const float *hi1, int32_t ref0,
+
+// f32 -> f16 bits rounded toward -inf (down) or +inf (up); a subnormal result is pushed outward to
+// 0 or the smallest normal, so the kernel never reads an f16 subnormal plane.
+uint16_t f16_bits(float x) {
+    const _Float16 h = (_Float16)x;
+    uint16_t b;
+    std::memcpy(&b, &h, 2);
+    return b;
+}
+float f16_value(uint16_t b) {
+    _Float16 h;
+    std::memcpy(&h, &b, 2);
+    return (float)h;
+}
+uint16_t f16_round(float x, bool up) {
+    uint16_t b = f16_bits(x);
+    const float v = f16_value(b);
+    if (up ? v < x : v > x) {  // one f16 step outward (toward +inf / -inf)
+        if ((b & 0x7fffu) == 0) b = up ? 0x0001u : 0x8001u;
+        else if (((b & 0x8000u) != 0) == up) b = (uint16_t)(b - 1u);
+        else b = (uint16_t)(b + 1u);
+    }
+    if ((b & 0x7c00u) == 0 && (b & 0x03ffu) != 0) {  // subnormal: outward to 0 or +-2^-14
+        const bool neg = (b & 0x8000u) != 0;
+        b = up ? (neg ? 0x8000u : 0x0400u) : (neg ? 0x8400u : 0x0000u);
+    }
+    return b;
+}
+void put_node2(rrt::GNodeH &n, const float *lo0, const float *hi0, const float *lo1, const float *hi1, int32_t ref0,
                int32_t cnt0, int32_t ref1, int32_t cnt1) {
-    n.b0 = make_float4(lo0[0], hi0[0], lo0[1], hi0[1]);
-    n.b1 = make_float4(lo0[2], hi0[2], lo1[0], hi1[0]);
-    n.b2 = make_float4(lo1[1], hi1[1], lo1[2], hi1[2]);
-    n.link = make_uint4((uint32_t)ref0 | ((uint32_t)cnt0 << rrt::kLinkCountShift),
-                        (uint32_t)ref1 | ((uint32_t)cnt1 << rrt::kLinkCountShift), 0u, 0u);
+    const float *lo[2] = {lo0, lo1}, *hi[2] = {hi0, hi1};
+    uint32_t *dst[2] = {n.c0, n.c1};
+    for (int c = 0; c < 2; ++c) {
+        const bool never = lo[c][0] >= 1e30f;  // never_hit_box(): the point (65504, 65504, 65504)
+        for (int a = 0; a < 3; ++a) {
+            const uint16_t l = never ? 0x7bffu : f16_round(lo[c][a], false);
+            const uint16_t h = never ? 0x7bffu : f16_round(hi[c][a], true);
+            dst[c][a] = (uint32_t)l | ((uint32_t)h << 16);
+        }
+    }
+    n.link[0] = (uint32_t)ref0 | ((uint32_t)cnt0 << rrt::kLinkCountShift);
+    n.link[1] = (uint32_t)ref1 | ((uint32_t)cnt1 << rrt::kLinkCountShift);
 }
 
 // BVH2: the binary tree as is, root = node 0, both child boxes stored in the parent; Node =
-// rrt::GNode (80 B, sign-ordered planes, LDS) or rrt::GNodeG (64 B, global memory).
+// rrt::GNode (80 B, sign-ordered planes, LDS) or rrt::GNodeH (32 B, f16 planes, global memory).
 template <class Node>
 FlatBvh flatten2(const Builder &bd, int32_t root) {
     FlatBvh f;
@@ -658,7 +693,7 @@ std::vector<uint32_t> unbounded_media(const RrtSphere *spheres, uint32_t n_spher
 }
 
 // BVH2 node layout: the sign-ordered 80-B nodes when `lds_fit(bytes of those nodes)` says the
-// scene will be staged in LDS, else the 64-B global-memory nodes.
+// scene will be staged in LDS, else the 32-B f16 global-memory nodes.
 FlatBvh build_bvh(const RrtSphere *spheres, uint32_t n_spheres, const ExtView &ex, uint32_t width,
                   uint32_t max_leaf, std::vector<uint32_t> &order, const std::function<bool(size_t)> &lds_fit) {
     const float *motion = ex.motion;
@@ -710,7 +745,7 @@ FlatBvh build_bvh(const RrtSphere *spheres, uint32_t n_spheres, const ExtView &e
         fb = flatten4(bld, root);
     } else {
         fb = flatten2<rrt::GNode>(bld, root);
-        if (!lds_fit(fb.bytes.size())) fb = flatten2<rrt::GNodeG>(bld, root);
+        if (!lds_fit(fb.bytes.size())) fb = flatten2<rrt::GNodeH>(bld, root);
     }
     order = bld.objs;
     for (uint32_t m : unb) order.push_back(n_spheres + n_quads + m);

@@ -18,20 +18,21 @@ struct alignas(16) GNode {
     uint32_t link[2];   // child c: node index (internal), or first primitive | count << 28 (leaf)
 };
 static_assert(sizeof(GNode) == 80, "GNode must be 80 B");
-// The same node in 64 B, for scenes read from global memory (beyond the LDS budget): an 80-B
-// node straddles 128-B cache lines and costs a fifth load (C5 -23 %), so there both children's
-// boxes are packed lo, hi per axis and the slab test takes min/max.
-//   b0 = c0.lo.x c0.hi.x c0.lo.y c0.hi.y
-//   b1 = c0.lo.z c0.hi.z c1.lo.x c1.hi.x
-//   b2 = c1.lo.y c1.hi.y c1.lo.z c1.hi.z
-//   link.x/.y = child link (as GNode::link), link.z/.w unused (0)
-struct alignas(16) GNodeG {
-    float4 b0;
-    float4 b1;
-    float4 b2;
-    uint4 link;
+// The same node in 32 B, for scenes read from global memory (beyond the LDS budget): each plane
+// as an f16 rounded outward (lo down, hi up; subnormals pushed out to 0 or the smallest normal),
+// lo | hi << 16 per axis, and the min/max slab test. Two 16-B loads per visit: a scene read from
+// L2 spends its time in the vector memory pipeline (TA/TD busy ~90 %), and the slab test reads
+// each f16 plane with v_fma_mix_f32 (exact f16 -> f32 inside the FMA), so the decode costs no
+// instruction. Looser boxes only add visits (C5 +0.06 %); hits are decided by the primitive
+// tests. Same-box against the 64-B f32 node (round 2's layout): C5 +7.5 %, bouncing spheres
+// +4.6 %, final_scene +-0.3 %. A never-hit child is the point (65504, 65504, 65504).
+//   c0[a] / c1[a] = child c's axis-a planes; link as GNode::link
+struct alignas(16) GNodeH {
+    uint32_t c0[3];
+    uint32_t c1[3];
+    uint32_t link[2];
 };
-static_assert(sizeof(GNodeG) == 64, "GNodeG must be 64 B");
+static_assert(sizeof(GNodeH) == 32, "GNodeH must be 32 B");
 constexpr uint32_t kLinkCountShift = 28;
 constexpr uint32_t kLinkFirstMask = (1u << kLinkCountShift) - 1u;
 constexpr uint32_t kMaxLeafPrims = 7;  // two leaf children's counts share one 4-bit field

@@ -551,13 +551,14 @@ __device__ __forceinline__ bool trav_node(const Node *__restrict__ nodes, Stack 
         l0 = n.link[0];
         l1 = n.link[1];
     } else {
-        // global memory (scenes beyond the LDS budget): the 64-B node in four 16-B loads and the
-        // min/max slab (per-lane dword gathers cost more there than the min/max)
-        const GNodeG n = nodes[t.node];
-        h0 = box_hit(n.b0.x, n.b0.y, n.b0.z, n.b0.w, n.b1.x, n.b1.y, rk.inv, rk.oi, 0.001f, t.closest, tn0);
-        h1 = box_hit(n.b1.z, n.b1.w, n.b2.x, n.b2.y, n.b2.z, n.b2.w, rk.inv, rk.oi, 0.001f, t.closest, tn1);
-        l0 = n.link.x;
-        l1 = n.link.y;
+        // global memory (scenes beyond the LDS budget): the 32-B f16 node in two 16-B loads and
+        // the min/max slab (per-lane dword gathers cost more there than the min/max)
+        const uint4 *q = reinterpret_cast<const uint4 *>(nodes + t.node);
+        const uint4 a = q[0], b = q[1];
+        h0 = box_hit(lo16(a.x), hi16(a.x), lo16(a.y), hi16(a.y), lo16(a.z), hi16(a.z), rk.inv, rk.oi, 0.001f, t.closest, tn0);
+        h1 = box_hit(lo16(a.w), hi16(a.w), lo16(b.x), hi16(b.x), lo16(b.y), hi16(b.y), rk.inv, rk.oi, 0.001f, t.closest, tn1);
+        l0 = b.z;
+        l1 = b.w;
     }
     // Leaf children (count in the link's top bits, 0 = internal) are postponed; the hit ones
     // form one range: sibling leaves are adjacent in primitive order, so l0's first primitive
@@ -1198,8 +1199,8 @@ __device__ __forceinline__ void render_body(const KParams &P) {
     extern __shared__ uint4 lds_dyn[];
     // LDS layout: [traversal stack: stack_depth x kBlk x StackT, 16-B aligned][nodes][primitives]
     StackT *lds_stack = reinterpret_cast<StackT *>(lds_dyn);
-    // BVH2 nodes: sign-ordered 80-B GNode when staged in LDS, 64-B GNodeG in global memory
-    using Node = typename std::conditional<kWide, GNode4, typename std::conditional<kLds, GNode, GNodeG>::type>::type;
+    // BVH2 nodes: sign-ordered 80-B GNode when staged in LDS, 32-B f16 GNodeH in global memory
+    using Node = typename std::conditional<kWide, GNode4, typename std::conditional<kLds, GNode, GNodeH>::type>::type;
     const Node *nodes = reinterpret_cast<const Node *>(P.nodes);
     const float4 *prims = P.prim_cr;
     const GMaterial *mtl = P.prim_mtl;

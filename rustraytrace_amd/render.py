@@ -251,7 +251,7 @@ def build_bvh(scene: SceneData, width: int = 0, max_leaf: int = 0):
 
 def decode_bvh2(nodes: np.ndarray, stride: int):
     """Decode build_bvh's width-2 node bytes (rrt_internal.h; stride = info["node_stride"]: 80 =
-    GNode, sign-ordered lo/hi/lo planes, 64 = GNodeG): per node and child, box lo/hi (n, 2, 3),
+    GNode, sign-ordered lo/hi/lo planes, 32 = GNodeH, f16 planes): per node and child, box lo/hi (n, 2, 3),
     first primitive or child node (n, 2) and leaf count (n, 2; 0 = internal)."""
     words = stride // 4
     f = nodes.view(np.float32).reshape(-1, words)
@@ -260,9 +260,9 @@ def decode_bvh2(nodes: np.ndarray, stride: int):
         box = f[:, :18].reshape(-1, 2, 3, 3)  # [node][child][axis][lo, hi, lo]
         assert np.array_equal(box[..., 2], box[..., 0])
         lo, hi, links = box[..., 0].copy(), box[..., 1].copy(), u[:, 18:20]
-    elif stride == 64:
-        box = f[:, :12].reshape(-1, 2, 3, 2)  # [node][child][axis][lo, hi]
-        lo, hi, links = box[..., 0].copy(), box[..., 1].copy(), u[:, 12:14]
+    elif stride == 32:  # GNodeH: f16 planes, lo | hi << 16 per child and axis
+        box = nodes.view(np.float16).reshape(-1, 16)[:, :12].astype(np.float32).reshape(-1, 2, 3, 2)  # [node][child][axis][lo, hi]
+        lo, hi, links = box[..., 0].copy(), box[..., 1].copy(), u[:, 6:8]
     else:
         raise ValueError(f"decode_bvh2: stride {stride}")
     return lo, hi, (links & 0x0FFFFFFF).astype(np.int64), (links >> 28).astype(np.int64)

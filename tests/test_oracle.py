@@ -420,20 +420,28 @@ def test_axis_parallel_rays_hit_through_straddling_boxes():
 
 
 def test_bvh2_node_layouts_hold_the_same_tree(monkeypatch):
-    """RTOW fits the LDS budget: 80-B sign-ordered nodes; C5's 10k spheres do not: 64-B nodes.
-    Forcing global memory on RTOW gives the 64-B layout of the same tree (same boxes, links)."""
+    """RTOW fits the LDS budget: 80-B sign-ordered nodes; C5's 10k spheres do not: 32-B f16 nodes.
+    Forcing global memory on RTOW gives the 32-B layout of the same tree: same links, and every f16
+    box holds its f32 box (rounded outward, no subnormal planes); a never-hit child stays never-hit."""
     from rustraytrace_amd.render import build_bvh, decode_bvh2
 
     sc = rrt.rtow(image_width=32, samples_per_pixel=2)
     nodes, order, info = build_bvh(sc)
     assert info["node_stride"] == 80 and nodes.size == 80 * info["n_nodes"]
     c5 = rrt.config_scene("C5", image_width=32, samples_per_pixel=2)
-    assert build_bvh(c5)[2]["node_stride"] == 64
+    assert build_bvh(c5)[2]["node_stride"] == 32
     monkeypatch.setenv("RRT_SCENE_IN_LDS", "0")
     nodes_g, order_g, info_g = build_bvh(sc)
-    assert info_g["node_stride"] == 64 and np.array_equal(order, order_g)
-    for x, y in zip(decode_bvh2(nodes, 80), decode_bvh2(nodes_g, 64)):
-        assert np.array_equal(x, y)
+    assert info_g["node_stride"] == 32 and nodes_g.size == 32 * info_g["n_nodes"] and np.array_equal(order, order_g)
+    lo, hi, first, count = decode_bvh2(nodes, 80)
+    lo_h, hi_h, first_h, count_h = decode_bvh2(nodes_g, 32)
+    assert np.array_equal(first, first_h) and np.array_equal(count, count_h)
+    live = lo[..., 0] < 1e29
+    assert np.all(lo_h[live] <= lo[live]) and np.all(hi_h[live] >= hi[live])
+    assert np.all(hi_h[live] - lo_h[live] <= (hi[live] - lo[live]) * 1.01 + 2e-2)  # ~f16 ulps at RTOW scale
+    planes = np.concatenate([lo_h.ravel(), hi_h.ravel()])
+    assert not np.any((planes != 0) & (np.abs(planes) < 2.0 ** -14))  # no f16 subnormals
+    assert np.all(lo_h[~live] == 65504.0) and np.all(hi_h[~live] == 65504.0)
 
 
 @pytest.mark.parametrize("S,chunk", [(20, 8), (512, 64), (64, 64), (65, 64), (7, 0), (300, 128), (256, 128)])
