@@ -229,3 +229,20 @@ def test_counting_kernel_matches_oracle_test_counts():
     _, rays, tests = oracle.render_kbvh(scene, nodes, order, info, threads=16)
     assert work["rays"] == rays == ctr["rays"]
     assert work["sphere_tests"] == tests
+
+
+@pytest.mark.parametrize("s", [1.0, 3000.0, 1e5])
+def test_f16_global_nodes_at_every_scale(monkeypatch, s):
+    """Scenes read from global memory walk 32-B f16 nodes (planes rounded outward, saturating to
+    +-inf / 65504 beyond f16's range: tests/test_f16_nodes.py). The kernel reads them with
+    v_fma_mix_f32 and must take the oracle KBVH walk's every decision on the same bits."""
+    from test_f16_nodes import scaled_scene
+
+    monkeypatch.setenv("RRT_SCENE_IN_LDS", "0")
+    scene = scaled_scene(rrt.rtow(image_width=40, samples_per_pixel=4, max_depth=8), s)
+    nodes, order, info = build_bvh(scene)
+    assert info["node_stride"] == 32
+    gpu, idx, ctr, _ = gpu_tile(scene)
+    ref, rays, _ = oracle.render_kbvh(scene, nodes, order, info, threads=16)
+    assert ctr["rays"] == rays
+    assert_bit_exact(gpu, ref[idx], scene.spp)
