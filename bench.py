@@ -258,6 +258,9 @@ def wall_clock_breakdown(scene, accum, kernel_ms):
     host, d2h_ms = timed(lambda: accum.cpu())
     _, fmt_ms = timed(lambda: rrt.write_ppm_from_accum(scene.width, scene.height, host.numpy(), scene.spp, os.devnull))
     e2e_accum, render_ms = timed(lambda: rrt.render(scene, n_gpus=1))
+    # the same call as the Rust shim and the CLI make it (flags 0: progress lines on stderr, the
+    # work-queue heads read every 100 ms, the end noticed within ~1 ms)
+    _, progress_ms = timed(lambda: rrt.render(scene, n_gpus=1, quiet=False))
     _, fmt2_ms = timed(lambda: rrt.write_ppm_from_accum(scene.width, scene.height, e2e_accum, scene.spp, os.devnull))
     # output step on the device: render + device quantiser, 3 B/pixel D2H
     rgb8, rgb8_ms = timed(lambda: rrt.render_rgb8(scene, n_gpus=1))
@@ -271,6 +274,8 @@ def wall_clock_breakdown(scene, accum, kernel_ms):
         "ppm_write_ms": round(fmt_ms, 3),
         "end_to_end_ms": round(render_ms + fmt2_ms, 3),
         "end_to_end_note": "rrt_hip_render (BVH build, H2D, kernel, D2H, 1 GPU) + P3 write of the frame",
+        "render_with_progress_ms": round(progress_ms, 3),
+        "progress_note": "rrt_hip_render without RRT_FLAG_QUIET (as the Rust shim and the CLI call it), no P3 write",
         "end_to_end_rgb8_p3_ms": round(rgb8_ms + p3_ms, 3),
         "end_to_end_rgb8_p6_ms": round(rgb8_ms + p6_ms, 3),
         "rgb8_note": "rrt_hip_render_rgb8 (device quantiser, same bytes) + P3 / binary P6 write",
