@@ -30,7 +30,7 @@
 namespace rrt {
 namespace {
 
-// Debug builds only (-DRRT_PHASE_TIMING=1..4, never the shipped library): per-wave phase
+// Debug builds only (-DRRT_PHASE_TIMING=1..8, never the shipped library): per-wave phase
 // statistics written into counter slots 2..4 by the non-counting kernel.
 //   1: s_memtime cycles spent in refill+ray start / traversal loop / shading
 //   2: traversal wave-iterations x 64 / sum of tracing lanes per iteration / outer iterations
@@ -39,6 +39,7 @@ namespace {
 //   5: dielectric-branch wave entries x 64 / dielectric lanes / metal-branch wave entries x 64
 //   6: metal lanes / miss (sky) wave entries x 64 / miss lanes
 //   7: camera-ray wave entries x 64 (after a path ends) / their lanes / disk-loop wave-iterations x 64
+//   8: node-step wave-iterations x 64 / those whose stepping lanes all visit one node x 64 / their lanes
 #ifndef RRT_PHASE_TIMING
 #define RRT_PHASE_TIMING 0
 #endif
@@ -1394,6 +1395,19 @@ __device__ __forceinline__ void render_body(const KParams &P) {
                     ph0 += 64;
                     ph1 += (uint64_t)__popcll(__ballot(tr.node >= 0 && lv == 0));
                 }
+                if constexpr (RRT_PHASE_TIMING == 8) {  // node steps whose stepping lanes all visit one node
+                    const bool stepping = tr.node >= 0 && lv == 0;
+                    const uint64_t sm = __ballot(stepping);
+                    const int n0 = __builtin_amdgcn_readfirstlane(stepping ? tr.node : 0x7fffffff);
+                    const uint64_t same = __ballot(stepping && tr.node == n0);
+                    if (sm != 0) {
+                        ph0 += 64;
+                        if (same == sm) {
+                            ph1 += 64;
+                            ph2 += (uint64_t)__popcll(sm);
+                        }
+                    }
+                }
                 if (tr.node >= 0 && lv == 0) {
                     Leaves l;
                     if (trav_node<kCount>(nodes, stack, rk, tr, l, cnt)) lv = l;
@@ -1478,7 +1492,7 @@ __device__ __forceinline__ void render_body(const KParams &P) {
         }
         if constexpr (RRT_PHASE_TIMING == 1) ph2 += __builtin_amdgcn_s_memtime() - tp;
     }
-    if constexpr (RRT_PHASE_TIMING >= 3 && !kCount) {
+    if constexpr (RRT_PHASE_TIMING >= 3 && RRT_PHASE_TIMING <= 7 && !kCount) {
         ph0 = wave_sum_u32(cnt.d0);
         ph1 = wave_sum_u32(cnt.d1);
         ph2 = wave_sum_u32(cnt.d2);

@@ -24,6 +24,7 @@ VARIANTS = {
     "phase5": ["-DRRT_PHASE_TIMING=5"],
     "phase6": ["-DRRT_PHASE_TIMING=6"],
     "phase7": ["-DRRT_PHASE_TIMING=7"],
+    "phase8": ["-DRRT_PHASE_TIMING=8"],
     "trace": ["-DRRT_TRACE_X=3", "-DRRT_TRACE_Y=4", "-DRRT_TRACE_S=5"],
     "knobs": ["-DRRT_BLOCK=256", "-DRRT_WAVES=4", "-DRRT_TILE_W=16", "-DRRT_B2_WAVES=1", "-DRRT_B2_BLOCK=512",
               "-DRRT_PRIO_REFILL=0", "-DRRT_PRIO_NODE=0", "-DRRT_PRIO_LEAF=0", "-DRRT_PRIO_SHADE=0"],
