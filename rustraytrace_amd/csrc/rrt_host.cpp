@@ -762,7 +762,6 @@ struct RrtScene {
     float4 *d_prim_cr = nullptr;
     rrt::GMaterial *d_prim_mtl = nullptr;
     float4 *d_prim_motion = nullptr;
-    float4 *d_prim_quv = nullptr;
     rrt::GPerlin *d_perlin = nullptr;
     rrt::GQuad *d_quads = nullptr;
     rrt::GMedium *d_media = nullptr;
@@ -793,7 +792,6 @@ void free_scene(RrtScene *s) {
     (void)hipFree(s->d_prim_cr);
     (void)hipFree(s->d_prim_mtl);
     (void)hipFree(s->d_prim_motion);
-    (void)hipFree(s->d_prim_quv);
     (void)hipFree(s->d_perlin);
     (void)hipFree(s->d_quads);
     (void)hipFree(s->d_media);
@@ -1088,8 +1086,6 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
     std::vector<float4> prim_cr(n_prims);
     std::vector<rrt::GMaterial> prim_mtl(n_prims);
     std::vector<float4> prim_motion(book2 ? n_prims : 0, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
-    // a quad's u, v, w at its leaf-order slot: the leaf test needs no dependent fetch of its GQuad
-    std::vector<float4> prim_quv(n_quads ? 3 * (size_t)n_prims : 0, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
     for (uint32_t i = 0; i < n_prims; ++i) {
         if (order[i] >= n_spheres) {  // quad j / medium j - n_quads: tagged by a negative w (spheres have r >= 0)
             const uint32_t j = order[i] - n_spheres;
@@ -1099,9 +1095,6 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
                 const rrt::GQuad &g = gquads[j];
                 prim_cr[i] = make_float4(g.q.x, g.q.y, g.q.z, -(float)(j + 1));
                 prim_motion[i] = make_float4(g.n.x, g.n.y, g.n.z, g.q.w);
-                prim_quv[3 * (size_t)i + 0] = g.u;
-                prim_quv[3 * (size_t)i + 1] = g.v;
-                prim_quv[3 * (size_t)i + 2] = g.w;
             }
             continue;
         }
@@ -1168,7 +1161,6 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
         if (book2 && (rc = upload(&s->d_prim_motion, prim_motion.data(), prim_motion.size(), "sphere motion"))) break;
         if (n_perlin && (rc = upload(&s->d_perlin, perlin.data(), perlin.size(), "Perlin tables"))) break;
         if (!gquads.empty() && (rc = upload(&s->d_quads, gquads.data(), gquads.size(), "quads"))) break;
-        if (!prim_quv.empty() && (rc = upload(&s->d_prim_quv, prim_quv.data(), prim_quv.size(), "quad frames"))) break;
         if (n_media && (rc = upload(&s->d_media, gmedia.data(), gmedia.size(), "media"))) break;
         if (!glights.empty() && (rc = upload(&s->d_lights, glights.data(), glights.size(), "lights"))) break;
         if ((rc = upload(&s->d_tex_pool, tex_pool.data(), tex_pool.size(), "textures"))) break;
@@ -1198,7 +1190,6 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
     p.perlin = s->d_perlin;
     p.n_perlin = n_perlin;
     p.quads = s->d_quads;
-    p.prim_quv = s->d_prim_quv;
     p.n_quads = n_quads;
     p.media = s->d_media;
     p.n_media = n_media;

@@ -131,8 +131,8 @@ struct KParams {
     const float4 *prim_motion;   // (center2 - center1).xyz per primitive, same order; null = static scene
     const GPerlin *perlin;       // Perlin tables (noise textures)
     const GQuad *quads;          // quads, then media boundary quads; a quad's leaf-order primitive record is
-                                 // (q.xyz, -(1 + index)) with (normal.xyz, D) in its motion slot and
-                                 // (u, v, w) at prim_quv[3 i ...]; a medium's (0, 0, 0, -(1 + n_quads + index))
+                                 // (q.xyz, -(1 + index)) with (normal.xyz, D) in its motion slot; a
+                                 // medium's (0, 0, 0, -(1 + n_quads + index))
     const GMedium *media;
     const GLight *lights;        // book 3: the MIS light list
     const uint8_t *tex_pool;
@@ -218,9 +218,6 @@ struct KParams {
     D4 *partial64;
     float cam_u[3];
     float cam_v[3];
-    // Book-2 scenes: each leaf-order quad's u, v, w (3 float4 per primitive slot; other slots unused),
-    // read by the leaf test only once the plane test (from the primitive and motion records) passes.
-    const float4 *prim_quv;
 };
 
 // RRT_FLAG_F64 (include/rrt_hip.h): the f64 books-arithmetic kernel (rrt_books64.hip)

@@ -275,7 +275,6 @@ struct Prims {
     uint32_t n_quads;
     uint64_t seg;  // the path's RNG state at this segment ^ (bounce << 32): key of the media draws
     const GPerlin *perlin;  // Perlin tables (LDS copy when staged, else KParams.perlin)
-    const float4 *quv;      // a quad's u, v, w at 3 x its primitive index (KParams.prim_quv)
     static constexpr bool kHasQuads = kBook2 >= 2;
     static constexpr bool kHasMedia = kBook2 >= 3;
     // Book-1 scenes store r * r (f32, rounded as the test would round it) in the record's w and
@@ -317,16 +316,17 @@ __device__ __forceinline__ bool quad_hit(const GQuad &g, V3 o, V3 d, float tmin,
     return true;
 }
 
-// quad_hit on the leaf-order record: q and the tag in the primitive slot, (normal, D) in the motion
-// slot, so the plane test needs no further fetch; u, v, w are read only for a t inside the range.
-__device__ __forceinline__ bool quad_hit_leaf(const float4 *quv, float4 c, float4 m, V3 o, V3 d, float closest,
+// quad_hit on the leaf-order records: q and the tag in the primitive slot, (normal, D) in the
+// motion slot, so the plane test needs no further fetch; the quad's u, v, w (GQuad) are read only
+// for a t inside the interval.
+__device__ __forceinline__ bool quad_hit_leaf(const GQuad *g, float4 c, float4 m, V3 o, V3 d, float closest,
                                               float &t_out) {
     const V3 n = v3(m.x, m.y, m.z);
     const float denom = dot(n, d);
     if (__builtin_fabsf(denom) < 1e-8f) return false;
     const float t = (m.w - dot(n, o)) / denom;
     if (!(0.001f <= t && t <= closest)) return false;
-    const float4 u = quv[0], v = quv[1], w4 = quv[2];
+    const float4 u = g->u, v = g->v, w4 = g->w;
     const V3 p = v3(o.x + t * d.x, o.y + t * d.y, o.z + t * d.z);  // Ray::at
     const V3 hp = v3(p.x - c.x, p.y - c.y, p.z - c.z);
     const V3 w = v3(w4.x, w4.y, w4.z);
@@ -474,7 +474,7 @@ __device__ __forceinline__ void test_range(const PR &prim_cr, int first, int cou
                 float tq;
                 bool hit;
                 if (PR::kHasMedia && j >= (int)prim_cr.n_quads) hit = medium_hit(prim_cr, j - (int)prim_cr.n_quads, o, d, rk, closest, tq);
-                else hit = quad_hit_leaf(prim_cr.quv + 3 * i, cr, m, o, d, closest, tq);
+                else hit = quad_hit_leaf(prim_cr.qd + j, cr, m, o, d, closest, tq);
                 if (hit) {
                     closest = tq;
                     hit_prim = i;
@@ -1373,7 +1373,7 @@ __device__ __forceinline__ void render_body(const KParams &P) {
         }
         RayK rk;
         if (tr.node >= 0) rk = ray_consts(ps.o, ps.d);
-        const Prims<kBook2> pr{prims, motion, ps.time, P.quads, P.media, P.n_quads, rng_key(ps.rng) ^ ((uint64_t)ps.k << 32), perlin, P.prim_quv};
+        const Prims<kBook2> pr{prims, motion, ps.time, P.quads, P.media, P.n_quads, rng_key(ps.rng) ^ ((uint64_t)ps.k << 32), perlin};
         if constexpr (kWide) {
             for (;;) {
                 if constexpr (RRT_PHASE_TIMING == 2) {
@@ -1437,7 +1437,7 @@ __device__ __forceinline__ void render_body(const KParams &P) {
         }
         if (has && !need_ray && tr.node < 0) {
             need_ray = 1;
-            const Prims<kBook2> spr{prims, motion, ps.time, P.quads, P.media, P.n_quads, rng_key(ps.rng) ^ ((uint64_t)ps.k << 32), perlin, P.prim_quv};
+            const Prims<kBook2> spr{prims, motion, ps.time, P.quads, P.media, P.n_quads, rng_key(ps.rng) ^ ((uint64_t)ps.k << 32), perlin};
             if constexpr (Prims<kBook2>::kHasMedia) {
                 // The unbounded media (a fog around the whole scene; rrt_host.cpp unbounded_media):
                 // not in the tree, tested here against the closest hit of the walk, every lane whose
