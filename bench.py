@@ -8,7 +8,9 @@ on the device by the kernel itself.
 * N = 1 (default): config C2, 1920x1080x512 spp (BASELINE.json configs[1], the metric's config),
   the whole frame on one GPU, no gather. The line also carries a 1-GPU C3 frame (`c3_one_gpu`,
   the strong-scaling base of the N > 1 runs), the C1 CPU-path config timed on the CPU and the
-  GPU (`c1`), the wall-clock split and the CPU baseline.
+  GPU (`c1`), the wall-clock split, the CPU baseline, and the reference's own GPU kernel (its
+  CUDA_SOURCE built for gfx950, oracle/_ref) timed beside this backend on a bounded sample of the
+  same workload (`reference_gpu_slot`).
 * N > 1 (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): config C3,
   3840x2160x2048 spp, tile-split the north star's way: row bands (15 rows at
   2/4/8 ranks, so every rank owns 2160/N rows; `distributed.balanced_band`) dealt round-robin (band b -> rank b mod N), every rank renders its bands over all samples, and the
@@ -65,6 +67,8 @@ def parse():
     ap.add_argument("--no-breakdown", action="store_true", help="skip the wall-clock split (one extra frame)")
     ap.add_argument("--no-extra", action="store_true", help="skip the 1-GPU C3 frame and the C1 timings")
     ap.add_argument("--no-f64", action="store_true", help="skip the f64 books-arithmetic frame (f64_books)")
+    ap.add_argument("--no-ref-slot", action="store_true",
+                    help="skip timing the reference's own GPU kernel on a bounded sample (reference_gpu_slot)")
     ap.add_argument("--issue-json", default=None,
                     help="issue-side PMC record (tools/pmc_issue.py); default profiles/issue_<config>.json")
     ap.add_argument("--traffic-json", default=None,
@@ -232,6 +236,53 @@ def f64_books_frame(config, frames=2):
             "kernel_ms": round(ms, 3), "rays_per_frame": rays, "frames": frames,
             "parity": "tests/test_gpu_books64.py: closest-hit counts equal to the f64 books restatement, every "
                       "channel within 1e-4 (max |diff|/S ~1e-16), every PPM byte equal"}
+
+
+def reference_gpu_slot(config, budget_s=1.5):
+    """The reference's own GPU kernel on this GPU (oracle/_ref/ref_slot.hsaco: CUDA_SOURCE of
+    src/cuda/mod.rs:15-335 compiled unmodified for gfx950, launched as imp::render launches it;
+    oracle/ref_slot.cpp) against this backend on the identical bounded sample: the workload's
+    image at the spp that fits ~budget_s of the reference kernel. The unit is paths/s (W*H*spp
+    over HIP-event kernel time): the reference kernel counts no rays and its Russian roulette and
+    f32 re-hits trace a slightly different number of them (tests/test_gpu_ref_slot.py)."""
+    import numpy as np
+    import torch
+
+    import rustraytrace_amd as rrt
+    from oracle import ref_slot
+
+    if not ref_slot.available():
+        return {"skipped": "oracle/_ref/ref_slot.hsaco not built (needs /root/reference at build time)"}
+    probe = rrt.config_scene(config, samples_per_pixel=1)
+    ref_slot.render(probe)  # module load + first launch
+    _, ms1 = ref_slot.render(probe, return_ms=True)
+    full = rrt.config_scene(config)
+    spp = int(max(1, min(full.spp, 256, budget_s * 1e3 / max(ms1, 1e-3))))
+    scene = rrt.config_scene(config, samples_per_pixel=spp)
+    _, ref_ms = ref_slot.render(scene, return_ms=True)
+    ds = rrt.DeviceScene(scene)
+    tile = ds.tile(BAND_ROWS, 0, 1, 0, spp)
+    buf = torch.empty((scene.height, scene.width, 4), dtype=torch.float32, device="cuda")
+    stream = torch.cuda.current_stream()
+    ds.render_tile_async(tile, buf.data_ptr(), stream.cuda_stream)  # warm
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    for i in range(3):
+        ev[i].record(stream)
+        ds.render_tile_async(tile, buf.data_ptr(), stream.cuda_stream)
+    ev[3].record(stream)
+    torch.cuda.synchronize()
+    ours_ms = float(np.mean([ev[i].elapsed_time(ev[i + 1]) for i in range(3)]))
+    ds.close()
+    paths = scene.width * scene.height * spp
+    return {
+        "sample": f"{config} {scene.width}x{scene.height} at {spp} spp (max_depth {scene.max_depth}), both kernels on "
+                  "this GPU, HIP-event kernel time",
+        "kernel": "reference CUDA_SOURCE (src/cuda/mod.rs:15-335) built unmodified by hipcc for gfx950; brute-force "
+                  "closest hit over every sphere, one thread per pixel, passes of <= 256 spp",
+        "ref_ms": round(ref_ms, 3), "ref_mpaths_s": round(paths / ref_ms / 1e3, 2),
+        "ours_ms": round(ours_ms, 3), "ours_mpaths_s": round(paths / ours_ms / 1e3, 2),
+        "speedup": round(ref_ms / ours_ms, 2),
+    }
 
 
 def wall_clock_breakdown(scene, accum, kernel_ms):
@@ -515,6 +566,8 @@ def main():
             out["c1"] = c1_timings(cpus)
         if world == 1 and not args.no_f64 and config in ("C1", "C2", "C4", "C5"):
             out["f64_books"] = f64_books_frame(config)
+        if world == 1 and not args.no_ref_slot and config in ("C1", "C2", "C5"):
+            out["reference_gpu_slot"] = reference_gpu_slot(config)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(scene, args.cpu_seconds, cpus)
         print(json.dumps(out), flush=True)
