@@ -12,8 +12,10 @@ on the device by the kernel itself.
   CUDA_SOURCE built for gfx950, oracle/_ref) timed beside this backend on a bounded sample of the
   same workload (`reference_gpu_slot`).
 * N > 1 (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): config C3,
-  3840x2160x2048 spp, tile-split the north star's way: row bands (15 rows at
-  2/4/8 ranks, so every rank owns 2160/N rows; `distributed.balanced_band`) dealt round-robin (band b -> rank b mod N), every rank renders its bands over all samples, and the
+  3840x2160x2048 spp, tile-split the north star's way: row bands (10 rows at
+  2/4/8 ranks, so every rank owns 2160/N rows; `distributed.balanced_band`) dealt in serpentine order (period p of
+  N bands: ranks 0..N-1 for even p, N-1..0 for odd p; `distributed.band_owner`), every rank renders its bands over
+  all samples, and the
   float tiles are gathered to rank 0 over RCCL inside the timed step (`distributed.gather_rows`).
   Strong scaling: the frame is fixed, value = all ranks' rays / the max over ranks of the timed
   wall-clock. `--split samples` is the opt-in weak-scaling mode (every rank renders the whole
@@ -410,7 +412,7 @@ def main():
     scene = rrt.named_scene(config, **kw)
     W, H, S = scene.width, scene.height, scene.spp
     ds = rrt.DeviceScene(scene, device=device)
-    # bands of equal count per rank when the height allows it (C3: 15 rows at 2/4/8 ranks)
+    # bands of equal count per rank when the height allows it (C3: 10 rows at 2/4/8 ranks)
     band = balanced_band(H, world) if (bands and world > 1) else BAND_ROWS
     if bands:
         tile = ds.tile(band_rows=band, rank=rank, n_ranks=world, sample_begin=0, sample_end=S)
@@ -487,7 +489,7 @@ def main():
             issue = load_issue(args.issue_json or os.path.join(ROOT, "profiles", f"issue_{config}.json"), config, W, S,
                                rrt._lib.LIB_PATH)
         if bands:
-            split = (f"{band}-row bands dealt round-robin over {world} rank(s), RCCL gather of the float tiles "
+            split = (f"{band}-row bands dealt in serpentine order over {world} rank(s), RCCL gather of the float tiles "
                      f"to rank 0 inside the timed step" if world > 1 else
                      "whole frame on 1 GPU (the band split with one rank), no gather")
         else:

@@ -34,8 +34,8 @@ extern "C" {
  * rrt_quantize_accum_books, chunk partials bounded by RRT_PARTIAL_MB (sample passes);
  * 6: RrtBvhInfo.n_unbounded (scene-enclosing media tested after the BVH walk; was _pad);
  * 7: RRT_FLAG_F64 (the books path's f64 arithmetic), rrt_hip_render_f64, rrt_render_tile_f64_async,
- * rrt_quantize_accum_books_f64. */
-#define RRT_ABI_VERSION 7u
+ * rrt_quantize_accum_books_f64; 8: RrtTile bands dealt in serpentine order (was b % n_ranks). */
+#define RRT_ABI_VERSION 8u
 
 /* ---- scene ABI (== src/gpu/mod.rs:13-42) ------------------------------------------ */
 
@@ -273,8 +273,10 @@ uint32_t rrt_accum_chunk(void);
 /* ---- device-resident API (bench / multi-rank hosts) --------------------------------- */
 typedef struct RrtScene RrtScene;
 
-/* A tile = the rows this rank owns (row bands of `band_rows`, band b -> rank b % n_ranks)
- * crossed with the sample range [sample_begin, sample_end). */
+/* A tile = the rows this rank owns (row bands of `band_rows`, dealt in serpentine order: band b
+ * lies in period p = b / n_ranks at slot s = b % n_ranks and belongs to rank s when p is even,
+ * n_ranks - 1 - s when p is odd) crossed with the sample range [sample_begin, sample_end). The
+ * tile's rows are its bands in image order. */
 typedef struct RrtTile {
     uint32_t band_rows;
     uint32_t rank;

@@ -51,7 +51,7 @@ mod imp {
     /// The books path's f64 arithmetic (RRT_FLAG_F64): checked against `--backend cpu` output.
     pub const RRT_FLAG_F64: u32 = 0x8;
     /// ABI this shim was written against (RRT_ABI_VERSION).
-    pub const RRT_ABI_VERSION: u32 = 7;
+    pub const RRT_ABI_VERSION: u32 = 8;
 
     #[link(name = "rrt_hip")]
     extern "C" {
@@ -97,7 +97,7 @@ mod imp {
     }
 
     /// Devices to render on: RRT_GPUS (default 1, capped at the visible count). Row bands are
-    /// dealt round-robin over them inside the library (one host thread per device).
+    /// dealt over them in serpentine order inside the library (one host thread per device).
     fn gpus() -> Result<u32, String> {
         let mut visible = 0i32;
         check(unsafe { rrt_device_count(&mut visible) })?;

@@ -534,7 +534,8 @@ __device__ __forceinline__ void render64_body(const KParams &P) {
                 const uint32_t ly = ty * kTileH + (lit / kTileW);
                 if (x < Q.width && ly < Q.tile_rows) {
                     const uint32_t band = fast_div(ly, fdiv(Q.fd_band_rows));
-                    const uint32_t y = (band * Q.n_ranks + Q.rank) * Q.band_rows + (ly - band * Q.band_rows);
+                    const uint32_t slot = (band & 1u) ? Q.n_ranks - 1u - Q.rank : Q.rank;  // serpentine bands
+                    const uint32_t y = (band * Q.n_ranks + slot) * Q.band_rows + (ly - band * Q.band_rows);
                     xy = x | (y << 16);
                     s = Q.sample_begin + chunk_first(Q, chunk);
                     s_hi = min(s + (chunk < Q.n_big ? Q.chunk : Q.chunk_small), Q.sample_end);
@@ -614,7 +615,7 @@ __device__ __forceinline__ void render64_body(const KParams &P) {
                 const uint32_t chunk =
                     rel < nbs ? fast_div(rel, fdiv(Q.fd_chunk)) : Q.n_big + fast_div(rel - nbs, fdiv(Q.fd_chunk_small));
                 const uint32_t gb = fast_div(y, fdiv(Q.fd_band_rows));
-                const uint32_t ly = fast_div(gb - Q.rank, fdiv(Q.fd_n_ranks)) * Q.band_rows + (y - gb * Q.band_rows);
+                const uint32_t ly = fast_div(gb, fdiv(Q.fd_n_ranks)) * Q.band_rows + (y - gb * Q.band_rows);
                 const size_t px = (size_t)ly * Q.width + x;
                 const D4 out{sum.x, sum.y, sum.z, (double)(s_hi - (Q.sample_begin + chunk_first(Q, chunk)))};
                 if (Q.n_chunks == 1) Q.accum64[px] = out;

@@ -815,10 +815,20 @@ int upload(T **dst, const T *src, size_t n, const char *what) {
     return RRT_OK;
 }
 
+// Serpentine band dealing (include/rrt_hip.h RrtTile): the tile's j-th band is image band
+// j * n_ranks + band_slot(t, j). Round-robin (slot = rank in every period) gave rank n-1 the
+// lowest band of every period, so on C3 its tile was the most expensive: 1.96 % over the mean at 8
+// ranks (tools/c3_rank_balance.py); alternating the order per period cancels that trend.
+uint32_t band_slot(const RrtTile &t, uint32_t j) { return (j & 1u) ? t.n_ranks - 1u - t.rank : t.rank; }
+
 uint32_t tile_rows_of(uint32_t height, const RrtTile &t) {
     uint32_t rows = 0;
     const uint32_t bands = (height + t.band_rows - 1) / t.band_rows;
-    for (uint32_t b = t.rank; b < bands; b += t.n_ranks) rows += std::min(t.band_rows, height - b * t.band_rows);
+    for (uint32_t j = 0;; ++j) {
+        const uint32_t b = j * t.n_ranks + band_slot(t, j);
+        if (j * t.n_ranks >= bands) break;
+        if (b < bands) rows += std::min(t.band_rows, height - b * t.band_rows);
+    }
     return rows;
 }
 
@@ -1367,7 +1377,7 @@ int32_t rrt_tile_row_index(uint32_t height, const RrtTile *tile, uint32_t local_
     if (!row_out) return fail(RRT_E_INVALID, "null row_out");
     if (local_row >= tile_rows_of(height, *tile)) return fail(RRT_E_INVALID, "local_row out of range");
     const uint32_t band = local_row / tile->band_rows;
-    *row_out = (band * tile->n_ranks + tile->rank) * tile->band_rows + local_row % tile->band_rows;
+    *row_out = (band * tile->n_ranks + band_slot(*tile, band)) * tile->band_rows + local_row % tile->band_rows;
     return RRT_OK;
 }
 
@@ -1594,19 +1604,25 @@ static int32_t render_frame(const RrtCamera *cam, const RrtSphere *spheres, uint
         }
         if (!rc && rows) {
             // straight into the caller's image: the tile's local bands (band_rows rows each) are
-            // contiguous on both sides, so one strided 2-D copy places every whole band (its
-            // image rows are band * n_ranks + rank) and one plain copy the partial last band
+            // contiguous on both sides, so two strided 2-D copies place every whole band — the
+            // even local bands j (image band j * n_ranks + rank) and the odd ones (image band
+            // j * n_ranks + n_ranks - 1 - rank), each at a stride of two periods — and one plain
+            // copy the partial last band
             const uint8_t *src = rgb8_out ? (const uint8_t *)d_rgb8 : (const uint8_t *)d_accum;
             uint8_t *dst = rgb8_out ? rgb8_out
                                     : accum64_out ? reinterpret_cast<uint8_t *>(accum64_out) : reinterpret_cast<uint8_t *>(accum_out);
             const size_t band_bytes = (size_t)tile.band_rows * row_bytes;
             const uint32_t whole = rows / tile.band_rows, rest = rows % tile.band_rows;
             e = hipDeviceSynchronize();
-            if (e == hipSuccess && whole)
-                e = hipMemcpy2D(dst + (size_t)tile.rank * band_bytes, band_bytes * tile.n_ranks, src, band_bytes,
-                                band_bytes, whole, hipMemcpyDeviceToHost);
+            for (uint32_t par = 0; par < 2 && e == hipSuccess; ++par) {
+                const uint32_t count = (whole + 1u - par) / 2u;  // local bands j = par, par + 2, ...
+                if (count)
+                    e = hipMemcpy2D(dst + ((size_t)par * tile.n_ranks + band_slot(tile, par)) * band_bytes,
+                                    band_bytes * 2u * tile.n_ranks, src + (size_t)par * band_bytes, 2u * band_bytes,
+                                    band_bytes, count, hipMemcpyDeviceToHost);
+            }
             if (e == hipSuccess && rest)
-                e = hipMemcpy(dst + ((size_t)whole * tile.n_ranks + tile.rank) * band_bytes,
+                e = hipMemcpy(dst + ((size_t)whole * tile.n_ranks + band_slot(tile, whole)) * band_bytes,
                               src + (size_t)whole * band_bytes, (size_t)rest * row_bytes, hipMemcpyDeviceToHost);
             if (e != hipSuccess) {
                 g_err = std::string("render failed: ") + hipGetErrorString(e);

@@ -3,9 +3,12 @@
 One process per GPU. The scene and BVH are replicated (KB-sized); the work is split one of two
 ways, with no data-path collective until the single final exchange:
 
-* rows    (strong scaling, C3): row bands (`balanced_band`: 15 rows for C3 at 2/4/8 ranks)
-          dealt round-robin over ranks (rank r owns bands b with b % n == r), which balances
-          cheap sky rows against expensive ground rows.
+* rows    (strong scaling, C3): row bands (`balanced_band`: 10 rows for C3 at 2/4/8 ranks)
+          dealt over ranks in serpentine order (`band_owner`: period p = b // n holds one band
+          per rank, ranks 0..n-1 in even periods and n-1..0 in odd ones), which balances cheap
+          sky rows against expensive ground rows. Plain round-robin (b % n) gave every rank the
+          same offset in every period, so rank n-1 always drew the lowest band of a period: C3's
+          render time rose monotonically with rank, 1.96 % max over mean at 8 ranks.
           Rank 0 receives every rank's rows and places them — the image is bit-identical to a
           1-GPU render because every pixel is computed by the same lane program from the same
           (seed, pixel, sample) keys.
@@ -22,26 +25,42 @@ from typing import Callable, Optional, Sequence
 import numpy as np
 
 
+def band_owner(b: int, n_ranks: int) -> int:
+    """Rank owning row band b (include/rrt_hip.h RrtTile): serpentine over periods of n_ranks bands."""
+    p, slot = divmod(b, n_ranks)
+    return n_ranks - 1 - slot if p & 1 else slot
+
+
 def band_rows(height: int, band: int, rank: int, n_ranks: int) -> np.ndarray:
-    """Global image rows owned by `rank` (mirror of rrt_tile_row_index, rrt_host.cpp)."""
+    """Global image rows owned by `rank`, in the tile's local order (mirror of rrt_tile_row_index,
+    rrt_host.cpp): its p-th band is band p * n + (rank, or n - 1 - rank in odd periods)."""
     rows = []
     n_bands = (height + band - 1) // band
-    for b in range(rank, n_bands, n_ranks):
-        rows.extend(range(b * band, min((b + 1) * band, height)))
+    for p in range((n_bands + n_ranks - 1) // n_ranks):
+        b = p * n_ranks + (n_ranks - 1 - rank if p & 1 else rank)
+        if b < n_bands:
+            rows.extend(range(b * band, min((b + 1) * band, height)))
     return np.asarray(rows, dtype=np.int64)
 
 
-def balanced_band(height: int, n_ranks: int, max_band: int = 16, min_band: int = 8) -> int:
-    """Rows per band: the largest b in [min_band, max_band] with height % (b * n_ranks) == 0, so
-    every rank owns the same number of bands and rows; max_band when no such b exists.
+def balanced_band(height: int, n_ranks: int, max_band: int = 16, min_band: int = 10) -> int:
+    """Rows per band: every rank must own the same number of bands and rows, so the candidates are
+    the b with height % (b * n_ranks) == 0. Among those in [min_band, max_band] the smallest (the
+    most bands per rank), else the largest in [8, min_band), else max_band.
 
-    C3 (2160 rows) at 16-row bands leaves 135 bands: at 2/4/8 ranks the busiest rank owns 0.74 %
-    more rows than the mean, and the frame waits for it. 15-row bands give 144 = 8 x 18. The image
-    does not depend on the band height (every pixel is keyed by its global index)."""
-    for b in range(max_band, min_band - 1, -1):
-        if height % (b * n_ranks) == 0:
-            return b
-    return max_band
+    C3 (2160 rows) at 16-row bands left 135 bands: at 2/4/8 ranks the busiest rank owned 0.74 %
+    more rows than the mean. With equal counts what is left is how evenly each rank's bands sample
+    the image's row costs (sky rows are cheap, ground rows expensive): at 8 ranks, serpentine
+    dealing, 15-row bands (18 per rank) put the slowest rank 1.17 % over the mean, 10-row bands
+    (27 per rank) 0.21 %, 9-row 0.28 %; below 10 rows the 8-row work tiles straddle more band
+    edges and the sum of the ranks' times grows (+0.2 % at 9, +0.3 % at 6, +0.7 % at 5;
+    tools/c3_rank_balance.py). At 2 and 4 ranks every height from 9 to 15 is within 0.3 %. The
+    image does not depend on the band height (every pixel is keyed by its global index)."""
+    fits = [b for b in range(8, max_band + 1) if height % (b * n_ranks) == 0]
+    upper = [b for b in fits if b >= min_band]
+    if upper:
+        return min(upper)
+    return max(fits) if fits else max_band
 
 
 def sample_range(spp_per_rank: int, rank: int) -> tuple:

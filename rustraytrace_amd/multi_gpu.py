@@ -7,7 +7,7 @@ One process per GPU, launched by torch.distributed.run:
         --master-port 29500 -m rustraytrace_amd.multi_gpu --config C3 --out image.ppm
 
 Every rank builds the same scene and BVH (KB-sized, replicated), renders the row bands it
-owns (band b goes to rank b mod n) over all samples, and the float tiles are gathered to rank 0
+owns (band b of period p = b // n goes to rank b % n for even p, n - 1 - b % n for odd p) over all samples, and the float tiles are gathered to rank 0
 (`distributed.gather_rows`), which writes the render_io.rs PPM. The image is bit-identical to a
 1-GPU render: each pixel's samples are keyed by (seed, global pixel, sample) only. Rank 0 prints
 one JSON line: the slowest rank's kernel time, the gather time, Mrays/s over all ranks.
@@ -127,7 +127,7 @@ def main(argv=None) -> int:
                 rrt.write_ppm_from_accum(W, H, host, S, args.out)
         print(json.dumps({
             "config": args.config, "image": [W, H], "spp": S, "ranks": world, "backend": backend if use_dist else None,
-            "split": f"{args.band}-row bands dealt round-robin", "kernel_ms_max_over_ranks": round(kernel_ms, 3),
+            "split": f"{args.band}-row bands dealt in serpentine order", "kernel_ms_max_over_ranks": round(kernel_ms, 3),
             "gather_ms": round(gather_ms, 3), "rays": rays, "mrays_per_s": round(rays / kernel_ms / 1e3, 2),
         }), file=sys.stderr if args.out == "-" else sys.stdout, flush=True)
     if use_dist:

@@ -69,8 +69,10 @@ def test_two_rank_gather(tmp_path, mode):
 
 def test_balanced_band_gives_every_rank_equal_rows():
     from rustraytrace_amd.distributed import balanced_band
-    # C3 (2160 rows): 16-row bands leave the busiest rank 0.74 % above the mean at 2/4/8 ranks
-    assert [balanced_band(2160, n) for n in (1, 2, 3, 4, 8)] == [16, 15, 16, 15, 15]
+    # C3 (2160 rows): 16-row bands leave the busiest rank 0.74 % above the mean at 2/4/8 ranks;
+    # the smallest equal-count height of at least 10 rows, else the largest of 8-9, else 16
+    assert [balanced_band(2160, n) for n in (1, 2, 3, 4, 8)] == [10, 10, 10, 10, 10]
+    assert balanced_band(1080, 8) == 15 and balanced_band(54, 2) == 9 and balanced_band(144, 2) == 12
     for H, n in [(2160, 2), (2160, 4), (2160, 8), (1080, 8), (1080, 2)]:
         b = balanced_band(H, n)
         counts = [len(band_rows(H, b, r, n)) for r in range(n)]

@@ -1,5 +1,5 @@
 """The drop-in's in-library multi-device path (rrt_hip_render with n_gpus > 1: one host thread per
-device, row bands dealt round-robin, each device's bands copied straight into the caller's image by
+device, row bands dealt in serpentine order, each device's bands copied straight into the caller's image by
 a strided 2-D copy plus one plain copy of a partial last band; rrt_host.cpp render_frame) run with
 more than one worker on a one-GPU box: the test mode RRT_DEVICE_WRAP=1 maps worker g to device
 g % device_count, so 2, 3 and 8 workers share the GPU and every copy path runs. The frame is 100x56

@@ -75,6 +75,6 @@ def test_bench_band_split_line(ranks):
     if ranks > 1:
         assert "gather_ms" in line and "bands" in line["config"]["parallelism"]
         assert sum(line["rows_per_rank"]) == 144
-        assert line["rows_per_rank"] == [144 // ranks] * ranks  # balanced_band: 12-row bands
+        assert line["rows_per_rank"] == [144 // ranks] * ranks  # balanced_band: 12-row bands at 2 ranks
     else:
         assert "no gather" in line["config"]["parallelism"]
