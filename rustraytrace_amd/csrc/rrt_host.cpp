@@ -771,8 +771,8 @@ struct RrtScene {
     unsigned long long *d_counters = nullptr;       // 5 x u64, render launches
     unsigned long long *d_work_counters = nullptr;  // 5 x u64, instrumented launches
     uint32_t *d_unit_counter = nullptr;             // persistent-queue head
-    float4 *d_partial = nullptr;                    // chunk partial sums
-    size_t partial_cap = 0;                         // float4 elements
+    rrt::F3 *d_partial = nullptr;                   // chunk partial sums (RGB)
+    size_t partial_cap = 0;                         // F3 elements
     bool f64 = false;                               // RRT_FLAG_F64: the books-arithmetic kernel
     rrt::D4 *d_partial64 = nullptr;                 // its chunk partial sums
     size_t partial64_cap = 0;                       // D4 elements
@@ -892,7 +892,7 @@ int fill_params(RrtScene *s, const RrtTile *t, float *d_accum, rrt::KParams &p) 
     p.pass_chunks = p.n_chunks;
     if (p.n_chunks > 1) {  // partial sums [pass chunk][pixel], within the partial budget; grow on demand
         const size_t n_px = std::max<size_t>((size_t)p.tile_rows * p.width, 1);
-        const size_t elem = s->f64 ? sizeof(rrt::D4) : sizeof(float4);
+        const size_t elem = s->f64 ? sizeof(rrt::D4) : sizeof(rrt::F3);
         p.pass_chunks = (uint32_t)std::min<size_t>(p.n_chunks, std::max<size_t>(1, partial_budget() / (n_px * elem)));
         const size_t need = n_px * p.pass_chunks;
         size_t &cap = s->f64 ? s->partial64_cap : s->partial_cap;

@@ -124,6 +124,12 @@ struct alignas(16) D4 {
 };
 static_assert(sizeof(D4) == 32, "D4 must be 32 B");
 
+// A chunk partial: the RGB sums of one (chunk, pixel) — the sample count is the chunk schedule's,
+// so 12 B instead of a float4's 16.
+struct F3 {
+    float x, y, z;
+};
+
 struct KParams {
     const void *nodes;           // GNode[] (bvh_width 2) or GNode4[] (bvh_width 4)
     const float4 *prim_cr;       // sphere center.xyz, radius — in BVH leaf order
@@ -207,8 +213,9 @@ struct KParams {
     // generic 32-bit division sequence is ~35 instructions, paid at every unit start and end.
     FastDiv fd_pass_big, fd_pass_tail, fd_tiles_x, fd_band_rows, fd_n_ranks, fd_chunk, fd_chunk_small, fd_sqrt_spp;
     uint32_t *unit_counter;   // device queue heads: kQueues counters 128 B apart (zeroed per launch)
-    float4 *partial;          // [pass chunk][tile pixel] partial sums when n_chunks > 1: a chunk's
-                              // pixels are contiguous, so an 8x8 tile's rows fill whole 128-B lines
+    F3 *partial;              // [pass chunk][tile pixel] RGB partial sums when n_chunks > 1 (12 B: the
+                              // combine derives the count): a chunk's pixels are contiguous, so an
+                              // 8x8 tile's rows fill whole 128-B lines
 
     // The f64 books path (flags & kFlagF64, rrt_books64.hip); appended so the f32 kernels' field
     // offsets stay unchanged. Sums and chunk partials as D4 (RGB sums, w = count) in the same

@@ -1487,7 +1487,7 @@ __device__ __forceinline__ void render_body(const KParams &P) {
                 const size_t px = (size_t)ly * Q.width + x;
                 const float4 out = make_float4(sum.x, sum.y, sum.z, (float)(s_hi - (Q.sample_begin + chunk_first(Q, chunk))));
                 if (Q.n_chunks == 1) Q.accum[px] = out;
-                else Q.partial[(size_t)(chunk - Q.chunk_begin) * ((size_t)Q.tile_rows * Q.width) + px] = out;
+                else Q.partial[(size_t)(chunk - Q.chunk_begin) * ((size_t)Q.tile_rows * Q.width) + px] = F3{sum.x, sum.y, sum.z};
                 has = 0;
             }
         }
@@ -1533,14 +1533,20 @@ __global__ __launch_bounds__(kBlk, kWaves) void rrt_render(KParams P) {
 // The pass's chunk sums into accum, continuing the left fold over chunks in order: the first
 // pass starts from its chunk 0, later passes from the accum so far; w = the tile's sample count.
 // partial is [pass chunk][pixel], so each chunk row is read coalesced.
-__global__ __launch_bounds__(256) void rrt_combine_chunks(const float4 *__restrict__ partial, float4 *__restrict__ accum,
+__global__ __launch_bounds__(256) void rrt_combine_chunks(const F3 *__restrict__ partial, float4 *__restrict__ accum,
                                                           uint32_t n_pixels, uint32_t n_chunks, uint32_t first,
                                                           float count) {
     const uint32_t p = blockIdx.x * 256u + threadIdx.x;
     if (p >= n_pixels) return;
-    float4 acc = first ? partial[p] : accum[p];
+    float4 acc;
+    if (first) {
+        const F3 v = partial[p];
+        acc = make_float4(v.x, v.y, v.z, 0.0f);
+    } else {
+        acc = accum[p];
+    }
     for (uint32_t c = first ? 1u : 0u; c < n_chunks; ++c) {
-        const float4 v = partial[(size_t)c * n_pixels + p];
+        const F3 v = partial[(size_t)c * n_pixels + p];
         acc.x = acc.x + v.x;
         acc.y = acc.y + v.y;
         acc.z = acc.z + v.z;
