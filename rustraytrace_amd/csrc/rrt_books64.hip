@@ -252,12 +252,18 @@ __device__ __forceinline__ D3 texel64(const KParams &P, int tex, D3 outward) {
 // finite slope, so fma(P, inv, -o*inv) keeps the sign of P - o), and o * inv.
 struct RayK64 {
     D3 inv, oi;
+    // byte offsets of the ray's (entry, exit) plane pair of each axis in a GNode child box (the
+    // f32 kernel's RayK): 12a + 4 when 1/d_a < 0 (hi, lo), else 12a (lo, hi)
+    uint32_t ox, oy, oz;
 };
 __device__ __forceinline__ double clamp_inv64(double v) { return __builtin_fmax(__builtin_fmin(v, 0x1.0p500), -0x1.0p500); }
 __device__ __forceinline__ RayK64 ray_consts64(D3 o, D3 d) {
     RayK64 r;
     r.inv = d3(clamp_inv64(1.0 / d.x), clamp_inv64(1.0 / d.y), clamp_inv64(1.0 / d.z));
     r.oi = d3(o.x * r.inv.x, o.y * r.inv.y, o.z * r.inv.z);
+    r.ox = r.inv.x < 0.0 ? 4u : 0u;
+    r.oy = r.inv.y < 0.0 ? 16u : 12u;
+    r.oz = r.inv.z < 0.0 ? 28u : 24u;
     return r;
 }
 // Slab test of a stored f32 box in f64 (role of Aabb::hit, aabb.rs:52-85: a box test only prunes).
@@ -272,6 +278,21 @@ __device__ __forceinline__ bool box64(double lx, double hx, double ly, double hy
                                      __builtin_fmax(__builtin_fmin(z0, z1), 0.001));
     const double fr = __builtin_fmin(__builtin_fmin(__builtin_fmax(x0, x1), __builtin_fmax(y0, y1)),
                                      __builtin_fmin(__builtin_fmax(z0, z1), tmax));
+    tnear = nr;
+    return nr < fr;
+}
+
+// box64 on planes given in (entry, exit) order per axis (GNode's lo, hi, lo layout read at the
+// ray's sign offsets): fma(P, inv, -oi) is monotone in P for a fixed inv, so the entry plane's
+// distance is exactly min(t_lo, t_hi) and the exit plane's the max — box64's values and decisions
+// without its six f64 min/max (rrt_kernel.hip box_hit_ordered).
+__device__ __forceinline__ bool box64_ordered(double nx, double fx, double ny, double fy, double nz, double fz,
+                                              const RayK64 &rk, double tmax, double &tnear) {
+    const double x0 = __builtin_fma(nx, rk.inv.x, -rk.oi.x), x1 = __builtin_fma(fx, rk.inv.x, -rk.oi.x);
+    const double y0 = __builtin_fma(ny, rk.inv.y, -rk.oi.y), y1 = __builtin_fma(fy, rk.inv.y, -rk.oi.y);
+    const double z0 = __builtin_fma(nz, rk.inv.z, -rk.oi.z), z1 = __builtin_fma(fz, rk.inv.z, -rk.oi.z);
+    const double nr = __builtin_fmax(__builtin_fmax(x0, y0), __builtin_fmax(z0, 0.001));
+    const double fr = __builtin_fmin(__builtin_fmin(x1, y1), __builtin_fmin(z1, tmax));
     tnear = nr;
     return nr < fr;
 }
@@ -295,9 +316,13 @@ __device__ __forceinline__ bool trav_node64(const Node *__restrict__ nodes, Stac
     uint32_t l0, l1;
     double tn0 = 0.0, tn1 = 0.0;
     if constexpr (std::is_same<Node, GNode>::value) {
-        const GNode &n = nodes[t.node];  // LDS: lo, hi, lo per axis
-        h0 = box64(n.box[0][0], n.box[0][1], n.box[0][3], n.box[0][4], n.box[0][6], n.box[0][7], rk, t.closest, tn0);
-        h1 = box64(n.box[1][0], n.box[1][1], n.box[1][3], n.box[1][4], n.box[1][6], n.box[1][7], rk, t.closest, tn1);
+        const GNode &n = nodes[t.node];  // LDS: lo, hi, lo per axis, each pair read at the ray's sign offset
+        const char *bx = reinterpret_cast<const char *>(&n.box[0][0]);
+        auto plane = [&](uint32_t byte_off) { return (double)*reinterpret_cast<const float *>(bx + byte_off); };
+        h0 = box64_ordered(plane(rk.ox), plane(rk.ox + 4), plane(rk.oy), plane(rk.oy + 4), plane(rk.oz),
+                           plane(rk.oz + 4), rk, t.closest, tn0);
+        h1 = box64_ordered(plane(rk.ox + 36), plane(rk.ox + 40), plane(rk.oy + 36), plane(rk.oy + 40),
+                           plane(rk.oz + 36), plane(rk.oz + 40), rk, t.closest, tn1);
         l0 = n.link[0];
         l1 = n.link[1];
     } else {  // global memory: the 32-B f16 node (GNodeH)
@@ -335,9 +360,32 @@ __device__ __forceinline__ bool trav_node64(const Node *__restrict__ nodes, Stac
 // c = |oc|^2 - r*r, disc = h*h - a*c, roots (h -+ sqrt(disc)) / a in the open (0.001, closest).
 // (h + sq) / a >= (h - sq) / a, so the far root is tried only when the near one is <= 0.001 (or
 // NaN), exactly the roots the reference's surrounds() tests accept.
+#ifndef RRT_F64_DIVA
+#define RRT_F64_DIVA 0
+#endif
+// Per-ray reciprocal of a = |d|^2 for the root divisions: the reciprocal steps of the compiler's
+// IEEE f64 division expansion (v_rcp_f64 + two Newton steps) once per ray instead of per division.
+// For a in [2^-64, 2^64] v_div_scale is an identity on a, and on any numerator whose quotient is
+// not far below 0.001 (the acceptance bound), so quotient = fma(n - a q, r, q) with q = n r is the
+// expansion's own v_div_fmas result; 0 marks a ray outside that range (plain division).
+__device__ __forceinline__ double recip_a64(double a) {
+    if (!(a >= 0x1.0p-64 && a <= 0x1.0p64)) return 0.0;
+    double r = __builtin_amdgcn_rcp(a);
+    double e = __builtin_fma(-a, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    e = __builtin_fma(-a, r, 1.0);
+    return __builtin_fma(r, e, r);
+}
+__device__ __forceinline__ double div_a64(double n, double a, double ra) {
+    if (!RRT_F64_DIVA || ra == 0.0) return n / a;
+    const double q = n * ra;
+    return __builtin_fma(__builtin_fma(-a, q, n), ra, q);
+}
+
 template <bool kCount>
 __device__ __forceinline__ void leaves64(const float4 *__restrict__ prims, Leaves lv, D3 o, D3 d, double a, Trav64 &t,
                                          Counters &cnt) {
+    const double ra = RRT_F64_DIVA ? recip_a64(a) : 0.0;
     const int first = (int)(lv & kLinkFirstMask), count = (int)(lv >> kLinkCountShift);
     for (int i = first; i < first + count; ++i) {
         if (kCount) cnt.spheres++;
@@ -349,8 +397,8 @@ __device__ __forceinline__ void leaves64(const float4 *__restrict__ prims, Leave
         const double disc = h * h - a * c;
         if (disc < 0.0) continue;
         const double sq = __builtin_sqrt(disc);
-        double root = (h - sq) / a;
-        if (!(0.001 < root)) root = (h + sq) / a;
+        double root = div_a64(h - sq, a, ra);
+        if (!(0.001 < root)) root = div_a64(h + sq, a, ra);
         if (0.001 < root && root < t.closest) {
             t.closest = root;
             t.hit_prim = i;
@@ -394,6 +442,11 @@ __device__ __forceinline__ void camera_ray64(uint32_t x, uint32_t y, Path64 &ps)
 
 // After the closest-hit query: sky / background, or emission / scatter / RR (camera.rs:182-209).
 // Returns true when the path has ended; its radiance T * Le (if any) goes into `sum`.
+// kClass: kF64Full (every book-1 material kind), kF64Untextured (no image texture: the f64 acos /
+// atan2 / texel path compiled out), kF64Diffuse (Lambertian and emissive only: metal and dielectric
+// compiled out), chosen per scene by launch_render_pass_f64 like the f32 kernel's classes.
+constexpr int kF64Full = 0, kF64Untextured = 1, kF64Diffuse = 2;
+template <int kClass>
 __device__ __forceinline__ bool shade64(const KParams &P, const float4 *prims, const GMaterial *mtl, Path64 &ps, double t,
                                         int prim, D3 &sum) {
     if (prim < 0) {
@@ -421,12 +474,12 @@ __device__ __forceinline__ bool shade64(const KParams &P, const float4 *prims, c
         return true;
     }
     D3 att, dir;
-    if (kind == 1) {  // Metal (material.rs:53-64): unit(reflect) + fuzz * random_unit_vector
+    if (kClass != kF64Diffuse && kind == 1) {  // Metal (material.rs:53-64): unit(reflect) + fuzz * random_unit_vector
         const D3 refl = unit_vector(reflect(ps.d, nrm));
         dir = add(refl, muls(random_unit_vector(ps.rng), (double)m.a.w));
         if (!(dot(dir, nrm) > 0.0)) return true;  // absorbed
         att = albedo;
-    } else if (kind == 2) {  // Dielectric (material.rs:83-102)
+    } else if (kClass != kF64Diffuse && kind == 2) {  // Dielectric (material.rs:83-102)
         const double eta = (double)__int_as_float(m.b.y);
         const double ri = front ? 1.0 / eta : eta;
         const D3 ud = unit_vector(ps.d);
@@ -439,7 +492,7 @@ __device__ __forceinline__ bool shade64(const KParams &P, const float4 *prims, c
     } else {  // Lambertian, plain or image-textured (material.rs:28-40; the_next_week/material.rs:41-53)
         dir = add(nrm, random_unit_vector(ps.rng));
         if (__builtin_fabs(dir.x) < 1e-8 && __builtin_fabs(dir.y) < 1e-8 && __builtin_fabs(dir.z) < 1e-8) dir = nrm;
-        att = kind == 3 ? texel64(P, m.b.z, outward) : albedo;
+        att = (kClass != kF64Untextured && kind == 3) ? texel64(P, m.b.z, outward) : albedo;
     }
     if (ps.k >= 5u) {  // camera.rs:189-200
         double pr = att.x;
@@ -460,7 +513,7 @@ __device__ __forceinline__ bool shade64(const KParams &P, const float4 *prims, c
 
 // The persistent work loop of rrt_kernel.hip's render_body (same queue, units, chunk order,
 // postponed leaves and wave-uniform exits) over Path64 state.
-template <bool kLds, bool kCount, int kBlk>
+template <bool kLds, bool kCount, int kBlk, int kClass>
 __device__ __forceinline__ void render64_body(const KParams &P) {
     extern __shared__ uint4 lds_dyn[];
     uint16_t *lds_stack = reinterpret_cast<uint16_t *>(lds_dyn);
@@ -599,7 +652,7 @@ __device__ __forceinline__ void render64_body(const KParams &P) {
         __builtin_amdgcn_s_setprio(kPrioShade);
         if (has && !need_ray && tr.node < 0) {
             need_ray = 1;
-            seg_done = shade64(P, prims, mtl, ps, tr.closest, tr.hit_prim, sum) ? 1u : 0u;
+            seg_done = shade64<kClass>(P, prims, mtl, ps, tr.closest, tr.hit_prim, sum) ? 1u : 0u;
         }
         w_paths += (uint32_t)__popcll(__ballot(seg_done));
         if (seg_done) {  // pixel_color += ray_color(..): already in `sum`
@@ -641,11 +694,17 @@ __device__ __forceinline__ void render64_body(const KParams &P) {
     }
 }
 
-constexpr int kBlock64 = 256;  // threads per block of the f64 kernel
+#ifndef RRT_F64_BLOCK
+#define RRT_F64_BLOCK 256
+#endif
+#ifndef RRT_F64_WAVES
+#define RRT_F64_WAVES 4  // waves/SIMD bound of the untextured and diffuse classes (<= 128 VGPRs, no spills)
+#endif
+constexpr int kBlock64 = RRT_F64_BLOCK;  // threads per block of the f64 kernel
 
-template <bool kLds, bool kCount>
-__global__ __launch_bounds__(kBlock64) void rrt_render64(KParams P) {
-    render64_body<kLds, kCount, kBlock64>(P);
+template <bool kLds, bool kCount, int kClass>
+__global__ __launch_bounds__(kBlock64, kClass == kF64Full ? 1 : RRT_F64_WAVES) void rrt_render64(KParams P) {
+    render64_body<kLds, kCount, kBlock64, kClass>(P);
 }
 
 // The pass's f64 chunk sums into accum64, continuing the left fold over chunks in order (as
@@ -674,11 +733,11 @@ __global__ __launch_bounds__(256) void rrt_accum64_to_f32(const D4 *__restrict__
     a32[p] = make_float4((float)v.x, (float)v.y, (float)v.z, (float)v.w);
 }
 
-template <bool kLds>
+template <bool kLds, int kClass>
 hipError_t launch64(const KParams &p, bool count, hipStream_t stream) {
     size_t lds = ((size_t)p.stack_depth * kBlock64 * sizeof(uint16_t) + 15u) / 16u * 16u;
     if (kLds) lds += (size_t)p.n_nodes * sizeof(GNode) + (size_t)p.n_prims * kPrimBytes;
-    auto kernel = count ? rrt_render64<kLds, true> : rrt_render64<kLds, false>;
+    auto kernel = count ? rrt_render64<kLds, true, kClass> : rrt_render64<kLds, false, kClass>;
     int per_cu = 0;
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock64, lds);
     if (e != hipSuccess) return e;
@@ -697,7 +756,13 @@ hipError_t launch_render_pass_f64(const KParams &p, bool count, hipStream_t stre
     if (p.n_units == 0) return hipSuccess;
     if (p.bvh_width != 2 || p.prim_motion || p.stack_depth > (uint32_t)kMaxStackDepth || p.n_nodes > 65535u)
         return hipErrorInvalidValue;  // the host builds a 16-bit-stack BVH2 for book-1 scenes
-    hipError_t e = p.scene_in_lds ? launch64<true>(p, count, stream) : launch64<false>(p, count, stream);
+#ifndef RRT_F64_CLASSES
+#define RRT_F64_CLASSES 1
+#endif
+    hipError_t e;
+    if (RRT_F64_CLASSES && !p.specular) e = p.scene_in_lds ? launch64<true, kF64Diffuse>(p, count, stream) : launch64<false, kF64Diffuse>(p, count, stream);
+    else if (RRT_F64_CLASSES && !p.image_tex) e = p.scene_in_lds ? launch64<true, kF64Untextured>(p, count, stream) : launch64<false, kF64Untextured>(p, count, stream);
+    else e = p.scene_in_lds ? launch64<true, kF64Full>(p, count, stream) : launch64<false, kF64Full>(p, count, stream);
     if (e != hipSuccess || p.n_chunks <= 1) return e;
     const uint32_t n_pixels = p.tile_rows * p.width;
     hipLaunchKernelGGL(rrt_combine_chunks64, dim3((n_pixels + 255) / 256), dim3(256), 0, stream, p.partial64,

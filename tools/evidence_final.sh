@@ -15,7 +15,7 @@ cp gpurun_out/gpu_suite.log gpurun_out/profiles/${TAG}_gpu_suite.log
 step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
 TAG=$TAG CONFIGS="C2:512 C4:1024 C5:256 NW9:64:1080" bash tools/evidence_r3.sh || exit 1
 for c in C4 C5 NW9; do
-  step bench_$c 300 python3 bench.py --config $c --no-f64 --no-cpu-baseline --no-extra --no-breakdown
+  step bench_$c 300 python3 bench.py --config $c --no-cpu-baseline --no-extra --no-breakdown  # f64_books on C4 / C5
   grep -v "^W20\|amdgpu.ids" gpurun_out/bench_$c.log | tail -n 1 > gpurun_out/profiles/${TAG}_bench_$c.json
 done
 step scenes 600 python3 tools/bench_scenes.py
