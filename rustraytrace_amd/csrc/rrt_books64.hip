@@ -361,7 +361,7 @@ __device__ __forceinline__ bool trav_node64(const Node *__restrict__ nodes, Stac
 // (h + sq) / a >= (h - sq) / a, so the far root is tried only when the near one is <= 0.001 (or
 // NaN), exactly the roots the reference's surrounds() tests accept.
 #ifndef RRT_F64_DIVA
-#define RRT_F64_DIVA 0
+#define RRT_F64_DIVA 1
 #endif
 // Per-ray reciprocal of a = |d|^2 for the root divisions: the reciprocal steps of the compiler's
 // IEEE f64 division expansion (v_rcp_f64 + two Newton steps) once per ray instead of per division.

@@ -1,4 +1,4 @@
-"""Every compile-time arm left in the megakernel source is the shipped default or compiled here.
+"""Every compile-time arm left in the kernel sources is the shipped default or compiled here.
 
 rrt_kernel.hip keeps only debug builds (-DRRT_PHASE_TIMING=1..4: per-wave phase statistics,
 -DRRT_TRACE_X/Y/S: a printf trace of one path) and numeric tuning knobs (launch shapes, issue
@@ -28,6 +28,8 @@ VARIANTS = {
     "trace": ["-DRRT_TRACE_X=3", "-DRRT_TRACE_Y=4", "-DRRT_TRACE_S=5"],
     "knobs": ["-DRRT_BLOCK=256", "-DRRT_WAVES=4", "-DRRT_TILE_W=16", "-DRRT_B2_WAVES=1", "-DRRT_B2_BLOCK=512",
               "-DRRT_PRIO_REFILL=0", "-DRRT_PRIO_NODE=0", "-DRRT_PRIO_LEAF=0", "-DRRT_PRIO_SHADE=0"],
+    # rrt_books64.hip: the per-ray reciprocal root division, one class for every scene, launch shape
+    "f64_knobs": ["-DRRT_F64_DIVA=0", "-DRRT_F64_CLASSES=0", "-DRRT_F64_BLOCK=512", "-DRRT_F64_WAVES=2"],
 }
 
 
