@@ -695,7 +695,7 @@ __device__ __forceinline__ void render64_body(const KParams &P) {
 }
 
 #ifndef RRT_F64_BLOCK
-#define RRT_F64_BLOCK 256
+#define RRT_F64_BLOCK 512
 #endif
 #ifndef RRT_F64_WAVES
 #define RRT_F64_WAVES 4  // waves/SIMD bound of the untextured and diffuse classes (<= 128 VGPRs, no spills)
