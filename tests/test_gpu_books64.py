@@ -107,3 +107,31 @@ def test_f64_sample_passes_are_bit_identical(monkeypatch):
     monkeypatch.setenv("RRT_PARTIAL_MB", "1")
     b, _, _ = _gpu_f64(scene)
     assert np.array_equal(a, b)
+
+
+def _textured_specular_scene(image_width=64, samples_per_pixel=256):
+    """A book-1 scene with an image texture AND metal and dielectric materials: the f64 kernel's
+    full class (launch_render_pass_f64 picks it only when both are present; the BASELINE configs
+    run the untextured (C2, C5) and diffuse (C1, C4) classes)."""
+    from rustraytrace_amd import scenes as S
+
+    mats = np.concatenate([S._material(3, (0.0, 0.0, 0.0), tex=0), S._material(1, (0.7, 0.6, 0.5), fuzz=0.1),
+                           S._material(2, (1.0, 1.0, 1.0), ref_idx=1.5), S._material(0, (0.5, 0.5, 0.5)),
+                           S._material(4, (4.0, 4.0, 4.0))])
+    sph = np.concatenate([S._sphere((0.0, 0.0, 0.0), 2.0, 0), S._sphere((4.2, 0.0, 0.0), 1.5, 1),
+                          S._sphere((-4.2, 0.0, 0.0), 1.5, 2), S._sphere((0.0, -1002.0, 0.0), 1000.0, 3),
+                          S._sphere((0.0, 7.0, 0.0), 2.0, 4)])
+    cam = S.make_camera(aspect_ratio=16.0 / 9.0, image_width=image_width, samples_per_pixel=samples_per_pixel,
+                        max_depth=20, vfov=40.0, lookfrom=(0.0, 2.0, 14.0), lookat=(0.0, 0.0, 0.0),
+                        seed=0x7E57, n_spheres=len(sph))
+    return S.SceneData(cam, sph, mats, textures=[S.earth_texture()], name="textured_specular")
+
+
+def test_f64_full_class_matches_books_path():
+    scene = _textured_specular_scene()
+    gpu, gpu32, gpu_rays = _gpu_f64(scene)
+    books, books_rays, _ = oracle.render(scene, oracle.BOOKS, threads=16)
+    assert gpu_rays == books_rays, f"{gpu_rays} closest-hit queries vs BOOKS {books_rays}"
+    rel = _check(scene, gpu, books, "textured + specular")
+    assert rel < 1e-12
+    assert np.array_equal(gpu32, gpu.astype(np.float32))
