@@ -255,6 +255,9 @@ struct RayK64 {
     // byte offsets of the ray's (entry, exit) plane pair of each axis in a GNode child box (the
     // f32 kernel's RayK): 12a + 4 when 1/d_a < 0 (hi, lo), else 12a (lo, hi)
     uint32_t ox, oy, oz;
+    // the 32-B f16 node (GNodeH, global memory) holds lo | hi << 16 per axis: rotating the word by
+    // 16 bits when 1/d_a < 0 puts the (entry, exit) pair in (lo, hi) order
+    uint32_t rx, ry, rz;
 };
 __device__ __forceinline__ double clamp_inv64(double v) { return __builtin_fmax(__builtin_fmin(v, 0x1.0p500), -0x1.0p500); }
 __device__ __forceinline__ RayK64 ray_consts64(D3 o, D3 d) {
@@ -264,28 +267,19 @@ __device__ __forceinline__ RayK64 ray_consts64(D3 o, D3 d) {
     r.ox = r.inv.x < 0.0 ? 4u : 0u;
     r.oy = r.inv.y < 0.0 ? 16u : 12u;
     r.oz = r.inv.z < 0.0 ? 28u : 24u;
+    r.rx = r.inv.x < 0.0 ? 16u : 0u;
+    r.ry = r.inv.y < 0.0 ? 16u : 0u;
+    r.rz = r.inv.z < 0.0 ? 16u : 0u;
     return r;
 }
 // Slab test of a stored f32 box in f64 (role of Aabb::hit, aabb.rs:52-85: a box test only prunes).
 // The stored planes lie outside the f64 sphere box by the f32 slab bound (~2^-22 |P|, rrt_host.cpp
 // BoxSlack), far above this test's f64 rounding, so it never rejects a box whose sphere a ray hits.
-__device__ __forceinline__ bool box64(double lx, double hx, double ly, double hy, double lz, double hz, const RayK64 &rk,
-                                      double tmax, double &tnear) {
-    const double x0 = __builtin_fma(lx, rk.inv.x, -rk.oi.x), x1 = __builtin_fma(hx, rk.inv.x, -rk.oi.x);
-    const double y0 = __builtin_fma(ly, rk.inv.y, -rk.oi.y), y1 = __builtin_fma(hy, rk.inv.y, -rk.oi.y);
-    const double z0 = __builtin_fma(lz, rk.inv.z, -rk.oi.z), z1 = __builtin_fma(hz, rk.inv.z, -rk.oi.z);
-    const double nr = __builtin_fmax(__builtin_fmax(__builtin_fmin(x0, x1), __builtin_fmin(y0, y1)),
-                                     __builtin_fmax(__builtin_fmin(z0, z1), 0.001));
-    const double fr = __builtin_fmin(__builtin_fmin(__builtin_fmax(x0, x1), __builtin_fmax(y0, y1)),
-                                     __builtin_fmin(__builtin_fmax(z0, z1), tmax));
-    tnear = nr;
-    return nr < fr;
-}
-
-// box64 on planes given in (entry, exit) order per axis (GNode's lo, hi, lo layout read at the
-// ray's sign offsets): fma(P, inv, -oi) is monotone in P for a fixed inv, so the entry plane's
-// distance is exactly min(t_lo, t_hi) and the exit plane's the max — box64's values and decisions
-// without its six f64 min/max (rrt_kernel.hip box_hit_ordered).
+// The planes come in (entry, exit) order per axis (GNode's lo, hi, lo layout read at the ray's sign
+// offsets, or GNodeH's halves rotated by the sign): fma(P, inv, -oi) is monotone in P for a fixed
+// inv, so the entry plane's distance is exactly min(t_lo, t_hi) and the exit plane's the max — the
+// min/max slab's values and decisions without its twelve f64 min/max (rrt_kernel.hip
+// box_hit_ordered).
 __device__ __forceinline__ bool box64_ordered(double nx, double fx, double ny, double fy, double nz, double fz,
                                               const RayK64 &rk, double tmax, double &tnear) {
     const double x0 = __builtin_fma(nx, rk.inv.x, -rk.oi.x), x1 = __builtin_fma(fx, rk.inv.x, -rk.oi.x);
@@ -325,11 +319,14 @@ __device__ __forceinline__ bool trav_node64(const Node *__restrict__ nodes, Stac
                            plane(rk.oz + 36), plane(rk.oz + 40), rk, t.closest, tn1);
         l0 = n.link[0];
         l1 = n.link[1];
-    } else {  // global memory: the 32-B f16 node (GNodeH)
+    } else {  // global memory: the 32-B f16 node (GNodeH), each axis's halves in (entry, exit) order
         const uint4 *q = reinterpret_cast<const uint4 *>(nodes + t.node);
         const uint4 a = q[0], b = q[1];
-        h0 = box64(lo16(a.x), hi16(a.x), lo16(a.y), hi16(a.y), lo16(a.z), hi16(a.z), rk, t.closest, tn0);
-        h1 = box64(lo16(a.w), hi16(a.w), lo16(b.x), hi16(b.x), lo16(b.y), hi16(b.y), rk, t.closest, tn1);
+        auto ord = [](uint32_t w, uint32_t r) { return __builtin_amdgcn_alignbit(w, w, r); };
+        const uint32_t x0 = ord(a.x, rk.rx), y0 = ord(a.y, rk.ry), z0 = ord(a.z, rk.rz);
+        const uint32_t x1 = ord(a.w, rk.rx), y1 = ord(b.x, rk.ry), z1 = ord(b.y, rk.rz);
+        h0 = box64_ordered(lo16(x0), hi16(x0), lo16(y0), hi16(y0), lo16(z0), hi16(z0), rk, t.closest, tn0);
+        h1 = box64_ordered(lo16(x1), hi16(x1), lo16(y1), hi16(y1), lo16(z1), hi16(z1), rk, t.closest, tn1);
         l0 = b.z;
         l1 = b.w;
     }
