@@ -298,6 +298,16 @@ struct Trav64 {
     int sp;
 };
 
+// A GNode with its planes widened to f64 (exact) while the block stages the tree in LDS: the node
+// step then reads the (entry, exit) pairs as doubles instead of converting twelve f32 planes per
+// visit. 160 B (box[c][3a .. 3a+2] = lo, hi, lo as in GNode).
+struct alignas(16) GNode64 {
+    double box[2][9];
+    uint32_t link[2];
+    uint32_t pad[2];
+};
+static_assert(sizeof(GNode64) == 160, "GNode64 must be 160 B");
+
 // One BVH2 node visit (rrt_kernel.hip trav_node's schedule): both child boxes against the closest
 // hit so far, hit leaf children postponed as one primitive range, the nearer internal child next
 // and the farther one pushed. The visiting order only prunes: the closest hit is the smallest
@@ -309,7 +319,17 @@ __device__ __forceinline__ bool trav_node64(const Node *__restrict__ nodes, Stac
     bool h0, h1;
     uint32_t l0, l1;
     double tn0 = 0.0, tn1 = 0.0;
-    if constexpr (std::is_same<Node, GNode>::value) {
+    if constexpr (std::is_same<Node, GNode64>::value) {
+        const GNode64 &n = nodes[t.node];  // LDS, f64 planes: the f32 byte offsets doubled
+        const char *bx = reinterpret_cast<const char *>(&n.box[0][0]);
+        auto plane = [&](uint32_t byte_off) { return *reinterpret_cast<const double *>(bx + 2u * byte_off); };
+        h0 = box64_ordered(plane(rk.ox), plane(rk.ox + 4), plane(rk.oy), plane(rk.oy + 4), plane(rk.oz),
+                           plane(rk.oz + 4), rk, t.closest, tn0);
+        h1 = box64_ordered(plane(rk.ox + 36), plane(rk.ox + 40), plane(rk.oy + 36), plane(rk.oy + 40),
+                           plane(rk.oz + 36), plane(rk.oz + 40), rk, t.closest, tn1);
+        l0 = n.link[0];
+        l1 = n.link[1];
+    } else if constexpr (std::is_same<Node, GNode>::value) {
         const GNode &n = nodes[t.node];  // LDS: lo, hi, lo per axis, each pair read at the ray's sign offset
         const char *bx = reinterpret_cast<const char *>(&n.box[0][0]);
         auto plane = [&](uint32_t byte_off) { return (double)*reinterpret_cast<const float *>(bx + byte_off); };
@@ -510,15 +530,21 @@ __device__ __forceinline__ bool shade64(const KParams &P, const float4 *prims, c
 
 // The persistent work loop of rrt_kernel.hip's render_body (same queue, units, chunk order,
 // postponed leaves and wave-uniform exits) over Path64 state.
-template <bool kLds, bool kCount, int kBlk, int kClass>
+// kMode: kF64Global (f16 nodes and records read from global memory), kF64Lds (the f32 nodes,
+// spheres and materials staged in LDS), kF64LdsWide (nodes widened to f64 and spheres in LDS,
+// materials from global memory — one read per hit — to stay within the block's 64 KB).
+constexpr int kF64Global = 0, kF64Lds = 1, kF64LdsWide = 2;
+template <int kMode, bool kCount, int kBlk, int kClass>
 __device__ __forceinline__ void render64_body(const KParams &P) {
+    constexpr bool kLds = kMode != kF64Global;
     extern __shared__ uint4 lds_dyn[];
     uint16_t *lds_stack = reinterpret_cast<uint16_t *>(lds_dyn);
-    using Node = typename std::conditional<kLds, GNode, GNodeH>::type;
+    using Node = typename std::conditional<kMode == kF64LdsWide, GNode64,
+                                           typename std::conditional<kLds, GNode, GNodeH>::type>::type;
     const Node *nodes = reinterpret_cast<const Node *>(P.nodes);
     const float4 *prims = P.prim_cr;
     const GMaterial *mtl = P.prim_mtl;
-    if constexpr (kLds) {  // stage nodes + spheres + their materials once per block
+    if constexpr (kMode == kF64Lds) {  // stage nodes + spheres + their materials once per block
         uint4 *dst = lds_dyn + (P.stack_depth * kBlk * sizeof(uint16_t) + 15u) / 16u;
         const uint4 *src_n = reinterpret_cast<const uint4 *>(P.nodes);
         const uint32_t nn = P.n_nodes * (uint32_t)(sizeof(Node) / 16);
@@ -532,6 +558,26 @@ __device__ __forceinline__ void render64_body(const KParams &P) {
         nodes = reinterpret_cast<const Node *>(dst);
         prims = reinterpret_cast<const float4 *>(dst + nn);
         mtl = reinterpret_cast<const GMaterial *>(dst + nn + P.n_prims);
+    } else if constexpr (kMode == kF64LdsWide) {  // nodes widened to f64 (exact) + spheres
+        uint4 *dst = lds_dyn + (P.stack_depth * kBlk * sizeof(uint16_t) + 15u) / 16u;
+        GNode64 *dn = reinterpret_cast<GNode64 *>(dst);
+        const GNode *sn = reinterpret_cast<const GNode *>(P.nodes);
+        for (uint32_t i = threadIdx.x; i < P.n_nodes; i += kBlk) {
+            const GNode g = sn[i];
+            GNode64 w;
+            for (int c = 0; c < 2; ++c)
+                for (int k = 0; k < 9; ++k) w.box[c][k] = (double)g.box[c][k];
+            w.link[0] = g.link[0];
+            w.link[1] = g.link[1];
+            w.pad[0] = w.pad[1] = 0u;
+            dn[i] = w;
+        }
+        const uint32_t nn = P.n_nodes * (uint32_t)(sizeof(GNode64) / 16);
+        const uint4 *src_p = reinterpret_cast<const uint4 *>(P.prim_cr);
+        for (uint32_t i = threadIdx.x; i < P.n_prims; i += kBlk) dst[nn + i] = src_p[i];
+        __syncthreads();
+        nodes = reinterpret_cast<const Node *>(dst);
+        prims = reinterpret_cast<const float4 *>(dst + nn);
     }
     LdsStack<uint16_t, kBlk> stack;
     stack.init(lds_stack, threadIdx.x);
@@ -699,9 +745,9 @@ __device__ __forceinline__ void render64_body(const KParams &P) {
 #endif
 constexpr int kBlock64 = RRT_F64_BLOCK;  // threads per block of the f64 kernel
 
-template <bool kLds, bool kCount, int kClass>
+template <int kMode, bool kCount, int kClass>
 __global__ __launch_bounds__(kBlock64, kClass == kF64Full ? 1 : RRT_F64_WAVES) void rrt_render64(KParams P) {
-    render64_body<kLds, kCount, kBlock64, kClass>(P);
+    render64_body<kMode, kCount, kBlock64, kClass>(P);
 }
 
 // The pass's f64 chunk sums into accum64, continuing the left fold over chunks in order (as
@@ -730,11 +776,18 @@ __global__ __launch_bounds__(256) void rrt_accum64_to_f32(const D4 *__restrict__
     a32[p] = make_float4((float)v.x, (float)v.y, (float)v.z, (float)v.w);
 }
 
-template <bool kLds, int kClass>
-hipError_t launch64(const KParams &p, bool count, hipStream_t stream) {
+// LDS of the f64 kernel's block in each mode (stack, then the staged scene)
+size_t lds64_bytes(const KParams &p, int mode) {
     size_t lds = ((size_t)p.stack_depth * kBlock64 * sizeof(uint16_t) + 15u) / 16u * 16u;
-    if (kLds) lds += (size_t)p.n_nodes * sizeof(GNode) + (size_t)p.n_prims * kPrimBytes;
-    auto kernel = count ? rrt_render64<kLds, true, kClass> : rrt_render64<kLds, false, kClass>;
+    if (mode == kF64Lds) lds += (size_t)p.n_nodes * sizeof(GNode) + (size_t)p.n_prims * kPrimBytes;
+    if (mode == kF64LdsWide) lds += (size_t)p.n_nodes * sizeof(GNode64) + (size_t)p.n_prims * 16u;
+    return lds;
+}
+
+template <int kMode, int kClass>
+hipError_t launch64(const KParams &p, bool count, hipStream_t stream) {
+    const size_t lds = lds64_bytes(p, kMode);
+    auto kernel = count ? rrt_render64<kMode, true, kClass> : rrt_render64<kMode, false, kClass>;
     int per_cu = 0;
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock64, lds);
     if (e != hipSuccess) return e;
@@ -747,6 +800,18 @@ hipError_t launch64(const KParams &p, bool count, hipStream_t stream) {
     return hipGetLastError();
 }
 
+#ifndef RRT_F64_WIDE
+#define RRT_F64_WIDE 1
+#endif
+// The scene placement: global memory for f16-node scenes; for LDS scenes the f64-widened nodes
+// when they fit the 64 KB a block may declare, else the f32 nodes.
+template <int kClass>
+hipError_t launch64_placed(const KParams &p, bool count, hipStream_t stream) {
+    if (!p.scene_in_lds) return launch64<kF64Global, kClass>(p, count, stream);
+    if (RRT_F64_WIDE && lds64_bytes(p, kF64LdsWide) <= 64u * 1024u) return launch64<kF64LdsWide, kClass>(p, count, stream);
+    return launch64<kF64Lds, kClass>(p, count, stream);
+}
+
 }  // namespace
 
 hipError_t launch_render_pass_f64(const KParams &p, bool count, hipStream_t stream) {
@@ -757,9 +822,9 @@ hipError_t launch_render_pass_f64(const KParams &p, bool count, hipStream_t stre
 #define RRT_F64_CLASSES 1
 #endif
     hipError_t e;
-    if (RRT_F64_CLASSES && !p.specular) e = p.scene_in_lds ? launch64<true, kF64Diffuse>(p, count, stream) : launch64<false, kF64Diffuse>(p, count, stream);
-    else if (RRT_F64_CLASSES && !p.image_tex) e = p.scene_in_lds ? launch64<true, kF64Untextured>(p, count, stream) : launch64<false, kF64Untextured>(p, count, stream);
-    else e = p.scene_in_lds ? launch64<true, kF64Full>(p, count, stream) : launch64<false, kF64Full>(p, count, stream);
+    if (RRT_F64_CLASSES && !p.specular) e = launch64_placed<kF64Diffuse>(p, count, stream);
+    else if (RRT_F64_CLASSES && !p.image_tex) e = launch64_placed<kF64Untextured>(p, count, stream);
+    else e = launch64_placed<kF64Full>(p, count, stream);
     if (e != hipSuccess || p.n_chunks <= 1) return e;
     const uint32_t n_pixels = p.tile_rows * p.width;
     hipLaunchKernelGGL(rrt_combine_chunks64, dim3((n_pixels + 255) / 256), dim3(256), 0, stream, p.partial64,

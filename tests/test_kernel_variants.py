@@ -28,8 +28,10 @@ VARIANTS = {
     "trace": ["-DRRT_TRACE_X=3", "-DRRT_TRACE_Y=4", "-DRRT_TRACE_S=5"],
     "knobs": ["-DRRT_BLOCK=256", "-DRRT_WAVES=4", "-DRRT_TILE_W=16", "-DRRT_B2_WAVES=1", "-DRRT_B2_BLOCK=512",
               "-DRRT_PRIO_REFILL=0", "-DRRT_PRIO_NODE=0", "-DRRT_PRIO_LEAF=0", "-DRRT_PRIO_SHADE=0"],
-    # rrt_books64.hip: the per-ray reciprocal root division, one class for every scene, launch shape
-    "f64_knobs": ["-DRRT_F64_DIVA=0", "-DRRT_F64_CLASSES=0", "-DRRT_F64_BLOCK=256", "-DRRT_F64_WAVES=2"],
+    # rrt_books64.hip: the per-ray reciprocal root division, one class for every scene, f32 nodes in
+    # LDS for every LDS scene, launch shape
+    "f64_knobs": ["-DRRT_F64_DIVA=0", "-DRRT_F64_CLASSES=0", "-DRRT_F64_WIDE=0", "-DRRT_F64_BLOCK=256",
+                  "-DRRT_F64_WAVES=2"],
 }
 
 
