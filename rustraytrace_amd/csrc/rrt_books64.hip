@@ -31,6 +31,7 @@
 // rounded outward and grown by the f32 slab bound, tested in f64: conservative) as the f32 kernel.
 #include "rrt_internal.h"
 
+#include <cstdlib>
 #include <type_traits>
 
 namespace rrt {
@@ -805,10 +806,14 @@ hipError_t launch64(const KParams &p, bool count, hipStream_t stream) {
 #endif
 // The scene placement: global memory for f16-node scenes; for LDS scenes the f64-widened nodes
 // when they fit the 64 KB a block may declare, else the f32 nodes.
+// RRT_F64_LDS_F32 (environment, test mode): keep the f32 LDS layout, so the fallback runs on
+// scenes whose widened tree would fit.
 template <int kClass>
 hipError_t launch64_placed(const KParams &p, bool count, hipStream_t stream) {
     if (!p.scene_in_lds) return launch64<kF64Global, kClass>(p, count, stream);
-    if (RRT_F64_WIDE && lds64_bytes(p, kF64LdsWide) <= 64u * 1024u) return launch64<kF64LdsWide, kClass>(p, count, stream);
+    const char *f32_layout = std::getenv("RRT_F64_LDS_F32");
+    const bool wide_ok = !(f32_layout && std::atoi(f32_layout) != 0) && lds64_bytes(p, kF64LdsWide) <= 64u * 1024u;
+    if (RRT_F64_WIDE && wide_ok) return launch64<kF64LdsWide, kClass>(p, count, stream);
     return launch64<kF64Lds, kClass>(p, count, stream);
 }
 

@@ -135,3 +135,15 @@ def test_f64_full_class_matches_books_path():
     rel = _check(scene, gpu, books, "textured + specular")
     assert rel < 1e-12
     assert np.array_equal(gpu32, gpu.astype(np.float32))
+
+
+@pytest.mark.parametrize("cfg", ["C1", "C2"])
+def test_f64_f32_lds_layout_fallback_matches_books_path(cfg, monkeypatch):
+    """Scenes whose f64-widened tree exceeds a block's 64 KB keep the f32 LDS layout (planes
+    converted per visit, materials in LDS); RRT_F64_LDS_F32 forces that layout on a small scene."""
+    monkeypatch.setenv("RRT_F64_LDS_F32", "1")
+    scene = rrt.config_scene(cfg, image_width=64, samples_per_pixel=128)
+    gpu, _, gpu_rays = _gpu_f64(scene)
+    books, books_rays, _ = oracle.render(scene, oracle.BOOKS, threads=16)
+    assert gpu_rays == books_rays
+    _check(scene, gpu, books, f"{cfg} f32 LDS layout")
