@@ -8,17 +8,20 @@ on the device by the kernel itself.
 * N = 1 (default): config C2, 1920x1080x512 spp (BASELINE.json configs[1], the metric's config),
   the whole frame on one GPU, no gather. The line also carries a 1-GPU C3 frame (`c3_one_gpu`,
   the strong-scaling base of the N > 1 runs), the C1 CPU-path config timed on the CPU and the
-  GPU (`c1`), the wall-clock split, the CPU baseline, and the reference's own GPU kernel (its
-  CUDA_SOURCE built for gfx950, oracle/_ref) timed beside this backend on a bounded sample of the
-  same workload (`reference_gpu_slot`).
-* N > 1 (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): config C3,
+  GPU (`c1`), the wall-clock split, the CPU baseline, and (opt-in, `--ref-slot`) the reference's
+  own GPU kernel (its CUDA_SOURCE built for gfx950, oracle/_ref) timed beside this backend on a
+  bounded sample of the same workload (`reference_gpu_slot`).
+* N > 1 (`python bench.py --gpus N` starts `python -m torch.distributed.run --nproc-per-node N
+  bench.py --gpus N` as a child process before touching any device and forwards rank 0's line;
+  under an external launcher WORLD_SIZE must equal N): config C3,
   3840x2160x2048 spp, tile-split the north star's way: row bands (10 rows at
   2/4/8 ranks, so every rank owns 2160/N rows; `distributed.balanced_band`) dealt in serpentine order (period p of
   N bands: ranks 0..N-1 for even p, N-1..0 for odd p; `distributed.band_owner`), every rank renders its bands over
   all samples, and the
   float tiles are gathered to rank 0 over RCCL inside the timed step (`distributed.gather_rows`).
   Strong scaling: the frame is fixed, value = all ranks' rays / the max over ranks of the timed
-  wall-clock. `--split samples` is the opt-in weak-scaling mode (every rank renders the whole
+  wall-clock. The line carries each rank's kernel time, the gather time and the same frame on
+  rank 0's GPU alone (`c3_one_gpu`), so `scaling_efficiency` is in the line. `--split samples` is the opt-in weak-scaling mode (every rank renders the whole
   frame over its own sample range; partial accums summed on rank 0 in rank order).
 """
 from __future__ import annotations
@@ -52,7 +55,7 @@ SCENES = {
 }
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -69,14 +72,58 @@ def parse():
     ap.add_argument("--no-breakdown", action="store_true", help="skip the wall-clock split (one extra frame)")
     ap.add_argument("--no-extra", action="store_true", help="skip the 1-GPU C3 frame and the C1 timings")
     ap.add_argument("--no-f64", action="store_true", help="skip the f64 books-arithmetic frame (f64_books)")
-    ap.add_argument("--no-ref-slot", action="store_true",
-                    help="skip timing the reference's own GPU kernel on a bounded sample (reference_gpu_slot)")
+    ap.add_argument("--ref-slot", action="store_true",
+                    help="also time the reference's own GPU kernel on a bounded sample (reference_gpu_slot; opt-in: "
+                         "a third-party kernel, kept out of the default run)")
     ap.add_argument("--issue-json", default=None,
                     help="issue-side PMC record (tools/pmc_issue.py); default profiles/issue_<config>.json")
     ap.add_argument("--traffic-json", default=None,
                     help="per-launch HBM bytes from rocprofv3 PMC passes (tools/pmc_traffic.py); "
                          "default profiles/traffic_<config>.json")
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def launcher_command(args, argv, env):
+    """The child launch `python bench.py --gpus N` (N > 1) needs when no launcher started it, or
+    None: one process per GPU, torch.distributed.run over 127.0.0.1 with this same argument list.
+    Decided from the arguments and the environment alone — the parent never imports torch or
+    touches a device, so it never holds a GPU context that a child (or an exec) could collide
+    with."""
+    if args.gpus <= 1 or "WORLD_SIZE" in env:
+        return None
+    port = env.get("MASTER_PORT")
+    if not port:
+        import socket
+
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = str(s.getsockname()[1])
+        s.close()
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def run_launcher(cmd):
+    """Run the N-rank child and forward rank 0's JSON line to stdout (everything else the ranks
+    print goes to stderr, so stdout carries exactly the one line); the child's exit status is
+    returned, non-zero when any rank failed."""
+    import subprocess
+
+    print(f"bench.py: launching {' '.join(cmd[2:5])} (one process per GPU)", file=sys.stderr, flush=True)
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, bufsize=1)
+    forwarded = False
+    for line in proc.stdout:
+        if not forwarded and line.startswith("{") and '"metric"' in line:
+            sys.stdout.write(line)
+            sys.stdout.flush()
+            forwarded = True
+        else:
+            sys.stderr.write(line)
+    rc = proc.wait()
+    if rc == 0 and not forwarded:
+        print("bench.py: the ranks exited without a result line", file=sys.stderr)
+        return 1
+    return rc
 
 
 def host_cpus():
@@ -175,17 +222,17 @@ def c1_timings(cpus):
     }
 
 
-def c3_one_gpu():
-    """One whole C3 frame (3840x2160x2048 spp) on this GPU: the 1-GPU base of the N > 1 strong
-    scaling runs (same config, same band split with one rank)."""
+def one_gpu_frame(config="C3", kw=None, device=0):
+    """One whole frame of `config` (default C3, 3840x2160x2048 spp) on one GPU: the 1-GPU base of
+    the N > 1 strong-scaling runs (same workload, the band split with one rank, no gather)."""
     import torch
 
     import rustraytrace_amd as rrt
 
-    scene = rrt.config_scene("C3")
-    ds = rrt.DeviceScene(scene)
+    scene = rrt.named_scene(config, **(kw or {}))
+    ds = rrt.DeviceScene(scene, device=device)
     tile = ds.tile(BAND_ROWS, 0, 1, 0, scene.spp)
-    buf = torch.empty((scene.height, scene.width, 4), dtype=torch.float32, device="cuda")
+    buf = torch.empty((scene.height, scene.width, 4), dtype=torch.float32, device=f"cuda:{device}")
     stream = torch.cuda.current_stream()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
@@ -198,7 +245,7 @@ def c3_one_gpu():
     rays = ds.counters()["rays"]
     ds.close()
     del buf
-    return {"workload": f"C3 {scene.width}x{scene.height}x{scene.spp}spp, 1 GPU, one frame (no warmup frame)",
+    return {"workload": f"{config} {scene.width}x{scene.height}x{scene.spp}spp, 1 GPU, one frame (no warmup frame)",
             "frame_s": round(wall, 4), "kernel_ms": round(a.elapsed_time(b), 2), "rays": rays,
             "mrays_s": round(rays / wall / 1e6, 2)}
 
@@ -381,6 +428,9 @@ def load_issue(path, config, W, S, lib_path):
 
 def main():
     args = parse()
+    cmd = launcher_command(args, sys.argv[1:], os.environ)
+    if cmd is not None:  # --gpus N without a launcher: start the N ranks as a child, never exec
+        sys.exit(run_launcher(cmd))
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -391,6 +441,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if "WORLD_SIZE" in os.environ and world != args.gpus:
+        sys.exit(f"bench.py: launched with WORLD_SIZE={world} but --gpus {args.gpus}")
     # RCCL ("nccl") between one process per GPU. RRT_BENCH_BACKEND=gloo is a rehearsal mode for
     # ranks sharing a GPU (device = local rank mod device count; host copies for the gather).
     backend = os.environ.get("RRT_BENCH_BACKEND", "nccl")
@@ -466,14 +518,21 @@ def main():
     ctr = ds.counters()
     rays = ctr["rays"]
     kmax = float(np.mean(kernel_ms))
+    rank_kernel_ms = [kmax]
+    one_gpu = None
     if world > 1:
         red_dev = f"cuda:{device}" if backend == "nccl" else "cpu"
-        t = torch.tensor([elapsed, kmax], dtype=torch.float64, device=red_dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kmax = float(t[0].item()), float(t[1].item())
-        r = torch.tensor([rays], dtype=torch.int64, device=red_dev)
-        dist.all_reduce(r, op=dist.ReduceOp.SUM)
-        rays = int(r.item())
+        every = [torch.zeros(3, dtype=torch.float64, device=red_dev) for _ in range(world)]
+        dist.all_gather(every, torch.tensor([elapsed, kmax, rays], dtype=torch.float64, device=red_dev))
+        every = torch.stack(every).cpu().numpy()
+        elapsed, kmax = float(every[:, 0].max()), float(every[:, 1].max())
+        rank_kernel_ms = [float(v) for v in every[:, 1]]
+        rays = int(every[:, 2].sum())
+        if rank == 0 and bands and not args.no_extra:
+            # the strong-scaling base on this node: the same frame on rank 0's GPU alone, after the
+            # timed region (the other ranks wait at the barrier below)
+            one_gpu = one_gpu_frame(config, kw, device)
+        dist.barrier()
 
     if rank == 0:
         work = ds.count_work(tile)  # instrumented twin kernel: same paths, per-launch work counts
@@ -559,16 +618,25 @@ def main():
             out["gather_note"] = "rank 0, HIP events between the end of its render and the end of the gather"
             if bands:
                 out["rows_per_rank"] = [len(band_rows(H, band, r, world)) for r in range(world)]
+        if world > 1:
+            out["kernel_ms_per_rank"] = [round(v, 3) for v in rank_kernel_ms]
+            out["kernel_ms_mean_over_ranks"] = round(float(np.mean(rank_kernel_ms)), 3)
+            out["rank_imbalance"] = round(max(rank_kernel_ms) / float(np.mean(rank_kernel_ms)) - 1.0, 5)
+            if one_gpu is not None:
+                out["c3_one_gpu" if config == "C3" else "one_gpu_base"] = one_gpu
+                out["scaling_efficiency"] = round(out["value"] / (world * one_gpu["mrays_s"]), 4)
+                out["scaling_note"] = ("value / (n_gpus x the same frame on rank 0's GPU alone, measured in this run "
+                                       "after the timed steps)")
         if world == 1 and not args.no_breakdown:
             out["wall_clock_breakdown"] = wall_clock_breakdown(scene, accum, avg_kernel_s * 1e3)
         cpus = host_cpus()
         if world == 1 and not args.no_extra:
             if config != "C3":
-                out["c3_one_gpu"] = c3_one_gpu()
+                out["c3_one_gpu"] = one_gpu_frame("C3")
             out["c1"] = c1_timings(cpus)
         if world == 1 and not args.no_f64 and config in ("C1", "C2", "C4", "C5"):
             out["f64_books"] = f64_books_frame(config)
-        if world == 1 and not args.no_ref_slot and config in ("C1", "C2", "C5"):
+        if world == 1 and args.ref_slot and config in ("C1", "C2", "C5"):
             out["reference_gpu_slot"] = reference_gpu_slot(config)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(scene, args.cpu_seconds, cpus)

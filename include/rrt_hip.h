@@ -542,6 +542,12 @@ int32_t rrt_write_pnm_from_rgb8(uint32_t width, uint32_t height, const uint8_t *
 /* Number of visible HIP devices (0 when no GPU). */
 int32_t rrt_device_count(int32_t *count);
 
+/* Test support, not part of the drop-in (no reference counterpart): on != 0 lets a one-shot render
+ * (rrt_hip_render*, n_gpus > 1) run worker g on device g % device_count, so the multi-device path
+ * runs on a one-GPU box (tests/test_gpu_multidevice.py). Off by default and at every load of the
+ * library: without it n_gpus must not exceed the visible devices. Process-wide. */
+void rrt_testing_device_wrap(int32_t on);
+
 #ifdef __cplusplus
 }
 #endif

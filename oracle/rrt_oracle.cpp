@@ -565,6 +565,10 @@ template <class T> struct World {
     std::vector<Texture> texs;
     std::vector<PerlinT<T>> perlin;
     bool book2 = false;  // moving spheres or checker / noise materials (kernel: kBook2)
+    // diagnostic mode bit 0x800 (BOOKS only): the sphere UV's acos / atan2 from this host's libm, as
+    // the reference's f64::acos / atan2 compute them, instead of the fdlibm restatement the f64
+    // kernel shares (tests/test_gpu_books64.py counts what the difference changes)
+    bool libm_trig = false;
     std::vector<BvhNode<T>> nodes;
     ChildRef root{false, -1};
     // f32 modes: the unbounded media's primitive ids, tested after the tree walk (not in the tree;
@@ -1219,8 +1223,14 @@ bool world_hit(const World<T> &w, Vec3<T> o, Vec3<T> d, T time, uint64_t seg, Re
 template <class T>
 Vec3<T> texture_value(const World<T> &w, uint32_t tex, Vec3<T> outward) {
     // get_sphere_uv (the_next_week/sphere.rs:46-52)
-    const T theta = t_acos<T>(-outward.y());
-    const T phi = t_atan2<T>(-outward.z(), outward.x()) + t_pi<T>();
+    T theta, phi;
+    if (std::is_same_v<T, double> && w.libm_trig) {
+        theta = (T)std::acos((double)-outward.y());
+        phi = (T)std::atan2((double)-outward.z(), (double)outward.x()) + t_pi<T>();
+    } else {
+        theta = t_acos<T>(-outward.y());
+        phi = t_atan2<T>(-outward.z(), outward.x()) + t_pi<T>();
+    }
     T u = phi / (T(2) * t_pi<T>());
     T v = theta / t_pi<T>();
     const Texture &t = w.texs[tex];
@@ -1701,6 +1711,7 @@ int render(const RrtCamera *c, const RrtSphere *s, uint32_t n, const RrtMaterial
     // choice of testing them after the walk does not change the image)
     load_world(w, cam, c, s, n, m, nm, tex, ntex, flags, ext, (mode & 0x400) != 0);
     cam.no_exit_skip = (mode & 0x200) != 0;
+    w.libm_trig = (mode & 0x800) != 0;
     if (y1 > cam.height) y1 = cam.height;
     if (y0 > y1) return -1;
     std::atomic<uint32_t> next_row{y0};

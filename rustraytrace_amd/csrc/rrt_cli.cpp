@@ -17,6 +17,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <optional>
 #include <string>
 #include <vector>
 
@@ -106,6 +107,24 @@ static void usage() {
                  "the_rest_of_your_life\n");
 }
 
+// Rust's `str::parse::<i32>()`: an optional '+' or '-', then at least one ASCII digit and nothing
+// else (no whitespace), the value within i32; anything else is an error (None).
+static std::optional<int> parse_i32(const std::string &a) {
+    size_t i = 0;
+    bool neg = false;
+    if (i < a.size() && (a[i] == '+' || a[i] == '-')) neg = a[i++] == '-';
+    if (i == a.size()) return std::nullopt;
+    int64_t v = 0;
+    for (; i < a.size(); ++i) {
+        if (a[i] < '0' || a[i] > '9') return std::nullopt;
+        v = v * 10 + (a[i] - '0');
+        if (v > (int64_t)INT32_MAX + 1) return std::nullopt;
+    }
+    if (neg) v = -v;
+    if (v < INT32_MIN || v > INT32_MAX) return std::nullopt;
+    return (int)v;
+}
+
 int main(int argc, char **argv) {
     std::string backend = "hip";
     std::vector<std::string> positional;
@@ -179,11 +198,7 @@ int main(int argc, char **argv) {
     // `match scene.unwrap_or(0)`: 1-9 name a scene, anything else (missing, unparsable, 0, 10, -1)
     // is the default arm final_scene(400, 250, 4) = rrt_build_next_week_scene's scene 10
     int scene = 0;
-    if (positional.size() > 1) {
-        char *end = nullptr;
-        const long v = std::strtol(positional[1].c_str(), &end, 10);
-        if (end && *end == 0 && end != positional[1].c_str()) scene = (int)v;
-    }
+    if (positional.size() > 1) scene = parse_i32(positional[1]).value_or(0);
     const int nw_scene = (scene >= 1 && scene <= 9) ? scene : 10;
     if (!book1 && !book2 && !book3) {  // main.rs:59-70, 93-97
         std::fprintf(stderr, "Usage: rrt [--backend hip] <book> [scene]\n"

@@ -1495,14 +1495,14 @@ int32_t rrt_scene_count_work(RrtScene *scene, const RrtTile *tile, RrtCounters *
 // ---- one-shot drop-in (cuda/mod.rs:342-439) ---------------------------------------------
 }  // extern "C"
 
-// Test mode RRT_DEVICE_WRAP=1: worker g of a one-shot render runs on device g % device_count, so
-// the multi-device path (threads, row bands, the strided copies into the caller's image) runs with
-// n_gpus > 1 on a one-GPU box (tests/test_gpu_multidevice.py). Off by default: n_gpus must not
-// exceed the visible devices.
-static bool device_wrap() {
-    const char *e = std::getenv("RRT_DEVICE_WRAP");
-    return e && std::atoi(e) != 0;
-}
+// Test mode (rrt_testing_device_wrap(1), a test-only entry point; no environment variable reaches
+// it): worker g of a one-shot render runs on device g % device_count, so the multi-device path
+// (threads, row bands, the strided copies into the caller's image) runs with n_gpus > 1 on a
+// one-GPU box (tests/test_gpu_multidevice.py). Off by default: n_gpus must not exceed the visible
+// devices.
+static std::atomic<bool> g_device_wrap{false};
+extern "C" void rrt_testing_device_wrap(int32_t on) { g_device_wrap.store(on != 0); }
+static bool device_wrap() { return g_device_wrap.load(); }
 
 // One-shot frame on n_gpus devices: float accum rows (accum_out), f64 accum rows (accum64_out, the
 // RRT_FLAG_F64 kernel) or render_io-quantised rows (rgb8_out, quantised on the device) assembled

@@ -83,3 +83,17 @@ def test_balanced_band_gives_every_rank_equal_rows():
         assert b == 16
         allr = np.concatenate([band_rows(H, b, r, n) for r in range(n)])
         assert sorted(allr.tolist()) == list(range(H))
+
+
+def test_c3_eight_rank_partition_covers_every_row_once():
+    # the partition bench.py --gpus 8 times: 10-row serpentine bands, 27 per rank, 270 rows each
+    from rustraytrace_amd.distributed import balanced_band, band_owner
+
+    band = balanced_band(2160, 8)
+    assert band == 10
+    per = [band_rows(2160, band, r, 8) for r in range(8)]
+    assert [len(p) for p in per] == [270] * 8
+    allr = np.concatenate(per)
+    assert sorted(allr.tolist()) == list(range(2160))
+    for r, rows in enumerate(per):
+        assert all(band_owner(int(y) // band, 8) == r for y in rows)

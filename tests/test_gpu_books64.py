@@ -147,3 +147,23 @@ def test_f64_f32_lds_layout_fallback_matches_books_path(cfg, monkeypatch):
     books, books_rays, _ = oracle.render(scene, oracle.BOOKS, threads=16)
     assert gpu_rays == books_rays
     _check(scene, gpu, books, f"{cfg} f32 LDS layout")
+
+
+@pytest.mark.parametrize("size,rows", [((64, 256), None), ((None, None), (536, 544))])
+def test_f64_textured_matches_books_with_libm_trig(size, rows):
+    """C4 against the books path with the sphere UV's acos / atan2 from the host's libm (the
+    reference's f64::acos / atan2; oracle diagnostic bit 0x800), not the fdlibm restatement the
+    kernel shares with the default BOOKS mode: the channel and PPM-byte mismatches are reported and
+    must stay inside the north star's bars (<= 1 ulp in the angle moves a texel index only at a
+    boundary; tests/test_oracle.py counts none on C4)."""
+    w, spp = size
+    scene = rrt.config_scene("C4", **({} if w is None else dict(image_width=w, samples_per_pixel=spp)))
+    gpu, _, gpu_rays = _gpu_f64(scene)
+    books, books_rays, _ = oracle.render(scene, oracle.BOOKS | 0x800, rows=rows, threads=16)
+    if rows is None:
+        assert gpu_rays == books_rays
+    else:
+        gpu = gpu[rows[0]:rows[1]]
+    diff = np.abs(gpu[..., :3] - books[..., :3]) / scene.spp
+    print(f"C4 vs libm-trig BOOKS: {int((diff > 1e-12).sum())} of {diff.size} channels differ beyond 1e-12")
+    _check(scene, gpu, books, "C4 vs BOOKS (libm acos / atan2)")

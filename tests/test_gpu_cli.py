@@ -36,7 +36,8 @@ def _python_ppm(scene_id, textures=None):
     return rrt.format_ppm_from_accum(sc.width, sc.height, acc, sc.spp)
 
 
-@pytest.mark.parametrize("args,scene_id", [(["3"], 3), (["9"], 9), ([], 10), (["0"], 10), (["17"], 10)])
+@pytest.mark.parametrize("args,scene_id", [(["3"], 3), (["9"], 9), ([], 10), (["0"], 10), (["17"], 10),
+                                           (["+3"], 3), ([" 3"], 10), (["4294967297"], 10)])
 def test_cli_earth_scenes_match_python(tmp_path, args, scene_id):
     path = tmp_path / "nw.ppm"
     r = _cli(args, path, cwd=str(tmp_path))

@@ -113,20 +113,28 @@ def test_c2_counting_kernel_rays_equal_fast_kernel():
     ds.close()
 
 
-def test_c3_tiles_match_oracle_rows():
-    # C3 = 3840x2160x2048 split over 8 ranks; render rank 0's and rank 7's bands on this GPU.
+@pytest.mark.parametrize("rank", [0, 3, 7])
+def test_c3_tiles_match_oracle_rows(rank):
+    # C3 = 3840x2160x2048 split over 8 ranks exactly as bench.py --gpus 8 times it: 10-row
+    # serpentine bands (balanced_band(2160, 8)); render ranks 0, 3 and 7's bands on this GPU and
+    # check the first and last rows of each tile against the oracle at the full 2048 spp.
+    from rustraytrace_amd.distributed import balanced_band, band_rows
+
+    band = balanced_band(2160, 8)
+    assert band == 10
     scene = rrt.config_scene("C3")
-    for rank in (0, 7):
-        ds, tile, a, b, ctr = _render_full(scene, dict(band_rows=16, rank=rank, n_ranks=8, sample_begin=0,
-                                                       sample_end=scene.spp))
-        idx = ds.tile_row_indices(tile)
-        assert np.all(a[..., 3] == 2048) and np.isfinite(a).all()
-        assert np.array_equal(a, b)
-        y = int(idx[0])
-        nodes, order, info = build_bvh(scene)
+    ds, tile, a, b, ctr = _render_full(scene, dict(band_rows=band, rank=rank, n_ranks=8, sample_begin=0,
+                                                   sample_end=scene.spp))
+    idx = ds.tile_row_indices(tile)
+    assert np.array_equal(idx, band_rows(2160, band, rank, 8)) and len(idx) == 270
+    assert np.all(a[..., 3] == 2048) and np.isfinite(a).all()
+    assert np.array_equal(a, b)
+    nodes, order, info = build_bvh(scene)
+    for k in (0, len(idx) - 1):
+        y = int(idx[k])
         ref, _, _ = oracle.render_kbvh(scene, nodes, order, info, rows=(y, y + 1), threads=THREADS)
-        assert np.array_equal(a[0:1].astype(np.float64), ref)
-        ds.close()
+        assert np.array_equal(a[k:k + 1].astype(np.float64), ref), f"rank {rank} tile row {k} (image row {y})"
+    ds.close()
 
 
 GOLDENS = sorted(glob.glob(os.path.join(GOLDEN, "*.npz")))

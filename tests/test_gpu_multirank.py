@@ -78,3 +78,25 @@ def test_bench_band_split_line(ranks):
         assert line["rows_per_rank"] == [144 // ranks] * ranks  # balanced_band: 12-row bands at 2 ranks
     else:
         assert "no gather" in line["config"]["parallelism"]
+
+
+def test_bench_spawns_its_own_ranks():
+    # `python bench.py --gpus 2` with no external launcher: bench.py starts torch.distributed.run as
+    # a child (2 ranks sharing this GPU over gloo), forwards rank 0's line, and the N > 1 line
+    # carries the per-rank kernel times, the gather time and the same frame on one GPU.
+    args = ["bench.py", "--gpus", "2", "--config", "C3", "--width", "256", "--spp", "8", "--steps", "2",
+            "--warmup", "1", "--no-cpu-baseline", "--no-breakdown"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(RRT_BENCH_BACKEND="gloo", OMP_NUM_THREADS="1")
+    r = subprocess.run([sys.executable] + args, capture_output=True, text=True, cwd=ROOT, env=env, timeout=110)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1  # stdout holds exactly rank 0's line
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["scaling"] == "strong"
+    assert line["rows_per_rank"] == [72, 72] and "gather_ms" in line
+    assert len(line["kernel_ms_per_rank"]) == 2 and line["kernel_ms_max_over_ranks"] == max(line["kernel_ms_per_rank"])
+    base = line["c3_one_gpu"]
+    assert base["workload"].startswith("C3 256x144x8spp")
+    assert base["rays"] == line["rays_per_step"]  # the same frame, whole, on one GPU
+    assert line["scaling_efficiency"] > 0

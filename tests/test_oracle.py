@@ -489,3 +489,20 @@ def test_fdlibm_acos_atan2_within_one_ulp_of_libm():
     # exact special values of fdlibm
     sa, sb = oracle.acos_atan2_f64(np.array([1.0, -1.0, 0.0]), np.array([0.0, 0.0, 1.0]))
     assert sa[0] == 0.0 and sa[1] == np.pi and sb[0] == 0.0 and sb[1] == np.pi and sb[2] == np.pi / 2
+
+
+def test_books_libm_trig_changes_no_c4_pixel():
+    """BOOKS computes the sphere UV's acos / atan2 with fdlibm's algorithms (shared op for op with
+    the f64 kernel); the reference calls the platform libm. Diagnostic bit 0x800 switches BOOKS to
+    this host's libm: on C4 (the textured BASELINE config) no channel, ray count or PPM byte
+    changes, at a reduced frame and on full-size rows at the full 1024 spp (a <= 1-ulp angle moves
+    the texel index only when u * width sits on an integer)."""
+    for kw, rows in [(dict(image_width=320, samples_per_pixel=64), None), ({}, (536, 544))]:
+        scene = rrt.config_scene("C4", **kw)
+        a, ra, _ = oracle.render(scene, oracle.BOOKS, rows=rows, threads=8)
+        b, rb, _ = oracle.render(scene, oracle.BOOKS | 0x800, rows=rows, threads=8)
+        assert ra == rb
+        assert np.array_equal(a, b)
+        h = a.shape[0]
+        assert np.array_equal(rrt.quantize_accum_books_f64(scene.width, h, a, scene.spp),
+                              rrt.quantize_accum_books_f64(scene.width, h, b, scene.spp))
