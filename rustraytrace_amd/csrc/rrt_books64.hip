@@ -38,6 +38,7 @@ namespace rrt {
 namespace {
 
 #include "rrt_device.h"
+#include "rrt_box32.h"
 
 // issue priority by loop phase (as rrt_kernel.hip: refill 2, node steps 1, leaf batches 2, shading 0)
 constexpr int kPrioRefill = 2, kPrioNode = 1, kPrioLeaf = 2, kPrioShade = 0;
@@ -249,10 +250,10 @@ __device__ __forceinline__ D3 texel64(const KParams &P, int tex, D3 outward) {
     return d3(cs * (double)px[0], cs * (double)px[1], cs * (double)px[2]);
 }
 
-// Per-ray constants of the f64 box test: 1/d clamped to +-2^500 (a zero component gives a huge
-// finite slope, so fma(P, inv, -o*inv) keeps the sign of P - o), and o * inv.
+// Per-ray constants of the box test (rrt_box32.h: f32 arithmetic on the f32 / f16 planes, widened
+// so that it never rejects a box the f64 ray meets).
 struct RayK64 {
-    D3 inv, oi;
+    RayBox32 b;
     // byte offsets of the ray's (entry, exit) plane pair of each axis in a GNode child box (the
     // f32 kernel's RayK): 12a + 4 when 1/d_a < 0 (hi, lo), else 12a (lo, hi)
     uint32_t ox, oy, oz;
@@ -260,54 +261,25 @@ struct RayK64 {
     // 16 bits when 1/d_a < 0 puts the (entry, exit) pair in (lo, hi) order
     uint32_t rx, ry, rz;
 };
-__device__ __forceinline__ double clamp_inv64(double v) { return __builtin_fmax(__builtin_fmin(v, 0x1.0p500), -0x1.0p500); }
 __device__ __forceinline__ RayK64 ray_consts64(D3 o, D3 d) {
     RayK64 r;
-    r.inv = d3(clamp_inv64(1.0 / d.x), clamp_inv64(1.0 / d.y), clamp_inv64(1.0 / d.z));
-    r.oi = d3(o.x * r.inv.x, o.y * r.inv.y, o.z * r.inv.z);
-    r.ox = r.inv.x < 0.0 ? 4u : 0u;
-    r.oy = r.inv.y < 0.0 ? 16u : 12u;
-    r.oz = r.inv.z < 0.0 ? 28u : 24u;
-    r.rx = r.inv.x < 0.0 ? 16u : 0u;
-    r.ry = r.inv.y < 0.0 ? 16u : 0u;
-    r.rz = r.inv.z < 0.0 ? 16u : 0u;
+    r.b = box32_ray(o.x, o.y, o.z, d.x, d.y, d.z);
+    r.ox = r.b.ix < 0.0f ? 4u : 0u;
+    r.oy = r.b.iy < 0.0f ? 16u : 12u;
+    r.oz = r.b.iz < 0.0f ? 28u : 24u;
+    r.rx = r.b.ix < 0.0f ? 16u : 0u;
+    r.ry = r.b.iy < 0.0f ? 16u : 0u;
+    r.rz = r.b.iz < 0.0f ? 16u : 0u;
     return r;
-}
-// Slab test of a stored f32 box in f64 (role of Aabb::hit, aabb.rs:52-85: a box test only prunes).
-// The stored planes lie outside the f64 sphere box by the f32 slab bound (~2^-22 |P|, rrt_host.cpp
-// BoxSlack), far above this test's f64 rounding, so it never rejects a box whose sphere a ray hits.
-// The planes come in (entry, exit) order per axis (GNode's lo, hi, lo layout read at the ray's sign
-// offsets, or GNodeH's halves rotated by the sign): fma(P, inv, -oi) is monotone in P for a fixed
-// inv, so the entry plane's distance is exactly min(t_lo, t_hi) and the exit plane's the max — the
-// min/max slab's values and decisions without its twelve f64 min/max (rrt_kernel.hip
-// box_hit_ordered).
-__device__ __forceinline__ bool box64_ordered(double nx, double fx, double ny, double fy, double nz, double fz,
-                                              const RayK64 &rk, double tmax, double &tnear) {
-    const double x0 = __builtin_fma(nx, rk.inv.x, -rk.oi.x), x1 = __builtin_fma(fx, rk.inv.x, -rk.oi.x);
-    const double y0 = __builtin_fma(ny, rk.inv.y, -rk.oi.y), y1 = __builtin_fma(fy, rk.inv.y, -rk.oi.y);
-    const double z0 = __builtin_fma(nz, rk.inv.z, -rk.oi.z), z1 = __builtin_fma(fz, rk.inv.z, -rk.oi.z);
-    const double nr = __builtin_fmax(__builtin_fmax(x0, y0), __builtin_fmax(z0, 0.001));
-    const double fr = __builtin_fmin(__builtin_fmin(x1, y1), __builtin_fmin(z1, tmax));
-    tnear = nr;
-    return nr < fr;
 }
 
 struct Trav64 {
     double closest;
+    float closest32;  // fl32(closest): the box test's exit bound (rrt_box32.h)
     int hit_prim;
     int node;
     int sp;
 };
-
-// A GNode with its planes widened to f64 (exact) while the block stages the tree in LDS: the node
-// step then reads the (entry, exit) pairs as doubles instead of converting twelve f32 planes per
-// visit. 160 B (box[c][3a .. 3a+2] = lo, hi, lo as in GNode).
-struct alignas(16) GNode64 {
-    double box[2][9];
-    uint32_t link[2];
-    uint32_t pad[2];
-};
-static_assert(sizeof(GNode64) == 160, "GNode64 must be 160 B");
 
 // One BVH2 node visit (rrt_kernel.hip trav_node's schedule): both child boxes against the closest
 // hit so far, hit leaf children postponed as one primitive range, the nearer internal child next
@@ -319,25 +291,15 @@ __device__ __forceinline__ bool trav_node64(const Node *__restrict__ nodes, Stac
     if (kCount) { cnt.nodes++; cnt.boxes += 2; }
     bool h0, h1;
     uint32_t l0, l1;
-    double tn0 = 0.0, tn1 = 0.0;
-    if constexpr (std::is_same<Node, GNode64>::value) {
-        const GNode64 &n = nodes[t.node];  // LDS, f64 planes: the f32 byte offsets doubled
-        const char *bx = reinterpret_cast<const char *>(&n.box[0][0]);
-        auto plane = [&](uint32_t byte_off) { return *reinterpret_cast<const double *>(bx + 2u * byte_off); };
-        h0 = box64_ordered(plane(rk.ox), plane(rk.ox + 4), plane(rk.oy), plane(rk.oy + 4), plane(rk.oz),
-                           plane(rk.oz + 4), rk, t.closest, tn0);
-        h1 = box64_ordered(plane(rk.ox + 36), plane(rk.ox + 40), plane(rk.oy + 36), plane(rk.oy + 40),
-                           plane(rk.oz + 36), plane(rk.oz + 40), rk, t.closest, tn1);
-        l0 = n.link[0];
-        l1 = n.link[1];
-    } else if constexpr (std::is_same<Node, GNode>::value) {
+    float tn0 = 0.0f, tn1 = 0.0f;
+    if constexpr (std::is_same<Node, GNode>::value) {
         const GNode &n = nodes[t.node];  // LDS: lo, hi, lo per axis, each pair read at the ray's sign offset
         const char *bx = reinterpret_cast<const char *>(&n.box[0][0]);
-        auto plane = [&](uint32_t byte_off) { return (double)*reinterpret_cast<const float *>(bx + byte_off); };
-        h0 = box64_ordered(plane(rk.ox), plane(rk.ox + 4), plane(rk.oy), plane(rk.oy + 4), plane(rk.oz),
-                           plane(rk.oz + 4), rk, t.closest, tn0);
-        h1 = box64_ordered(plane(rk.ox + 36), plane(rk.ox + 40), plane(rk.oy + 36), plane(rk.oy + 40),
-                           plane(rk.oz + 36), plane(rk.oz + 40), rk, t.closest, tn1);
+        auto plane = [&](uint32_t byte_off) { return *reinterpret_cast<const float *>(bx + byte_off); };
+        h0 = box32_hit(plane(rk.ox), plane(rk.ox + 4), plane(rk.oy), plane(rk.oy + 4), plane(rk.oz), plane(rk.oz + 4),
+                       rk.b, t.closest32, tn0);
+        h1 = box32_hit(plane(rk.ox + 36), plane(rk.ox + 40), plane(rk.oy + 36), plane(rk.oy + 40), plane(rk.oz + 36),
+                       plane(rk.oz + 40), rk.b, t.closest32, tn1);
         l0 = n.link[0];
         l1 = n.link[1];
     } else {  // global memory: the 32-B f16 node (GNodeH), each axis's halves in (entry, exit) order
@@ -346,8 +308,8 @@ __device__ __forceinline__ bool trav_node64(const Node *__restrict__ nodes, Stac
         auto ord = [](uint32_t w, uint32_t r) { return __builtin_amdgcn_alignbit(w, w, r); };
         const uint32_t x0 = ord(a.x, rk.rx), y0 = ord(a.y, rk.ry), z0 = ord(a.z, rk.rz);
         const uint32_t x1 = ord(a.w, rk.rx), y1 = ord(b.x, rk.ry), z1 = ord(b.y, rk.rz);
-        h0 = box64_ordered(lo16(x0), hi16(x0), lo16(y0), hi16(y0), lo16(z0), hi16(z0), rk, t.closest, tn0);
-        h1 = box64_ordered(lo16(x1), hi16(x1), lo16(y1), hi16(y1), lo16(z1), hi16(z1), rk, t.closest, tn1);
+        h0 = box32_hit(lo16(x0), hi16(x0), lo16(y0), hi16(y0), lo16(z0), hi16(z0), rk.b, t.closest32, tn0);
+        h1 = box32_hit(lo16(x1), hi16(x1), lo16(y1), hi16(y1), lo16(z1), hi16(z1), rk.b, t.closest32, tn1);
         l0 = b.z;
         l1 = b.w;
     }
@@ -419,6 +381,7 @@ __device__ __forceinline__ void leaves64(const float4 *__restrict__ prims, Leave
         if (!(0.001 < root)) root = div_a64(h + sq, a, ra);
         if (0.001 < root && root < t.closest) {
             t.closest = root;
+            t.closest32 = (float)root;
             t.hit_prim = i;
         }
     }
@@ -532,16 +495,14 @@ __device__ __forceinline__ bool shade64(const KParams &P, const float4 *prims, c
 // The persistent work loop of rrt_kernel.hip's render_body (same queue, units, chunk order,
 // postponed leaves and wave-uniform exits) over Path64 state.
 // kMode: kF64Global (f16 nodes and records read from global memory), kF64Lds (the f32 nodes,
-// spheres and materials staged in LDS), kF64LdsWide (nodes widened to f64 and spheres in LDS,
-// materials from global memory — one read per hit — to stay within the block's 64 KB).
-constexpr int kF64Global = 0, kF64Lds = 1, kF64LdsWide = 2;
+// spheres and materials staged in LDS).
+constexpr int kF64Global = 0, kF64Lds = 1;
 template <int kMode, bool kCount, int kBlk, int kClass>
 __device__ __forceinline__ void render64_body(const KParams &P) {
     constexpr bool kLds = kMode != kF64Global;
     extern __shared__ uint4 lds_dyn[];
     uint16_t *lds_stack = reinterpret_cast<uint16_t *>(lds_dyn);
-    using Node = typename std::conditional<kMode == kF64LdsWide, GNode64,
-                                           typename std::conditional<kLds, GNode, GNodeH>::type>::type;
+    using Node = typename std::conditional<kLds, GNode, GNodeH>::type;
     const Node *nodes = reinterpret_cast<const Node *>(P.nodes);
     const float4 *prims = P.prim_cr;
     const GMaterial *mtl = P.prim_mtl;
@@ -559,26 +520,6 @@ __device__ __forceinline__ void render64_body(const KParams &P) {
         nodes = reinterpret_cast<const Node *>(dst);
         prims = reinterpret_cast<const float4 *>(dst + nn);
         mtl = reinterpret_cast<const GMaterial *>(dst + nn + P.n_prims);
-    } else if constexpr (kMode == kF64LdsWide) {  // nodes widened to f64 (exact) + spheres
-        uint4 *dst = lds_dyn + (P.stack_depth * kBlk * sizeof(uint16_t) + 15u) / 16u;
-        GNode64 *dn = reinterpret_cast<GNode64 *>(dst);
-        const GNode *sn = reinterpret_cast<const GNode *>(P.nodes);
-        for (uint32_t i = threadIdx.x; i < P.n_nodes; i += kBlk) {
-            const GNode g = sn[i];
-            GNode64 w;
-            for (int c = 0; c < 2; ++c)
-                for (int k = 0; k < 9; ++k) w.box[c][k] = (double)g.box[c][k];
-            w.link[0] = g.link[0];
-            w.link[1] = g.link[1];
-            w.pad[0] = w.pad[1] = 0u;
-            dn[i] = w;
-        }
-        const uint32_t nn = P.n_nodes * (uint32_t)(sizeof(GNode64) / 16);
-        const uint4 *src_p = reinterpret_cast<const uint4 *>(P.prim_cr);
-        for (uint32_t i = threadIdx.x; i < P.n_prims; i += kBlk) dst[nn + i] = src_p[i];
-        __syncthreads();
-        nodes = reinterpret_cast<const Node *>(dst);
-        prims = reinterpret_cast<const float4 *>(dst + nn);
     }
     LdsStack<uint16_t, kBlk> stack;
     stack.init(lds_stack, threadIdx.x);
@@ -655,6 +596,7 @@ __device__ __forceinline__ void render64_body(const KParams &P) {
                 seg_done = 1;
             } else {
                 tr.closest = __builtin_inf();  // Interval(0.001, INFINITY)
+                tr.closest32 = __builtin_inff();
                 tr.hit_prim = -1;
                 tr.node = 0;
                 tr.sp = 0;
@@ -781,7 +723,6 @@ __global__ __launch_bounds__(256) void rrt_accum64_to_f32(const D4 *__restrict__
 size_t lds64_bytes(const KParams &p, int mode) {
     size_t lds = ((size_t)p.stack_depth * kBlock64 * sizeof(uint16_t) + 15u) / 16u * 16u;
     if (mode == kF64Lds) lds += (size_t)p.n_nodes * sizeof(GNode) + (size_t)p.n_prims * kPrimBytes;
-    if (mode == kF64LdsWide) lds += (size_t)p.n_nodes * sizeof(GNode64) + (size_t)p.n_prims * 16u;
     return lds;
 }
 
@@ -801,19 +742,11 @@ hipError_t launch64(const KParams &p, bool count, hipStream_t stream) {
     return hipGetLastError();
 }
 
-#ifndef RRT_F64_WIDE
-#define RRT_F64_WIDE 1
-#endif
-// The scene placement: global memory for f16-node scenes; for LDS scenes the f64-widened nodes
-// when they fit the 64 KB a block may declare, else the f32 nodes.
-// RRT_F64_LDS_F32 (environment, test mode): keep the f32 LDS layout, so the fallback runs on
-// scenes whose widened tree would fit.
+// The scene placement: the f32 nodes, spheres and materials in LDS when they fit (C1, C2, C4), else
+// the f16 nodes and records from global memory (C5).
 template <int kClass>
 hipError_t launch64_placed(const KParams &p, bool count, hipStream_t stream) {
     if (!p.scene_in_lds) return launch64<kF64Global, kClass>(p, count, stream);
-    const char *f32_layout = std::getenv("RRT_F64_LDS_F32");
-    const bool wide_ok = !(f32_layout && std::atoi(f32_layout) != 0) && lds64_bytes(p, kF64LdsWide) <= 64u * 1024u;
-    if (RRT_F64_WIDE && wide_ok) return launch64<kF64LdsWide, kClass>(p, count, stream);
     return launch64<kF64Lds, kClass>(p, count, stream);
 }
 

@@ -1671,10 +1671,11 @@ hipError_t launch_render_pass(const KParams &p, bool count, hipStream_t stream) 
         return p.n_quads ? launch_width<false, 2>(p, count, stream) : launch_width<false, 1>(p, count, stream);
     }
     if (p.bvh_width == 4) return launch_width<true, 0>(p, count, stream);
-    // Scenes staged in LDS without image textures run the kernel with the texture path compiled
-    // out (C2 +1.0 %); for scenes read from L2 it measured −0.4 % on C5, so they keep class 0.
+    // Scenes without image textures run the kernel with the texture path compiled out: C2 +1.0 %;
+    // for scenes read from L2 (C5) it removes the 7-wave kernel's 4 spilled VGPRs (20 B of scratch
+    // per lane, written and read back through memory) at equal time.
     if (!p.specular && p.scene_in_lds) return launch_width<false, kBook1Diffuse>(p, count, stream);
-    if (!p.image_tex && p.scene_in_lds) return launch_width<false, kBook1Untextured>(p, count, stream);
+    if (!p.image_tex) return launch_width<false, kBook1Untextured>(p, count, stream);
     return launch_width<false, 0>(p, count, stream);
 }
 

@@ -137,18 +137,6 @@ def test_f64_full_class_matches_books_path():
     assert np.array_equal(gpu32, gpu.astype(np.float32))
 
 
-@pytest.mark.parametrize("cfg", ["C1", "C2"])
-def test_f64_f32_lds_layout_fallback_matches_books_path(cfg, monkeypatch):
-    """Scenes whose f64-widened tree exceeds a block's 64 KB keep the f32 LDS layout (planes
-    converted per visit, materials in LDS); RRT_F64_LDS_F32 forces that layout on a small scene."""
-    monkeypatch.setenv("RRT_F64_LDS_F32", "1")
-    scene = rrt.config_scene(cfg, image_width=64, samples_per_pixel=128)
-    gpu, _, gpu_rays = _gpu_f64(scene)
-    books, books_rays, _ = oracle.render(scene, oracle.BOOKS, threads=16)
-    assert gpu_rays == books_rays
-    _check(scene, gpu, books, f"{cfg} f32 LDS layout")
-
-
 @pytest.mark.parametrize("size,rows", [((64, 256), None), ((None, None), (536, 544))])
 def test_f64_textured_matches_books_with_libm_trig(size, rows):
     """C4 against the books path with the sphere UV's acos / atan2 from the host's libm (the

@@ -8,7 +8,7 @@ for spec in "$@"; do
   name=${spec%%:*}; rest=${spec#*:}; v=${rest%%:*}; envs=${rest#*:}
   [ "$envs" = "$rest" ] && envs=""
   ( export RRT_LIB_PATH=variants/$v/librrt_hip.so; for kv in ${envs//,/ }; do export "$kv"; done
-    timeout -k 10 300 python bench.py --steps ${STEPS:-3} --warmup 1 --no-cpu-baseline --no-breakdown --no-f64 --no-ref-slot --no-extra ${BENCH_ARGS:-} > gpurun_out/ab_$name.log 2>&1 )
+    timeout -k 10 300 python bench.py --steps ${STEPS:-3} --warmup 1 --no-cpu-baseline --no-breakdown --no-f64 --no-extra ${BENCH_ARGS:-} > gpurun_out/ab_$name.log 2>&1 )
   rc=$?
   echo "r$r $name rc=$rc $(python -c "
 import json;d=json.loads(open('gpurun_out/ab_$name.log').read().splitlines()[-1]);r=d['rank0_rays_per_launch']

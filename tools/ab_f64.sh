@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 for r in $(seq 1 ${ROUNDS:-2}); do
 for n in ${VARIANTS:-$(ls variants)}; do
   d=variants/$n
-  RRT_LIB_PATH=$d/librrt_hip.so timeout -k 10 300 python bench.py --config ${CONFIG:-C2} --steps 1 --warmup 1 --no-cpu-baseline --no-breakdown --no-extra --no-ref-slot > gpurun_out/abf_$n.log 2>&1
+  RRT_LIB_PATH=$d/librrt_hip.so timeout -k 10 300 python bench.py --config ${CONFIG:-C2} --steps 1 --warmup 1 --no-cpu-baseline --no-breakdown --no-extra > gpurun_out/abf_$n.log 2>&1
   rc=$?
   echo "r$r $n rc=$rc $(python -c "import json;d=json.loads(open('gpurun_out/abf_$n.log').read().splitlines()[-1]);f=d['f64_books'];print(d['value'],'f32 Mrays/s |',f['value'],'f64 Mrays/s',f['ms_per_frame'],'ms')" 2>/dev/null)"
   if [ $rc -ne 0 ]; then tail -5 gpurun_out/abf_$n.log; exit $rc; fi

@@ -29,7 +29,7 @@ for spec in ${CONFIGS:-C2:512}; do
   fi
 done
 if [[ $STEPS == *stats* ]]; then
-  run kstats 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-breakdown --no-extra --no-f64 --no-ref-slot
+  run kstats 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-breakdown --no-extra --no-f64
   cp gpurun_out/prof_$TAG/run_kernel_stats.csv gpurun_out/profiles/${TAG}_kernel_stats.csv
 fi
 if [[ $STEPS == *bench* ]]; then

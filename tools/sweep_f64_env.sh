@@ -7,7 +7,7 @@ for r in $(seq 1 ${ROUNDS:-2}); do
 for spec in "$@"; do
   name=${spec%%:*}; tl=${spec#*:}
   ( if [ "$tl" != "default" ]; then export RRT_TRAV_FRAC=${tl%/*} RRT_LEAF_FRAC=${tl#*/}; fi
-    timeout -k 10 300 python bench.py --config ${CONFIG:-C2} --steps 1 --warmup 1 --no-cpu-baseline --no-breakdown --no-extra --no-ref-slot > gpurun_out/sf_$name.log 2>&1 )
+    timeout -k 10 300 python bench.py --config ${CONFIG:-C2} --steps 1 --warmup 1 --no-cpu-baseline --no-breakdown --no-extra > gpurun_out/sf_$name.log 2>&1 )
   rc=$?
   echo "r$r ${CONFIG:-C2} $name ($tl) rc=$rc $(python -c "import json;d=json.loads(open('gpurun_out/sf_$name.log').read().splitlines()[-1]);f=d['f64_books'];print(f['value'],'f64 Mrays/s',f['ms_per_frame'],'ms')" 2>/dev/null)"
   if [ $rc -ne 0 ]; then tail -5 gpurun_out/sf_$name.log; exit $rc; fi
