@@ -60,20 +60,34 @@ __device__ __forceinline__ D3 f2d(float x, float y, float z) { return d3((double
 // f64::min: a NaN operand yields the other
 __device__ __forceinline__ double rmin(double a, double b) { return a < b ? a : b; }
 
-// random_double(): the 24-bit draw, exact in f64; random_double_range(-1, 1) = u * 2 + -1 (exact)
+// random_double(): the 24-bit draw, exact in f64; random_double_range(-1, 1) = u * 2 + -1 (exact;
+// the rejection loops below draw it as draw_centred)
 __device__ __forceinline__ double rnd64(RngState &s) { return (double)(rng_next(s) >> 8) * 0x1.0p-24; }
-__device__ __forceinline__ double rnd64_pm1(RngState &s) { return rnd64(s) * 2.0 + -1.0; }
+
+// The rejection loops decide on integers. A coordinate drawn by random_double_range(-1, 1) is
+// x = a 2^-23 - 1 = (a - 2^23) 2^-23 for the draw's 24-bit a, exactly, in f64, so |p|^2 = S 2^-46
+// with the integer S = sum (a_i - 2^23)^2 <= 3 2^46. The reference's f64 sum of the (exact)
+// squares rounds by less than 2^-51 while S 2^-46 moves in steps of 2^-46, so its comparison with 1
+// decides exactly as S against 2^46, and |p|^2 > 1e-160 exactly when S > 0
+// (tests/test_rejection_exact.py). The loops compute S in 64-bit integers from 24-bit signed
+// multiplies (full-rate VALU) instead of the reference's f64 conversions, products and sums
+// (half-rate): same draws, same decisions, same accepted point, which is converted once.
+__device__ __forceinline__ int32_t draw_centred(RngState &s) { return (int32_t)(rng_next(s) >> 8) - 8388608; }
+__device__ __forceinline__ uint64_t sq_i24(int32_t a) { return (uint64_t)((int64_t)a * (int64_t)a); }
+__device__ __forceinline__ double centred_to_pm1(int32_t a) { return (double)a * 0x1.0p-23; }  // exact
 
 // vec3.rs:181-189 random_unit_vector (Vec3::random_range(-1, 1): x, y, z drawn in order)
 __device__ __forceinline__ D3 random_unit_vector(RngState &s) {
-    double x, y, z, lensq;
+    int32_t a, b, c;
     for (;;) {
-        x = rnd64_pm1(s);
-        y = rnd64_pm1(s);
-        z = rnd64_pm1(s);
-        lensq = x * x + y * y + z * z;
-        if (1e-160 < lensq && lensq <= 1.0) break;
+        a = draw_centred(s);
+        b = draw_centred(s);
+        c = draw_centred(s);
+        const uint64_t S = sq_i24(a) + sq_i24(b) + sq_i24(c);
+        if (S - 1u < (1ull << 46)) break;  // 0 < S <= 2^46
     }
+    const double x = centred_to_pm1(a), y = centred_to_pm1(b), z = centred_to_pm1(c);
+    const double lensq = x * x + y * y + z * z;
     return muls(d3(x, y, z), 1.0 / __builtin_sqrt(lensq));
 }
 
@@ -404,11 +418,14 @@ __device__ __forceinline__ void camera_ray64(uint32_t x, uint32_t y, Path64 &ps)
     D3 origin = f2d(C.center[0], C.center[1], C.center[2]);
     if (C.defocus_radius > 0.0f) {
         double px, py;
-        for (;;) {  // vec3.rs:172-179 random_in_unit_disk
-            px = rnd64_pm1(ps.rng);
-            py = rnd64_pm1(ps.rng);
-            if (px * px + py * py < 1.0) break;
+        int32_t a, b;
+        for (;;) {  // vec3.rs:172-179 random_in_unit_disk, decided on integers (random_unit_vector)
+            a = draw_centred(ps.rng);
+            b = draw_centred(ps.rng);
+            if (sq_i24(a) + sq_i24(b) < (1ull << 46)) break;
         }
+        px = centred_to_pm1(a);
+        py = centred_to_pm1(b);
         const double rad = (double)C.defocus_radius;  // defocus_disk_u = u * radius (camera.rs:136-138)
         const D3 du = muls(f2d(C.cam_u[0], C.cam_u[1], C.cam_u[2]), rad);
         const D3 dv = muls(f2d(C.cam_v[0], C.cam_v[1], C.cam_v[2]), rad);

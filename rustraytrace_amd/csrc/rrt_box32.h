@@ -2,17 +2,18 @@
 // reject a box the f64 ray meets (role of Aabb::hit, books/in_one_weekend/aabb.rs:52-85: a box test
 // only prunes; which sphere is hit is decided by the f64 sphere test alone).
 //
-// Compiled for the device by rrt_books64.hip and for the host by tests/box32_harness.cpp, which
-// checks the bound below against exact rational arithmetic on adversarial rays
-// (tests/test_box32_conservative.py). Plain IEEE f32: + - * /, fma, min, max, fabs.
+// Compiled for the device by rrt_books64.hip and for the host by tests/box32/box32_harness.cpp, which
+// checks the bound below against exact rational arithmetic on adversarial rays, with the hardware
+// reciprocal's estimate emulated 0, 1 and 2 ulps off either side of 1/x
+// (tests/test_box32_conservative.py). IEEE f32 fma, mul, min, max, fabs, and v_rcp_f32.
 //
-// The f64 ray (o, d) is rounded once per ray: d32 = fl(d), o32 = fl(o), q = fl(1 / d32) (correctly
-// rounded division), inv = q clamped to +-2^64, oi = fl(o32 * inv). A stored f32 plane P then gives
+// The f64 ray (o, d) is rounded once per ray: d32 = fl(d), o32 = fl(o), q = 1 / d32 to within 1.01 u
+// (box32_recip), inv = q clamped to +-2^64, oi = fl(o32 * inv). A stored f32 plane P then gives
 // t' = fl(fma(P, inv, -oi)) for the exact t = (P - o) / d. With u = 2^-24 and |q| <= 2^64:
-//   inv = (1/d)(1 + eta), |eta| <= 2u + u^2      (d rounding, division rounding)
+//   inv = (1/d)(1 + eta), |eta| <= 2.02u         (d rounding, reciprocal error)
 //   oi  = (o * inv)(1 + g), |g| <= 2u + u^2      (o rounding, product rounding)
 //   t'  = (t (1 + eta) - (o * inv) g)(1 + e), |e| <= u
-// so |t' - t| <= 3.001 u |t'| + 2.001 u |oi|. The test widens the entry distance down and the exit
+// so |t' - t| <= 3.03 u |t'| + 2.001 u |oi|. The test widens the entry distance down and the exit
 // distance up by E = 8u (|t'| + m) + 2^-100, m = max |oi_a| over the ray's unclamped axes (the
 // 2^-100 keeps E > 0): more than twice the bound, which also absorbs the rounding of E and of
 // t' -+ E. The entry is nr = max(entry planes, 0.001 rounded down), the exit fr = min(exit planes,
@@ -44,8 +45,21 @@ struct RayBox32 {
 
 RRT_HD inline float box32_clamp(float v) { return __builtin_fmaxf(__builtin_fminf(v, 0x1.0p64f), -0x1.0p64f); }
 
+// q ~ 1 / x: the hardware reciprocal (v_rcp_f32, <= 1 ulp) refined by one Newton step, which leaves
+// a relative error below 1.01 u (the error of the estimate squared, plus the step's own rounding);
+// no IEEE division is needed, only the bound. Skipped beyond 2^64 (x = +-0 or |x| < 2^-64: the
+// step would meet 0 * inf), where the clamp takes over.
+#ifndef RRT_BOX32_RCP
+#define RRT_BOX32_RCP(x) __builtin_amdgcn_rcpf(x)
+#endif
+RRT_HD inline float box32_recip(float x) {
+    const float r = RRT_BOX32_RCP(x);
+    const float e = __builtin_fmaf(-x, r, 1.0f);
+    return __builtin_fabsf(r) <= 0x1.0p64f ? __builtin_fmaf(e, r, r) : r;
+}
+
 RRT_HD inline RayBox32 box32_ray(double ox, double oy, double oz, double dx, double dy, double dz) {
-    const float qx = 1.0f / (float)dx, qy = 1.0f / (float)dy, qz = 1.0f / (float)dz;
+    const float qx = box32_recip((float)dx), qy = box32_recip((float)dy), qz = box32_recip((float)dz);
     RayBox32 r;
     r.ix = box32_clamp(qx);
     r.iy = box32_clamp(qy);

@@ -872,6 +872,7 @@ int fill_params(RrtScene *s, const RrtTile *t, float *d_accum, rrt::KParams &p) 
     // the frame's chunk (rrt_accum_chunk): K when S > 2K, else K/2 — big chunks pay at high spp
     // (per-unit cost), small ones at low spp (drain granularity)
     p.chunk = S > 2u * p.chunk ? p.chunk : std::max(1u, p.chunk / 2u);
+    if (const char *e = std::getenv("RRT_CHUNK_FORCE")) p.chunk = (uint32_t)std::max(1, std::atoi(e));  // A/B only
     p.chunk_small = std::max(1u, p.chunk / 8u);
     p.n_big = S > p.chunk ? (S - 1u) / p.chunk : 0u;
     const uint32_t tail = S - p.n_big * p.chunk;

@@ -25,6 +25,7 @@
 #include "rrt_internal.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 namespace rrt {
@@ -1656,10 +1657,17 @@ hipError_t launch_width(const KParams &p, bool count, hipStream_t stream) {
     }
 }
 
+#if RRT_WAVEFRONT
+#include "rrt_wavefront.inc"
+#endif
+
 }  // namespace
 
 hipError_t launch_render_pass(const KParams &p, bool count, hipStream_t stream) {
     if (p.flags & kFlagF64) return launch_render_pass_f64(p, count, stream);  // the f64 books path
+#if RRT_WAVEFRONT  // measurement variant: book-1 BVH2 scenes through the wavefront prototype
+    if (!count && !p.prim_motion && p.bvh_width == 2 && p.n_nodes <= 65535u) return launch_wavefront(p, stream);
+#endif
     // Variant choice: BVH width, smallest LDS stack that holds the traversal, and the scene
     // staged in LDS when the BVH + spheres fit the per-block budget (RTOW: ~20-26 KB).
     // Book-2 scenes (moving spheres, checker / noise textures): BVH2 only (the host builds a

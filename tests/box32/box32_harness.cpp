@@ -1,12 +1,22 @@
 // Host build of the f64 books kernel's box test (rustraytrace_amd/csrc/rrt_box32.h, the same source
 // the device compiles) for tests/test_box32_conservative.py. Test infrastructure only.
 // g++ -O2 -std=c++17 -ffp-contract=off -fno-fast-math -shared -fPIC box32_harness.cpp
-#define RRT_HD
-#include "../../rustraytrace_amd/csrc/rrt_box32.h"
-
 #include <cmath>
 #include <cstdint>
 #include <random>
+
+// v_rcp_f32 on the host: the correctly rounded 1/x moved g_rcp_ulps ulps (the device estimate is
+// within 1 ulp; the test runs -2 .. 2)
+static int g_rcp_ulps = 0;
+static float host_rcp(float x) {
+    float r = 1.0f / x;
+    for (int k = 0; k < g_rcp_ulps; ++k) r = std::nextafter(r, INFINITY);
+    for (int k = 0; k > g_rcp_ulps; --k) r = std::nextafter(r, -INFINITY);
+    return r;
+}
+#define RRT_HD
+#define RRT_BOX32_RCP(x) host_rcp(x)
+#include "../../rustraytrace_amd/csrc/rrt_box32.h"
 
 namespace {
 // the kernel's plane selection: (entry, exit) = (lo, hi) when inv >= 0 (not negative), else (hi, lo)
@@ -49,6 +59,8 @@ int meets_ld(const double *o, const double *d, const float *lo, const float *hi,
 }  // namespace
 
 extern "C" {
+void box32_set_rcp_ulps(int k) { g_rcp_ulps = k; }
+
 void box32_eval(uint32_t n, const double *o, const double *d, const float *lo, const float *hi, const double *closest,
                 uint8_t *accept, float *tnear) {
     for (uint32_t i = 0; i < n; ++i) accept[i] = eval_one(o + 3 * i, d + 3 * i, lo + 3 * i, hi + 3 * i, closest[i], tnear + i);

@@ -6,7 +6,8 @@ checked against
   * exact rational arithmetic (fractions) on corner, edge and face grazes, origins on and near the
     planes, far origins (|o| up to 1e5), direction components 0, -0 and tiny, closest hits just past
     the entry, and
-  * a long-double sweep of 6e6 adversarial rays (the harness's box32_sweep).
+  * a long-double sweep of 6e6 adversarial rays (the harness's box32_sweep),
+with the hardware reciprocal's estimate emulated up to 2 ulps off 1/x either way.
 Cases on an axis the test clamps (|1/d_a| > 2^64) with the origin within 4u|o_a| of that axis's plane
 are outside the contract: the product's stored planes are grown past every primitive box by more
 than that (rrt_host.cpp BoxSlack), so such a ray misses the primitive anyway."""
@@ -30,7 +31,11 @@ def lib(tmp_path_factory):
     L.box32_sweep.argtypes = [ctypes.c_uint32, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]
     P = ctypes.c_void_p
     L.box32_eval.argtypes = [ctypes.c_uint32, P, P, P, P, P, P, P]
+    L.box32_set_rcp_ulps.argtypes = [ctypes.c_int]
     return L
+
+
+ULPS = [-2, -1, 0, 1, 2]  # the device's v_rcp_f32 estimate emulated this many ulps from 1/x
 
 
 def _eval(L, o, d, lo, hi, closest):
@@ -120,12 +125,15 @@ def _cases(n, seed):
 
 def test_widened_f32_box_test_accepts_every_exactly_met_box(lib):
     o, d, lo, hi, closest = _cases(4000, 20261017)
-    acc = _eval(lib, o, d, lo, hi, closest)
     exact = np.array([_exact(o[i], d[i], lo[i], hi[i], closest[i]) for i in range(len(o))])
     inside = exact >= 0
     assert inside.mean() > 0.9 and (exact == 1).sum() > 1000  # the cases mostly meet the box
-    missed = np.flatnonzero((exact == 1) & ~acc)
-    assert missed.size == 0, f"{missed.size} met boxes rejected, first {missed[:5]}"
+    for k in ULPS:
+        lib.box32_set_rcp_ulps(k)
+        acc = _eval(lib, o, d, lo, hi, closest)
+        missed = np.flatnonzero((exact == 1) & ~acc)
+        assert missed.size == 0, f"rcp {k:+d} ulp: {missed.size} met boxes rejected, first {missed[:5]}"
+    lib.box32_set_rcp_ulps(0)
 
 
 def test_widening_stays_tight(lib):
@@ -144,7 +152,9 @@ def test_widening_stays_tight(lib):
         up = rng.uniform() < 0.5
         p[i][a[i]] = (hi[i][a[i]] + 1e-3 * scale[i]) if up else (lo[i][a[i]] - 1e-3 * scale[i])
     d = p - o
+    lib.box32_set_rcp_ulps(2)
     acc = _eval(lib, o, d, lo, hi, np.full(n, np.inf))
+    lib.box32_set_rcp_ulps(0)
     far = 0
     for i in range(n):
         te, tx = Fraction(1, 1000), None
@@ -161,10 +171,12 @@ def test_widening_stays_tight(lib):
 
 def test_sweep_six_million_adversarial_rays(lib):
     total = np.zeros(6, np.uint64)
-    for seed in (1, 2, 3):
+    for seed, k in zip((1, 2, 3, 4, 5, 6), (0, 1, -1, 2, -2, 0)):
+        lib.box32_set_rcp_ulps(k)
         out = (ctypes.c_uint64 * 6)()
-        lib.box32_sweep(2_000_000, seed, out)
+        lib.box32_sweep(1_000_000, seed, out)
         total += np.array(list(out), np.uint64)
+    lib.box32_set_rcp_ulps(0)
     cases, meets, accepted, violations, rejected, skipped = (int(v) for v in total)
     print(f"box32 sweep: {cases} cases in the contract ({skipped} outside), {meets} meet the box, "
           f"{accepted} accepted, {violations} met-but-rejected, {rejected} correctly rejected")

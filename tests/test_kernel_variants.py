@@ -30,8 +30,9 @@ VARIANTS = {
               "-DRRT_PRIO_REFILL=0", "-DRRT_PRIO_NODE=0", "-DRRT_PRIO_LEAF=0", "-DRRT_PRIO_SHADE=0"],
     # rrt_books64.hip: the per-ray reciprocal root division, one class for every scene, f32 nodes in
     # LDS for every LDS scene, launch shape
-    "f64_knobs": ["-DRRT_F64_DIVA=0", "-DRRT_F64_CLASSES=0", "-DRRT_F64_WIDE=0", "-DRRT_F64_BLOCK=256",
-                  "-DRRT_F64_WAVES=2"],
+    "f64_knobs": ["-DRRT_F64_DIVA=0", "-DRRT_F64_CLASSES=0", "-DRRT_F64_BLOCK=256", "-DRRT_F64_WAVES=2"],
+    # the wavefront prototype (rrt_wavefront.inc): a measurement variant, DESIGN.md §5
+    "wavefront": ["-DRRT_WAVEFRONT=1"],
 }
 
 

@@ -3,7 +3,8 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 for r in $(seq 1 ${ROUNDS:-2}); do
-for d in variants/*/; do
+if [ -n "$VARIANTS" ]; then DIRS=$(printf "variants/%s/ " $VARIANTS); else DIRS=$(ls -d variants/*/); fi
+for d in $DIRS; do
   n=$(basename $d)
   RRT_LIB_PATH=$d/librrt_hip.so timeout -k 10 300 python bench.py --steps ${STEPS:-3} --warmup 1 --no-cpu-baseline --no-breakdown --no-f64 ${BENCH_ARGS:-} > gpurun_out/ab_$n.log 2>&1
   rc=$?
