@@ -34,8 +34,10 @@ extern "C" {
  * rrt_quantize_accum_books, chunk partials bounded by RRT_PARTIAL_MB (sample passes);
  * 6: RrtBvhInfo.n_unbounded (scene-enclosing media tested after the BVH walk; was _pad);
  * 7: RRT_FLAG_F64 (the books path's f64 arithmetic), rrt_hip_render_f64, rrt_render_tile_f64_async,
- * rrt_quantize_accum_books_f64; 8: RrtTile bands dealt in serpentine order (was b % n_ranks). */
-#define RRT_ABI_VERSION 8u
+ * rrt_quantize_accum_books_f64; 8: RrtTile bands dealt in serpentine order (was b % n_ranks);
+ * 9: rrt_accum_chunk() = 256 and the frame's chunk halved while S <= 2K down to a quarter (frames
+ * over 512 samples sum in chunks of 256; was 128), rrt_testing_device_wrap. */
+#define RRT_ABI_VERSION 9u
 
 /* ---- scene ABI (== src/gpu/mod.rs:13-42) ------------------------------------------ */
 
@@ -259,9 +261,9 @@ uint32_t rrt_hip_abi_version(void);
 
 /* Summation order of the accum: a pixel's RGB = sum over consecutive chunks of its S samples
  * (counted from the tile's sample_begin) of each chunk's in-order sample sum, chunks added in
- * order: ((c0 + c1) + c2) + ... With K = rrt_accum_chunk() when S > 2 * rrt_accum_chunk(), else
- * K = rrt_accum_chunk() / 2 (ABI v6: big chunks at high spp, small ones at low spp), and
- * k = max(1, K / 8): the first
+ * order: ((c0 + c1) + c2) + ... With K = rrt_accum_chunk() halved while S <= 2K, down to
+ * rrt_accum_chunk() / 4 (ABI v9: 256 for S > 512, 128 for 256 < S <= 512, 64 below; big chunks at
+ * high spp, small ones at low spp), and k = max(1, K / 8): the first
  * nb = (S - 1) / K chunks hold K samples each (nb = 0 when S <= K), the remaining S - nb*K
  * samples form chunks of k (the last one possibly shorter) — small units at the end of the
  * work queue keep the persistent grid's tail short. Needed to reproduce it bit for bit.

@@ -16,10 +16,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "build", "librrt_oracle.so")
 TWIN, BOOKS = 0, 1
 # Accum summation chunk of the HIP backend (include/rrt_hip.h rrt_accum_chunk): a frame of S
-# samples uses K = DEFAULT_CHUNK when S > 2 * DEFAULT_CHUNK, else DEFAULT_CHUNK / 2; (S-1)/K chunks
-# of K samples, then chunks of max(1, K/8) for the tail; samples summed in order within a chunk,
-# chunk sums added in order.
-DEFAULT_CHUNK = 128
+# samples uses K = DEFAULT_CHUNK halved while S <= 2K, down to DEFAULT_CHUNK / 4 (256 for S > 512,
+# 128 for 256 < S <= 512, 64 below); (S-1)/K chunks of K samples, then chunks of max(1, K/8) for the
+# tail; samples summed in order within a chunk, chunk sums added in order.
+DEFAULT_CHUNK = 256
 
 _LIB = None
 

@@ -1730,8 +1730,10 @@ int render(const RrtCamera *c, const RrtSphere *s, uint32_t n, const RrtMaterial
                 // for the rest (chunk 0 = one chunk) — chunk sums added in order
                 Vec3<T> sum = mk(T(0), T(0), T(0));
                 const uint32_t S = s1 - s0;
-                // the frame's chunk: K when S > 2K, else K/2 (rrt_accum_chunk, include/rrt_hip.h)
-                const uint32_t big = chunk ? (S > 2u * chunk ? chunk : std::max(1u, chunk / 2u)) : (S ? S : 1);
+                // the frame's chunk: K0 = chunk halved while S <= 2K, down to K0/4 (rrt_accum_chunk,
+                // include/rrt_hip.h; rrt_host.cpp)
+                uint32_t big = chunk ? chunk : (S ? S : 1);
+                while (chunk && big > std::max(1u, chunk / 4u) && S <= 2u * big) big /= 2u;
                 const uint32_t small = chunk ? std::max(1u, big / 8u) : big;
                 const uint32_t nb = (chunk && S > big) ? (S - 1u) / big : 0u;
                 for (uint32_t c0 = s0; c0 < s1;) {

@@ -407,28 +407,37 @@ struct Path64 {
     uint32_t k;  // bounce index (camera ray = 0)
 };
 
-// Camera::get_ray (camera.rs:152-180) in f64 from the f32 camera block (gpu/mod.rs:278-298 casts).
+// Camera::get_ray (camera.rs:152-180) in f64 from the camera block the host widened to f64
+// (KParams.cam64: the f32 ABI values cast as gpu/mod.rs:278-298 casts them; defocus_disk_u/v =
+// u/v * radius formed in f64, camera.rs:136-138).
 __device__ __forceinline__ void camera_ray64(uint32_t x, uint32_t y, Path64 &ps) {
     const auto &C = *kernarg_params();
     const double ox = rnd64(ps.rng) - 0.5, oy = rnd64(ps.rng) - 0.5;  // sample_square
     const double fi = (double)x + ox, fj = (double)y + oy;
+#ifndef RRT_F64_CAM64
+#define RRT_F64_CAM64 0
+#endif
+#if !RRT_F64_CAM64
     const D3 sample = d3(((double)C.p00[0] + (double)C.du[0] * fi) + (double)C.dv[0] * fj,
                          ((double)C.p00[1] + (double)C.du[1] * fi) + (double)C.dv[1] * fj,
                          ((double)C.p00[2] + (double)C.du[2] * fi) + (double)C.dv[2] * fj);
     D3 origin = f2d(C.center[0], C.center[1], C.center[2]);
+#else
+    const D3 sample = d3((C.cam64[0][0] + C.cam64[1][0] * fi) + C.cam64[2][0] * fj,
+                         (C.cam64[0][1] + C.cam64[1][1] * fi) + C.cam64[2][1] * fj,
+                         (C.cam64[0][2] + C.cam64[1][2] * fi) + C.cam64[2][2] * fj);
+    D3 origin = d3(C.cam64[3][0], C.cam64[3][1], C.cam64[3][2]);
+#endif
     if (C.defocus_radius > 0.0f) {
-        double px, py;
         int32_t a, b;
         for (;;) {  // vec3.rs:172-179 random_in_unit_disk, decided on integers (random_unit_vector)
             a = draw_centred(ps.rng);
             b = draw_centred(ps.rng);
             if (sq_i24(a) + sq_i24(b) < (1ull << 46)) break;
         }
-        px = centred_to_pm1(a);
-        py = centred_to_pm1(b);
-        const double rad = (double)C.defocus_radius;  // defocus_disk_u = u * radius (camera.rs:136-138)
-        const D3 du = muls(f2d(C.cam_u[0], C.cam_u[1], C.cam_u[2]), rad);
-        const D3 dv = muls(f2d(C.cam_v[0], C.cam_v[1], C.cam_v[2]), rad);
+        const double px = centred_to_pm1(a), py = centred_to_pm1(b);
+        const D3 du = d3(C.cam64[4][0], C.cam64[4][1], C.cam64[4][2]);
+        const D3 dv = d3(C.cam64[5][0], C.cam64[5][1], C.cam64[5][2]);
         origin = add(add(origin, muls(du, px)), muls(dv, py));
     }
     if (C.flags & 0x1u) (void)rnd64(ps.rng);  // RRT_FLAG_RAY_TIME: the time draw (the_next_week/camera.rs:160)
@@ -445,8 +454,8 @@ __device__ __forceinline__ void camera_ray64(uint32_t x, uint32_t y, Path64 &ps)
 // compiled out), chosen per scene by launch_render_pass_f64 like the f32 kernel's classes.
 constexpr int kF64Full = 0, kF64Untextured = 1, kF64Diffuse = 2;
 template <int kClass>
-__device__ __forceinline__ bool shade64(const KParams &P, const float4 *prims, const GMaterial *mtl, Path64 &ps, double t,
-                                        int prim, D3 &sum) {
+__device__ __forceinline__ bool shade64(const KParams &P, const float4 *prims, const GMaterial *mtl, const double *inv_r,
+                                        Path64 &ps, double t, int prim, D3 &sum) {
     if (prim < 0) {
         D3 bg;
         if (P.bg_mode == 1u) {
@@ -461,7 +470,10 @@ __device__ __forceinline__ bool shade64(const KParams &P, const float4 *prims, c
     }
     const float4 cr = prims[prim];
     const D3 p = add(ps.o, muls(ps.d, t));  // Ray::at = orig + t * dir
-    const D3 outward = muls(sub(p, f2d(cr.x, cr.y, cr.z)), 1.0 / (double)cr.w);  // (p - center) / r
+#ifndef RRT_F64_HOST_INVR
+#define RRT_F64_HOST_INVR 0
+#endif
+    const D3 outward = muls(sub(p, f2d(cr.x, cr.y, cr.z)), RRT_F64_HOST_INVR ? inv_r[prim] : 1.0 / (double)cr.w);  // (p - center) / r = (1/r) * v
     const bool front = dot(ps.d, outward) < 0.0;
     const D3 nrm = front ? outward : d3(-outward.x, -outward.y, -outward.z);
     const GMaterial m = mtl[prim];
@@ -523,7 +535,8 @@ __device__ __forceinline__ void render64_body(const KParams &P) {
     const Node *nodes = reinterpret_cast<const Node *>(P.nodes);
     const float4 *prims = P.prim_cr;
     const GMaterial *mtl = P.prim_mtl;
-    if constexpr (kMode == kF64Lds) {  // stage nodes + spheres + their materials once per block
+    const double *inv_r = P.prim_inv_r64;
+    if constexpr (kMode == kF64Lds) {  // stage nodes + spheres + their materials + 1/r once per block
         uint4 *dst = lds_dyn + (P.stack_depth * kBlk * sizeof(uint16_t) + 15u) / 16u;
         const uint4 *src_n = reinterpret_cast<const uint4 *>(P.nodes);
         const uint32_t nn = P.n_nodes * (uint32_t)(sizeof(Node) / 16);
@@ -533,10 +546,14 @@ __device__ __forceinline__ void render64_body(const KParams &P) {
         const uint4 *src_m = reinterpret_cast<const uint4 *>(P.prim_mtl);
         const uint32_t nm = P.n_prims * (uint32_t)(sizeof(GMaterial) / 16);
         for (uint32_t i = threadIdx.x; i < nm; i += kBlk) dst[nn + P.n_prims + i] = src_m[i];
+        double *dr = reinterpret_cast<double *>(dst + nn + P.n_prims + nm);
+        if (P.inv_r_in_lds)
+            for (uint32_t i = threadIdx.x; i < P.n_prims; i += kBlk) dr[i] = P.prim_inv_r64[i];
         __syncthreads();
         nodes = reinterpret_cast<const Node *>(dst);
         prims = reinterpret_cast<const float4 *>(dst + nn);
         mtl = reinterpret_cast<const GMaterial *>(dst + nn + P.n_prims);
+        if (P.inv_r_in_lds) inv_r = dr;
     }
     LdsStack<uint16_t, kBlk> stack;
     stack.init(lds_stack, threadIdx.x);
@@ -655,7 +672,7 @@ __device__ __forceinline__ void render64_body(const KParams &P) {
         __builtin_amdgcn_s_setprio(kPrioShade);
         if (has && !need_ray && tr.node < 0) {
             need_ray = 1;
-            seg_done = shade64<kClass>(P, prims, mtl, ps, tr.closest, tr.hit_prim, sum) ? 1u : 0u;
+            seg_done = shade64<kClass>(P, prims, mtl, inv_r, ps, tr.closest, tr.hit_prim, sum) ? 1u : 0u;
         }
         w_paths += (uint32_t)__popcll(__ballot(seg_done));
         if (seg_done) {  // pixel_color += ray_color(..): already in `sum`
@@ -736,10 +753,12 @@ __global__ __launch_bounds__(256) void rrt_accum64_to_f32(const D4 *__restrict__
     a32[p] = make_float4((float)v.x, (float)v.y, (float)v.z, (float)v.w);
 }
 
-// LDS of the f64 kernel's block in each mode (stack, then the staged scene)
+// LDS of the f64 kernel's block in each mode (stack, then the staged scene; the 1/r table when
+// p.inv_r_in_lds)
 size_t lds64_bytes(const KParams &p, int mode) {
     size_t lds = ((size_t)p.stack_depth * kBlock64 * sizeof(uint16_t) + 15u) / 16u * 16u;
-    if (mode == kF64Lds) lds += (size_t)p.n_nodes * sizeof(GNode) + (size_t)p.n_prims * kPrimBytes;
+    if (mode == kF64Lds)
+        lds += (size_t)p.n_nodes * sizeof(GNode) + (size_t)p.n_prims * (kPrimBytes + (p.inv_r_in_lds ? sizeof(double) : 0u));
     return lds;
 }
 
@@ -764,7 +783,10 @@ hipError_t launch64(const KParams &p, bool count, hipStream_t stream) {
 template <int kClass>
 hipError_t launch64_placed(const KParams &p, bool count, hipStream_t stream) {
     if (!p.scene_in_lds) return launch64<kF64Global, kClass>(p, count, stream);
-    return launch64<kF64Lds, kClass>(p, count, stream);
+    KParams q = p;  // the 1/r table joins the staged scene when the block stays within 64 KB
+    q.inv_r_in_lds = 1u;
+    if (lds64_bytes(q, kF64Lds) > 64u * 1024u) q.inv_r_in_lds = 0u;
+    return launch64<kF64Lds, kClass>(q, count, stream);
 }
 
 }  // namespace

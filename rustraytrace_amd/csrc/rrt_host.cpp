@@ -761,6 +761,7 @@ struct RrtScene {
     uint8_t *d_nodes = nullptr;
     float4 *d_prim_cr = nullptr;
     rrt::GMaterial *d_prim_mtl = nullptr;
+    double *d_prim_inv_r64 = nullptr;  // f64 scenes: 1 / r per leaf-order sphere
     float4 *d_prim_motion = nullptr;
     rrt::GPerlin *d_perlin = nullptr;
     rrt::GQuad *d_quads = nullptr;
@@ -791,6 +792,7 @@ void free_scene(RrtScene *s) {
     (void)hipFree(s->d_nodes);
     (void)hipFree(s->d_prim_cr);
     (void)hipFree(s->d_prim_mtl);
+    (void)hipFree(s->d_prim_inv_r64);
     (void)hipFree(s->d_prim_motion);
     (void)hipFree(s->d_perlin);
     (void)hipFree(s->d_quads);
@@ -869,9 +871,13 @@ int fill_params(RrtScene *s, const RrtTile *t, float *d_accum, rrt::KParams &p) 
     p.tiles_x = (p.width + rrt::kTileW - 1u) / rrt::kTileW;
     p.n_work_tiles = p.tiles_x * ((p.tile_rows + rrt::kTileH - 1u) / rrt::kTileH);
     const uint32_t S = t->sample_end - t->sample_begin;
-    // the frame's chunk (rrt_accum_chunk): K when S > 2K, else K/2 — big chunks pay at high spp
-    // (per-unit cost), small ones at low spp (drain granularity)
-    p.chunk = S > 2u * p.chunk ? p.chunk : std::max(1u, p.chunk / 2u);
+    // the frame's chunk (rrt_accum_chunk = K0): halved while S <= 2K, down to K0/4 — big chunks pay
+    // at high spp (per-unit cost), small ones at low spp (drain granularity). K0 = 256: S > 512 ->
+    // 256 (C4, C3), 256 < S <= 512 -> 128 (C2), S <= 256 -> 64 (C5)
+    {
+        const uint32_t k0 = p.chunk;
+        while (p.chunk > std::max(1u, k0 / 4u) && S <= 2u * p.chunk) p.chunk /= 2u;
+    }
     if (const char *e = std::getenv("RRT_CHUNK_FORCE")) p.chunk = (uint32_t)std::max(1, std::atoi(e));  // A/B only
     p.chunk_small = std::max(1u, p.chunk / 8u);
     p.n_big = S > p.chunk ? (S - 1u) / p.chunk : 0u;
@@ -913,10 +919,12 @@ int fill_params(RrtScene *s, const RrtTile *t, float *d_accum, rrt::KParams &p) 
     return RRT_OK;
 }
 
-// Samples per big chunk (tail chunks K/8). 128 since round 2: with 8 work queues the per-unit cost
-// matters more than the drain — C2 +1.2 %, C4 +10 %, C5 -0.5 % against 64 (256: C4 +12.5 %, C5 -3 %).
+// The largest big chunk K0 (tail chunks K/8; the frame's K: rrt_accum_chunk's rule, halved while
+// S <= 2K down to K0/4). 128 in round 2 (with 8 work queues the per-unit cost matters more than the
+// drain: C2 +1.2 %, C4 +10 %, C5 -0.5 % against 64); 256 since round 4 for frames over 512 samples:
+// C4 +2.4 %, C3 +0.8 % same-box, C2 and C5 keep 128 and 64 (K = 256 at C2's 512 spp: -0.3 %).
 uint32_t accum_chunk() {
-    uint32_t c = 128;
+    uint32_t c = 256;
     if (const char *e = std::getenv("RRT_CHUNK")) c = (uint32_t)std::max(1, std::atoi(e));
     return c;
 }
@@ -1170,6 +1178,11 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
         if ((rc = upload(&s->d_prim_cr, prim_cr.data(), prim_cr.size(), "spheres"))) break;
         if ((rc = upload(&s->d_prim_mtl, prim_mtl.data(), prim_mtl.size(), "sphere materials"))) break;
         if (book2 && (rc = upload(&s->d_prim_motion, prim_motion.data(), prim_motion.size(), "sphere motion"))) break;
+        if (f64) {
+            std::vector<double> inv_r(n_prims);
+            for (uint32_t i = 0; i < n_prims; ++i) inv_r[i] = 1.0 / (double)prim_cr[i].w;
+            if ((rc = upload(&s->d_prim_inv_r64, inv_r.data(), inv_r.size(), "sphere 1/r"))) break;
+        }
         if (n_perlin && (rc = upload(&s->d_perlin, perlin.data(), perlin.size(), "Perlin tables"))) break;
         if (!gquads.empty() && (rc = upload(&s->d_quads, gquads.data(), gquads.size(), "quads"))) break;
         if (n_media && (rc = upload(&s->d_media, gmedia.data(), gmedia.size(), "media"))) break;
@@ -1197,6 +1210,7 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
     p.nodes = s->d_nodes;
     p.prim_cr = s->d_prim_cr;
     p.prim_mtl = s->d_prim_mtl;
+    p.prim_inv_r64 = s->d_prim_inv_r64;
     p.prim_motion = s->d_prim_motion;
     p.perlin = s->d_perlin;
     p.n_perlin = n_perlin;
@@ -1227,6 +1241,12 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
         p.cam_u[i] = cam->u[i];
         p.cam_v[i] = cam->v[i];
         p.background[i] = cam->background[i];
+        p.cam64[0][i] = (double)cam->pixel00[i];
+        p.cam64[1][i] = (double)cam->pixel_delta_u[i];
+        p.cam64[2][i] = (double)cam->pixel_delta_v[i];
+        p.cam64[3][i] = (double)cam->origin[i];
+        p.cam64[4][i] = (double)cam->u[i] * (double)radius;  // camera.rs:136-138 in f64
+        p.cam64[5][i] = (double)cam->v[i] * (double)radius;
     }
     p.defocus_radius = radius;
     p.max_depth = cam->params_u[0];

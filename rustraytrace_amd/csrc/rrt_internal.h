@@ -225,6 +225,13 @@ struct KParams {
     D4 *partial64;
     float cam_u[3];
     float cam_v[3];
+    // 1 / r per leaf-order sphere in f64 (sphere.rs:48's (p - center) / radius is (1/r) * v,
+    // vec3.rs:142-148: the same IEEE quotient, formed once on the host)
+    const double *prim_inv_r64;
+    uint32_t inv_r_in_lds;  // f64 kernel, scene in LDS: the 1/r table staged too (fits the block's 64 KB)
+    // the camera block widened to f64 on the host, as camera.rs:136-180 forms it from the f32 ABI
+    // values: pixel00, delta_u, delta_v, center, defocus_disk_u = u * radius, defocus_disk_v
+    double cam64[6][3];
 };
 
 // RRT_FLAG_F64 (include/rrt_hip.h): the f64 books-arithmetic kernel (rrt_books64.hip)

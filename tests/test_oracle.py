@@ -444,7 +444,8 @@ def test_bvh2_node_layouts_hold_the_same_tree(monkeypatch):
     assert np.all(lo_h[~live] == 65504.0) and np.all(hi_h[~live] == 65504.0)
 
 
-@pytest.mark.parametrize("S,chunk", [(20, 8), (512, 64), (64, 64), (65, 64), (7, 0), (300, 128), (256, 128)])
+@pytest.mark.parametrize("S,chunk", [(20, 8), (512, 64), (64, 64), (65, 64), (7, 0), (300, 128), (256, 128),
+                                     (600, 256), (513, 256), (512, 256), (256, 256)])
 def test_accum_chunk_schedule(S, chunk):
     """The TWIN accum groups samples as rrt_accum_chunk documents (include/rrt_hip.h): (S-1)/K
     chunks of K, then chunks of max(1, K/8); in-order f32 sums per chunk, chunks added in order."""
@@ -452,7 +453,9 @@ def test_accum_chunk_schedule(S, chunk):
     got, _, _ = oracle.render(sc, oracle.TWIN, chunk=chunk)
     per = [oracle.render(sc, oracle.TWIN, samples=(s, s + 1))[0][..., :3].astype(np.float32)
            for s in range(S)]
-    K = (chunk if S > 2 * chunk else max(1, chunk // 2)) if chunk else S  # the frame's chunk
+    K = chunk if chunk else S  # the frame's chunk: halved while S <= 2K, down to chunk / 4
+    while chunk and K > max(1, chunk // 4) and S <= 2 * K:
+        K //= 2
     k = max(1, K // 8) if chunk else S
     nb = (S - 1) // K if chunk and S > K else 0
     bounds, c0 = [], 0

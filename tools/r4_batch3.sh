@@ -16,3 +16,7 @@ for r in 1 2; do for k in 0 256; do
   timeout -k 10 200 python bench.py --config C2 --steps 3 --warmup 1 --no-cpu-baseline --no-breakdown --no-extra --no-f64 > gpurun_out/r4g_c2_k$k.json 2>/dev/null || exit 1
   echo "r$r K=$k C2 $(python -c "import json;d=json.load(open('gpurun_out/r4g_c2_k$k.json'));print(d['value'],d['kernel_ms_avg'])")"
 done; done > gpurun_out/r4g_c2_chunk.log 2>&1
+timeout -k 10 300 python -u -m pytest tests/test_gpu_books64.py tests/test_gpu_multidevice.py -x -q --timeout 200 --timeout-method thread > gpurun_out/r4g_f64_tests.log 2>&1 || exit 1
+for c in C2 C5 C4; do CONFIG=$c ROUNDS=2 VARIANTS="f64prev f64cam" timeout -k 10 300 bash tools/ab_f64.sh || exit 1; done > gpurun_out/r4g_f64_ab.log 2>&1
+timeout -k 10 400 python -u -m pytest tests/test_gpu_book2.py tests/test_gpu_book3.py -x -q --timeout 200 --timeout-method thread > gpurun_out/r4g_book2_tests.log 2>&1 || exit 1
+for c in NW9 NW8; do VARIANTS="f64cam medexit" ROUNDS=2 STEPS=3 BENCH_ARGS="--config $c --no-extra" timeout -k 10 300 bash tools/ab.sh || exit 1; done > gpurun_out/r4g_medexit_ab.log 2>&1
