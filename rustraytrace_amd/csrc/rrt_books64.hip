@@ -376,17 +376,27 @@ __device__ __forceinline__ double div_a64(double n, double a, double ra) {
     return __builtin_fma(__builtin_fma(-a, q, n), ra, q);
 }
 
-template <bool kCount>
-__device__ __forceinline__ void leaves64(const float4 *__restrict__ prims, Leaves lv, D3 o, D3 d, double a, Trav64 &t,
+// A sphere record widened to f64 while the block stages the scene in LDS (kF64LdsWide): center and
+// radius converted once (exact) instead of four f32 -> f64 conversions per sphere test.
+struct alignas(16) Sphere64 {
+    double cx, cy, cz, r;
+};
+__device__ __forceinline__ D3 center_of(const float4 &c) { return f2d(c.x, c.y, c.z); }
+__device__ __forceinline__ D3 center_of(const Sphere64 &c) { return d3(c.cx, c.cy, c.cz); }
+__device__ __forceinline__ double radius_of(const float4 &c) { return (double)c.w; }
+__device__ __forceinline__ double radius_of(const Sphere64 &c) { return c.r; }
+
+template <bool kCount, typename Rec>
+__device__ __forceinline__ void leaves64(const Rec *__restrict__ prims, Leaves lv, D3 o, D3 d, double a, Trav64 &t,
                                          Counters &cnt) {
     const double ra = RRT_F64_DIVA ? recip_a64(a) : 0.0;
     const int first = (int)(lv & kLinkFirstMask), count = (int)(lv >> kLinkCountShift);
     for (int i = first; i < first + count; ++i) {
         if (kCount) cnt.spheres++;
-        const float4 cr = prims[i];
-        const D3 oc = sub(f2d(cr.x, cr.y, cr.z), o);
+        const Rec cr = prims[i];
+        const D3 oc = sub(center_of(cr), o);
         const double h = dot(d, oc);
-        const double r = (double)cr.w;
+        const double r = radius_of(cr);
         const double c = dot(oc, oc) - r * r;
         const double disc = h * h - a * c;
         if (disc < 0.0) continue;
@@ -415,7 +425,7 @@ __device__ __forceinline__ void camera_ray64(uint32_t x, uint32_t y, Path64 &ps)
     const double ox = rnd64(ps.rng) - 0.5, oy = rnd64(ps.rng) - 0.5;  // sample_square
     const double fi = (double)x + ox, fj = (double)y + oy;
 #ifndef RRT_F64_CAM64
-#define RRT_F64_CAM64 0
+#define RRT_F64_CAM64 1
 #endif
 #if !RRT_F64_CAM64
     const D3 sample = d3(((double)C.p00[0] + (double)C.du[0] * fi) + (double)C.dv[0] * fj,
@@ -453,8 +463,8 @@ __device__ __forceinline__ void camera_ray64(uint32_t x, uint32_t y, Path64 &ps)
 // atan2 / texel path compiled out), kF64Diffuse (Lambertian and emissive only: metal and dielectric
 // compiled out), chosen per scene by launch_render_pass_f64 like the f32 kernel's classes.
 constexpr int kF64Full = 0, kF64Untextured = 1, kF64Diffuse = 2;
-template <int kClass>
-__device__ __forceinline__ bool shade64(const KParams &P, const float4 *prims, const GMaterial *mtl, const double *inv_r,
+template <int kClass, typename Rec>
+__device__ __forceinline__ bool shade64(const KParams &P, const Rec *prims, const GMaterial *mtl, const double *inv_r,
                                         Path64 &ps, double t, int prim, D3 &sum) {
     if (prim < 0) {
         D3 bg;
@@ -468,12 +478,13 @@ __device__ __forceinline__ bool shade64(const KParams &P, const float4 *prims, c
         sum = add(sum, mul(ps.T, bg));
         return true;
     }
-    const float4 cr = prims[prim];
+    const Rec cr = prims[prim];
     const D3 p = add(ps.o, muls(ps.d, t));  // Ray::at = orig + t * dir
 #ifndef RRT_F64_HOST_INVR
-#define RRT_F64_HOST_INVR 0
+#define RRT_F64_HOST_INVR 1
 #endif
-    const D3 outward = muls(sub(p, f2d(cr.x, cr.y, cr.z)), RRT_F64_HOST_INVR ? inv_r[prim] : 1.0 / (double)cr.w);  // (p - center) / r = (1/r) * v
+    // (p - center) / r = (1/r) * v (vec3.rs:142-148)
+    const D3 outward = muls(sub(p, center_of(cr)), RRT_F64_HOST_INVR ? inv_r[prim] : 1.0 / radius_of(cr));
     const bool front = dot(ps.d, outward) < 0.0;
     const D3 nrm = front ? outward : d3(-outward.x, -outward.y, -outward.z);
     const GMaterial m = mtl[prim];
@@ -524,35 +535,43 @@ __device__ __forceinline__ bool shade64(const KParams &P, const float4 *prims, c
 // The persistent work loop of rrt_kernel.hip's render_body (same queue, units, chunk order,
 // postponed leaves and wave-uniform exits) over Path64 state.
 // kMode: kF64Global (f16 nodes and records read from global memory), kF64Lds (the f32 nodes,
-// spheres and materials staged in LDS).
-constexpr int kF64Global = 0, kF64Lds = 1;
+// spheres and materials staged in LDS), kF64LdsWide (the same with the sphere records widened to
+// f64, Sphere64, when the block stays within 64 KB). The 1/r table joins an LDS scene when it fits.
+constexpr int kF64Global = 0, kF64Lds = 1, kF64LdsWide = 2;
 template <int kMode, bool kCount, int kBlk, int kClass>
 __device__ __forceinline__ void render64_body(const KParams &P) {
     constexpr bool kLds = kMode != kF64Global;
+    using Rec = typename std::conditional<kMode == kF64LdsWide, Sphere64, float4>::type;
     extern __shared__ uint4 lds_dyn[];
     uint16_t *lds_stack = reinterpret_cast<uint16_t *>(lds_dyn);
     using Node = typename std::conditional<kLds, GNode, GNodeH>::type;
     const Node *nodes = reinterpret_cast<const Node *>(P.nodes);
-    const float4 *prims = P.prim_cr;
+    const Rec *prims = reinterpret_cast<const Rec *>(P.prim_cr);
     const GMaterial *mtl = P.prim_mtl;
     const double *inv_r = P.prim_inv_r64;
-    if constexpr (kMode == kF64Lds) {  // stage nodes + spheres + their materials + 1/r once per block
+    if constexpr (kLds) {  // stage nodes + spheres + their materials (+ 1/r) once per block
         uint4 *dst = lds_dyn + (P.stack_depth * kBlk * sizeof(uint16_t) + 15u) / 16u;
         const uint4 *src_n = reinterpret_cast<const uint4 *>(P.nodes);
         const uint32_t nn = P.n_nodes * (uint32_t)(sizeof(Node) / 16);
         for (uint32_t i = threadIdx.x; i < nn; i += kBlk) dst[i] = src_n[i];
-        const uint4 *src_p = reinterpret_cast<const uint4 *>(P.prim_cr);
-        for (uint32_t i = threadIdx.x; i < P.n_prims; i += kBlk) dst[nn + i] = src_p[i];
+        constexpr uint32_t kRec16 = (uint32_t)(sizeof(Rec) / 16);
+        for (uint32_t i = threadIdx.x; i < P.n_prims; i += kBlk) {
+            const float4 c = P.prim_cr[i];
+            if constexpr (kMode == kF64LdsWide)
+                reinterpret_cast<Sphere64 *>(dst + nn)[i] = Sphere64{(double)c.x, (double)c.y, (double)c.z, (double)c.w};
+            else
+                reinterpret_cast<float4 *>(dst + nn)[i] = c;
+        }
         const uint4 *src_m = reinterpret_cast<const uint4 *>(P.prim_mtl);
-        const uint32_t nm = P.n_prims * (uint32_t)(sizeof(GMaterial) / 16);
-        for (uint32_t i = threadIdx.x; i < nm; i += kBlk) dst[nn + P.n_prims + i] = src_m[i];
-        double *dr = reinterpret_cast<double *>(dst + nn + P.n_prims + nm);
+        const uint32_t np = P.n_prims * kRec16, nm = P.n_prims * (uint32_t)(sizeof(GMaterial) / 16);
+        for (uint32_t i = threadIdx.x; i < nm; i += kBlk) dst[nn + np + i] = src_m[i];
+        double *dr = reinterpret_cast<double *>(dst + nn + np + nm);
         if (P.inv_r_in_lds)
             for (uint32_t i = threadIdx.x; i < P.n_prims; i += kBlk) dr[i] = P.prim_inv_r64[i];
         __syncthreads();
         nodes = reinterpret_cast<const Node *>(dst);
-        prims = reinterpret_cast<const float4 *>(dst + nn);
-        mtl = reinterpret_cast<const GMaterial *>(dst + nn + P.n_prims);
+        prims = reinterpret_cast<const Rec *>(dst + nn);
+        mtl = reinterpret_cast<const GMaterial *>(dst + nn + np);
         if (P.inv_r_in_lds) inv_r = dr;
     }
     LdsStack<uint16_t, kBlk> stack;
@@ -757,8 +776,10 @@ __global__ __launch_bounds__(256) void rrt_accum64_to_f32(const D4 *__restrict__
 // p.inv_r_in_lds)
 size_t lds64_bytes(const KParams &p, int mode) {
     size_t lds = ((size_t)p.stack_depth * kBlock64 * sizeof(uint16_t) + 15u) / 16u * 16u;
-    if (mode == kF64Lds)
-        lds += (size_t)p.n_nodes * sizeof(GNode) + (size_t)p.n_prims * (kPrimBytes + (p.inv_r_in_lds ? sizeof(double) : 0u));
+    if (mode != kF64Global)
+        lds += (size_t)p.n_nodes * sizeof(GNode) +
+               (size_t)p.n_prims * ((mode == kF64LdsWide ? sizeof(Sphere64) : sizeof(float4)) + sizeof(GMaterial) +
+                                    (p.inv_r_in_lds ? sizeof(double) : 0u));
     return lds;
 }
 
@@ -780,11 +801,17 @@ hipError_t launch64(const KParams &p, bool count, hipStream_t stream) {
 
 // The scene placement: the f32 nodes, spheres and materials in LDS when they fit (C1, C2, C4), else
 // the f16 nodes and records from global memory (C5).
+#ifndef RRT_F64_WIDE_SPHERES
+#define RRT_F64_WIDE_SPHERES 1
+#endif
 template <int kClass>
 hipError_t launch64_placed(const KParams &p, bool count, hipStream_t stream) {
     if (!p.scene_in_lds) return launch64<kF64Global, kClass>(p, count, stream);
-    KParams q = p;  // the 1/r table joins the staged scene when the block stays within 64 KB
+    // the widened sphere records and the 1/r table join the staged scene while the block stays
+    // within the 64 KB it may declare
+    KParams q = p;
     q.inv_r_in_lds = 1u;
+    if (RRT_F64_WIDE_SPHERES && lds64_bytes(q, kF64LdsWide) <= 64u * 1024u) return launch64<kF64LdsWide, kClass>(q, count, stream);
     if (lds64_bytes(q, kF64Lds) > 64u * 1024u) q.inv_r_in_lds = 0u;
     return launch64<kF64Lds, kClass>(q, count, stream);
 }

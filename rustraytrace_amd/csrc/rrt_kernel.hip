@@ -413,12 +413,6 @@ __device__ __forceinline__ bool medium_hit(const PR &pr, int m, V3 o, V3 d, cons
     const float len = __builtin_sqrtf(rk.a);
     const float inside = (t2 - t1) * len;
     const float u = (float)(uint32_t)(splitmix64(pr.seg ^ (uint64_t)m) >> 40) * 0x1.0p-24f;
-    // The free flight exceeds the chord (no scatter) whenever -(1 - u) / density already does by a
-    // relative 1e-5: ln u <= u - 1, rrt_logf(u) stays within 1e-6 of it relative to 1 - u on the
-    // whole 2^-24 draw grid (tests/test_book2.py), and 1 - u is exact there, so the rounded
-    // neg_inv_density * rrt_logf(u) is then above `inside` too — the same decision without the
-    // log. A thin fog (final_scene's density 1e-4) takes this exit for almost every segment.
-    if (g.neg_inv_density * (u - 1.0f) > inside * 1.00001f) return false;
     const float hd = g.neg_inv_density * rrt_logf(u);
     if (hd > inside) return false;
     t_out = t1 + hd / len;

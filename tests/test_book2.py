@@ -404,25 +404,3 @@ def test_media_scene_structure():
     assert (s9.width, s9.spp, s9.max_depth) == (800, 10000, 40)
     assert len(s9.spheres) == len(s10.spheres) and len(s9.quads) == len(s10.quads)
 
-
-def test_log_bound_of_the_medium_early_exit():
-    """rrt_kernel.hip medium_hit skips the log when neg_inv_density * (u - 1) > inside * 1.00001: it
-    relies on |rrt_logf(u)| >= (1 - u) (1 - 1e-6) on the whole draw grid u = k 2^-24, k in
-    [1, 2^24) (ln u <= u - 1), and on 1 - u being exact there. Exhaustive over the grid; then the
-    early decision against the full one at sampled densities and chords."""
-    k = np.arange(1, 2 ** 24, dtype=np.int64)
-    u = (k.astype(np.float32) * np.float32(2.0 ** -24)).astype(np.float32)
-    one_minus = (np.float32(1.0) - u).astype(np.float32)
-    assert np.array_equal(one_minus.astype(np.float64), 1.0 - k.astype(np.float64) * 2.0 ** -24)  # exact
-    L = oracle.log_f32(u)
-    ratio = -L.astype(np.float64) / one_minus.astype(np.float64)
-    assert ratio.min() >= 1.0 - 1e-6, ratio.min()
-    rng = np.random.default_rng(3)
-    for density in (1e-4, 0.01, 0.2, 1.0, 37.0):
-        nid = np.float32(-1.0 / density)
-        sel = rng.choice(u.size, 200_000, replace=False)
-        uu, LL = u[sel], L[sel]
-        inside = np.float32(rng.uniform(0, 3, sel.size) / density).astype(np.float32)
-        early = (nid * (uu - np.float32(1.0))).astype(np.float32) > (inside * np.float32(1.00001)).astype(np.float32)
-        full = (nid * LL).astype(np.float32) > inside
-        assert early.sum() > 0 and np.all(full[early])  # the early exit only where the full test rejects too
