@@ -264,18 +264,11 @@ __device__ __forceinline__ D3 texel64(const KParams &P, int tex, D3 outward) {
     return d3(cs * (double)px[0], cs * (double)px[1], cs * (double)px[2]);
 }
 
-// LDS scenes: 112-B nodes whose axis a holds both children's (lo, hi) then both (hi, lo), one
-// ds_read_b128 per axis (rrt_kernel.hip RRT_NODE96); the materials then come from global memory.
-#ifndef RRT_F64_NODE96
-#define RRT_F64_NODE96 0
-#endif
-
 // Per-ray constants of the box test (rrt_box32.h: f32 arithmetic on the f32 / f16 planes, widened
 // so that it never rejects a box the f64 ray meets).
 struct RayK64 {
     RayBox32 b;
-    // byte offsets of the ray's (entry, exit) plane pair of each axis in a GNode child box (the
-    // f32 kernel's RayK): 12a + 4 when 1/d_a < 0 (hi, lo), else 12a (lo, hi)
+    // byte offsets of the ray's (entry, exit) plane pairs of each axis in an LDS Node112
     uint32_t ox, oy, oz;
     // the 32-B f16 node (GNodeH, global memory) holds lo | hi << 16 per axis: rotating the word by
     // 16 bits when 1/d_a < 0 puts the (entry, exit) pair in (lo, hi) order
@@ -284,15 +277,11 @@ struct RayK64 {
 __device__ __forceinline__ RayK64 ray_consts64(D3 o, D3 d) {
     RayK64 r;
     r.b = box32_ray(o.x, o.y, o.z, d.x, d.y, d.z);
-    if constexpr (RRT_F64_NODE96) {  // the 112-B LDS node (rrt_kernel.hip RRT_NODE96)
-        r.ox = r.b.ix < 0.0f ? 16u : 0u;
-        r.oy = r.b.iy < 0.0f ? 48u : 32u;
-        r.oz = r.b.iz < 0.0f ? 80u : 64u;
-    } else {
-        r.ox = r.b.ix < 0.0f ? 4u : 0u;
-        r.oy = r.b.iy < 0.0f ? 16u : 12u;
-        r.oz = r.b.iz < 0.0f ? 28u : 24u;
-    }
+    // the ray's (entry, exit) offsets in a Node112 axis: both children's (lo, hi) at 32a, (hi, lo)
+    // at 32a + 16
+    r.ox = r.b.ix < 0.0f ? 16u : 0u;
+    r.oy = r.b.iy < 0.0f ? 48u : 32u;
+    r.oz = r.b.iz < 0.0f ? 80u : 64u;
     r.rx = r.b.ix < 0.0f ? 16u : 0u;
     r.ry = r.b.iy < 0.0f ? 16u : 0u;
     r.rz = r.b.iz < 0.0f ? 16u : 0u;
@@ -318,7 +307,7 @@ __device__ __forceinline__ bool trav_node64(const Node *__restrict__ nodes, Stac
     bool h0, h1;
     uint32_t l0, l1;
     float tn0 = 0.0f, tn1 = 0.0f;
-    if constexpr (std::is_same<Node, GNode>::value && RRT_F64_NODE96) {
+    if constexpr (std::is_same<Node, GNode>::value) {  // LDS: the Node112 layout (render64_body)
         const char *bx = reinterpret_cast<const char *>(nodes) + __umul24((uint32_t)t.node, 112u);
         auto quad = [&](uint32_t byte_off) { return *reinterpret_cast<const float4 *>(bx + byte_off); };
         const float4 x = quad(rk.ox), y = quad(rk.oy), z = quad(rk.oz);
@@ -327,16 +316,6 @@ __device__ __forceinline__ bool trav_node64(const Node *__restrict__ nodes, Stac
         const uint2 lk = *reinterpret_cast<const uint2 *>(bx + 96);
         l0 = lk.x;
         l1 = lk.y;
-    } else if constexpr (std::is_same<Node, GNode>::value) {
-        const GNode &n = nodes[t.node];  // LDS: lo, hi, lo per axis, each pair read at the ray's sign offset
-        const char *bx = reinterpret_cast<const char *>(&n.box[0][0]);
-        auto plane = [&](uint32_t byte_off) { return *reinterpret_cast<const float *>(bx + byte_off); };
-        h0 = box32_hit(plane(rk.ox), plane(rk.ox + 4), plane(rk.oy), plane(rk.oy + 4), plane(rk.oz), plane(rk.oz + 4),
-                       rk.b, t.closest32, tn0);
-        h1 = box32_hit(plane(rk.ox + 36), plane(rk.ox + 40), plane(rk.oy + 36), plane(rk.oy + 40), plane(rk.oz + 36),
-                       plane(rk.oz + 40), rk.b, t.closest32, tn1);
-        l0 = n.link[0];
-        l1 = n.link[1];
     } else {  // global memory: the 32-B f16 node (GNodeH), each axis's halves in (entry, exit) order
         const uint4 *q = reinterpret_cast<const uint4 *>(nodes + t.node);
         const uint4 a = q[0], b = q[1];
@@ -407,13 +386,10 @@ __device__ __forceinline__ D3 center_of(const Sphere64 &c) { return d3(c.cx, c.c
 __device__ __forceinline__ double radius_of(const float4 &c) { return (double)c.w; }
 __device__ __forceinline__ double radius_of(const Sphere64 &c) { return c.r; }
 
-#ifndef RRT_F64_RA_HOIST
-#define RRT_F64_RA_HOIST 0
-#endif
 template <bool kCount, typename Rec>
-__device__ __forceinline__ void leaves64(const Rec *__restrict__ prims, Leaves lv, D3 o, D3 d, double a, double ra_in,
-                                         Trav64 &t, Counters &cnt) {
-    const double ra = RRT_F64_RA_HOIST ? ra_in : (RRT_F64_DIVA ? recip_a64(a) : 0.0);
+__device__ __forceinline__ void leaves64(const Rec *__restrict__ prims, Leaves lv, D3 o, D3 d, double a, Trav64 &t,
+                                         Counters &cnt) {
+    const double ra = RRT_F64_DIVA ? recip_a64(a) : 0.0;
     const int first = (int)(lv & kLinkFirstMask), count = (int)(lv >> kLinkCountShift);
     for (int i = first; i < first + count; ++i) {
         if (kCount) cnt.spheres++;
@@ -558,8 +534,8 @@ __device__ __forceinline__ bool shade64(const KParams &P, const Rec *prims, cons
 
 // The persistent work loop of rrt_kernel.hip's render_body (same queue, units, chunk order,
 // postponed leaves and wave-uniform exits) over Path64 state.
-// kMode: kF64Global (f16 nodes and records read from global memory), kF64Lds (the f32 nodes,
-// spheres and materials staged in LDS), kF64LdsWide (the same with the sphere records widened to
+// kMode: kF64Global (f16 nodes and records read from global memory), kF64Lds (the f32 nodes as
+// Node112 and the spheres staged in LDS), kF64LdsWide (the same with the sphere records widened to
 // f64, Sphere64, when the block stays within 64 KB). The 1/r table joins an LDS scene when it fits.
 constexpr int kF64Global = 0, kF64Lds = 1, kF64LdsWide = 2;
 template <int kMode, bool kCount, int kBlk, int kClass>
@@ -573,10 +549,15 @@ __device__ __forceinline__ void render64_body(const KParams &P) {
     const Rec *prims = reinterpret_cast<const Rec *>(P.prim_cr);
     const GMaterial *mtl = P.prim_mtl;
     const double *inv_r = P.prim_inv_r64;
-    if constexpr (kLds) {  // stage nodes + spheres + their materials (+ 1/r) once per block
+    if constexpr (kLds) {  // stage nodes + spheres (+ 1/r) once per block
         uint4 *dst = lds_dyn + (P.stack_depth * kBlk * sizeof(uint16_t) + 15u) / 16u;
+        // Node112: each 80-B GNode re-laid as 112 B whose axis a holds both children's (lo, hi), then
+        // both (hi, lo), and the links at 96 — one ds_read_b128 per axis at the ray's sign offset
+        // reads both children's (entry, exit) pairs (4 LDS cycles, against 8 for two ds_read2_b32):
+        // C2 +0.5 %, C4 +0.6 % same-box. The materials stay in global memory (one 32-B read per hit)
+        // so the block keeps within the 64 KB it may declare.
         uint32_t nn;
-        if constexpr (RRT_F64_NODE96) {
+        {
             const GNode *sn = reinterpret_cast<const GNode *>(P.nodes);
             for (uint32_t i = threadIdx.x; i < P.n_nodes; i += kBlk) {
                 const GNode g = sn[i];
@@ -590,10 +571,6 @@ __device__ __forceinline__ void render64_body(const KParams &P) {
                 o[6] = make_uint4(g.link[0], g.link[1], 0u, 0u);
             }
             nn = 7u * P.n_nodes;
-        } else {
-            const uint4 *src_n = reinterpret_cast<const uint4 *>(P.nodes);
-            nn = P.n_nodes * (uint32_t)(sizeof(Node) / 16);
-            for (uint32_t i = threadIdx.x; i < nn; i += kBlk) dst[i] = src_n[i];
         }
         constexpr uint32_t kRec16 = (uint32_t)(sizeof(Rec) / 16);
         for (uint32_t i = threadIdx.x; i < P.n_prims; i += kBlk) {
@@ -603,16 +580,13 @@ __device__ __forceinline__ void render64_body(const KParams &P) {
             else
                 reinterpret_cast<float4 *>(dst + nn)[i] = c;
         }
-        const uint4 *src_m = reinterpret_cast<const uint4 *>(P.prim_mtl);
-        const uint32_t np = P.n_prims * kRec16, nm = RRT_F64_NODE96 ? 0u : P.n_prims * (uint32_t)(sizeof(GMaterial) / 16);
-        for (uint32_t i = threadIdx.x; i < nm; i += kBlk) dst[nn + np + i] = src_m[i];
-        double *dr = reinterpret_cast<double *>(dst + nn + np + nm);
+        const uint32_t np = P.n_prims * kRec16;
+        double *dr = reinterpret_cast<double *>(dst + nn + np);
         if (P.inv_r_in_lds)
             for (uint32_t i = threadIdx.x; i < P.n_prims; i += kBlk) dr[i] = P.prim_inv_r64[i];
         __syncthreads();
         nodes = reinterpret_cast<const Node *>(dst);
         prims = reinterpret_cast<const Rec *>(dst + nn);
-        if (!RRT_F64_NODE96) mtl = reinterpret_cast<const GMaterial *>(dst + nn + np);
         if (P.inv_r_in_lds) inv_r = dr;
     }
     LdsStack<uint16_t, kBlk> stack;
@@ -703,11 +677,10 @@ __device__ __forceinline__ void render64_body(const KParams &P) {
         const uint32_t min_active = (live * P.trav_frac) >> 8;
         const uint32_t leaf_min = (live * P.leaf_frac) >> 8;
         RayK64 rk;
-        double a = 0.0, ra = 0.0;
+        double a = 0.0;
         if (tr.node >= 0) {
             rk = ray_consts64(ps.o, ps.d);
             a = dot(ps.d, ps.d);  // sphere.rs:27 r.direction().length_squared()
-            if (RRT_F64_RA_HOIST && RRT_F64_DIVA) ra = recip_a64(a);  // the root divisions' reciprocal, once per loop entry
         }
         __builtin_amdgcn_s_setprio(kPrioNode);
         Leaves lv = 0;
@@ -723,7 +696,7 @@ __device__ __forceinline__ void render64_body(const KParams &P) {
             if ((pm != 0) & batch) {
                 __builtin_amdgcn_s_setprio(kPrioLeaf);
                 if (lv != 0) {
-                    leaves64<kCount>(prims, lv, ps.o, ps.d, a, ra, tr, cnt);
+                    leaves64<kCount>(prims, lv, ps.o, ps.d, a, tr, cnt);
                     lv = 0;
                 }
                 __builtin_amdgcn_s_setprio(kPrioNode);
@@ -819,9 +792,9 @@ __global__ __launch_bounds__(256) void rrt_accum64_to_f32(const D4 *__restrict__
 size_t lds64_bytes(const KParams &p, int mode) {
     size_t lds = ((size_t)p.stack_depth * kBlock64 * sizeof(uint16_t) + 15u) / 16u * 16u;
     if (mode != kF64Global)
-        lds += (size_t)p.n_nodes * (RRT_F64_NODE96 ? 112u : sizeof(GNode)) +
+        lds += (size_t)p.n_nodes * 112u +
                (size_t)p.n_prims * ((mode == kF64LdsWide ? sizeof(Sphere64) : sizeof(float4)) +
-                                    (RRT_F64_NODE96 ? 0u : sizeof(GMaterial)) + (p.inv_r_in_lds ? sizeof(double) : 0u));
+                                    (p.inv_r_in_lds ? sizeof(double) : 0u));
     return lds;
 }
 

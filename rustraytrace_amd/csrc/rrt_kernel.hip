@@ -25,7 +25,6 @@
 #include "rrt_internal.h"
 
 #include <algorithm>
-#include <cstdlib>
 #include <type_traits>
 
 namespace rrt {
@@ -59,14 +58,6 @@ namespace {
 #endif
 
 #include "rrt_device.h"
-
-// Book-1 LDS scenes: the block re-lays each 80-B GNode into a 112-B LDS node whose axis a holds both
-// children's (lo, hi) then both (hi, lo): one ds_read_b128 per axis (4 LDS cycles) reads both
-// children's (entry, exit) pairs instead of two ds_read2_b32 (8); the per-sphere materials are then
-// read from global memory to keep three 512-thread blocks per CU.
-#ifndef RRT_NODE96
-#define RRT_NODE96 0
-#endif
 
 
 
@@ -235,15 +226,9 @@ __device__ __forceinline__ RayK ray_consts(V3 o, V3 d) {
     // is NaN or -inf, and a slab that straddles o (lo < 0 < hi about o's sign) rejects the ray.
     r.inv = v3(clamp_inv(1.0f / d.x), clamp_inv(1.0f / d.y), clamp_inv(1.0f / d.z));
     r.oi = v3(o.x * r.inv.x, o.y * r.inv.y, o.z * r.inv.z);
-    if constexpr (RRT_NODE96) {  // axis a at 32a: both children's (lo, hi), then both (hi, lo)
-        r.ox = r.inv.x < 0.0f ? 16u : 0u;
-        r.oy = r.inv.y < 0.0f ? 48u : 32u;
-        r.oz = r.inv.z < 0.0f ? 80u : 64u;
-    } else {
-        r.ox = r.inv.x < 0.0f ? 4u : 0u;
-        r.oy = r.inv.y < 0.0f ? 16u : 12u;
-        r.oz = r.inv.z < 0.0f ? 28u : 24u;
-    }
+    r.ox = r.inv.x < 0.0f ? 4u : 0u;
+    r.oy = r.inv.y < 0.0f ? 16u : 12u;
+    r.oz = r.inv.z < 0.0f ? 28u : 24u;
     r.a = dot(d, d);                                  // sphere.rs:27, hoisted per ray
     // The reciprocal step of the IEEE f32 division expansion (v_rcp + one Newton step), done
     // once per ray instead of in every root division (div_by_a).
@@ -553,18 +538,7 @@ __device__ __forceinline__ bool trav_node(const Node *__restrict__ nodes, Stack 
     float tn0 = 0.0f, tn1 = 0.0f;
     bool h0, h1;
     uint32_t l0, l1;
-    if constexpr (std::is_same<Node, GNode>::value && RRT_NODE96) {
-        // the 112-B LDS node: axis a at 32a holds (lo0, hi0, lo1, hi1, hi0, lo0, hi1, lo1), so one
-        // 16-B read at the ray's sign offset gives both children's (entry, exit) pairs; links at 96
-        const char *bx = reinterpret_cast<const char *>(nodes) + __umul24((uint32_t)t.node, 112u);
-        auto quad = [&](uint32_t byte_off) { return *reinterpret_cast<const float4 *>(bx + byte_off); };
-        const float4 x = quad(rk.ox), y = quad(rk.oy), z = quad(rk.oz);
-        h0 = box_hit_ordered(x.x, x.y, y.x, y.y, z.x, z.y, rk.inv, rk.oi, 0.001f, t.closest, tn0);
-        h1 = box_hit_ordered(x.z, x.w, y.z, y.w, z.z, z.w, rk.inv, rk.oi, 0.001f, t.closest, tn1);
-        const uint2 lk = *reinterpret_cast<const uint2 *>(bx + 96);
-        l0 = lk.x;
-        l1 = lk.y;
-    } else if constexpr (std::is_same<Node, GNode>::value) {
+    if constexpr (std::is_same<Node, GNode>::value) {
         // node * 80 as a 24-bit multiply (full rate; node indices < 2^24)
         const GNode &n = *reinterpret_cast<const GNode *>(reinterpret_cast<const char *>(nodes) +
                                                            __umul24((uint32_t)t.node, (uint32_t)sizeof(GNode)));
@@ -1232,30 +1206,7 @@ __device__ __forceinline__ void render_body(const KParams &P) {
     const float4 *prims = P.prim_cr;
     const GMaterial *mtl = P.prim_mtl;
     const float4 *motion = P.prim_motion;
-    constexpr bool kNode96 = RRT_NODE96 && kLds && !kWide && kBook2 <= 0;
-    if constexpr (kNode96) {
-        // Stage the BVH as 112-B nodes ((lo, hi, hi, lo) per axis, links at 96) + the spheres; the
-        // materials stay in global memory.
-        uint4 *dst = lds_dyn + (P.stack_depth * kBlk * sizeof(StackT) + 15u) / 16u;
-        const GNode *src_n = reinterpret_cast<const GNode *>(P.nodes);
-        for (uint32_t i = threadIdx.x; i < P.n_nodes; i += kBlk) {
-            const GNode g = src_n[i];
-            uint4 *o = dst + 7u * i;
-            for (int a = 0; a < 3; ++a) {
-                const uint32_t lo0 = __float_as_uint(g.box[0][3 * a]), hi0 = __float_as_uint(g.box[0][3 * a + 1]);
-                const uint32_t lo1 = __float_as_uint(g.box[1][3 * a]), hi1 = __float_as_uint(g.box[1][3 * a + 1]);
-                o[2 * a] = make_uint4(lo0, hi0, lo1, hi1);
-                o[2 * a + 1] = make_uint4(hi0, lo0, hi1, lo1);
-            }
-            o[6] = make_uint4(g.link[0], g.link[1], 0u, 0u);
-        }
-        const uint32_t nn = 7u * P.n_nodes;
-        const uint4 *src_p = reinterpret_cast<const uint4 *>(P.prim_cr);
-        for (uint32_t i = threadIdx.x; i < P.n_prims; i += kBlk) dst[nn + i] = src_p[i];
-        __syncthreads();
-        nodes = reinterpret_cast<const Node *>(dst);
-        prims = reinterpret_cast<const float4 *>(dst + nn);
-    } else if constexpr (kLds) {
+    if constexpr (kLds) {
         // Stage the whole BVH + spheres + their materials (KB-sized) in LDS once per block.
         uint4 *dst = lds_dyn + (P.stack_depth * kBlk * sizeof(StackT) + 15u) / 16u;
         const uint4 *src_n = reinterpret_cast<const uint4 *>(P.nodes);
@@ -1648,9 +1599,7 @@ template <bool kLds, typename StackT, bool kWide, int kBook2, int kWaves = 1, in
 hipError_t launch_variant(const KParams &p, bool count, hipStream_t stream) {
     if (p.n_units == 0) return hipSuccess;
     size_t lds = ((size_t)p.stack_depth * kBlk * sizeof(StackT) + 15u) / 16u * 16u;
-    if (RRT_NODE96 && kLds && !kWide && kBook2 <= 0)  // 112-B nodes + spheres (materials from global)
-        lds += (size_t)p.n_nodes * 112u + (size_t)p.n_prims * sizeof(float4);
-    else if (kLds)
+    if (kLds)
         lds += (size_t)p.n_nodes * (kWide ? sizeof(GNode4) : sizeof(GNode)) +  // LDS BVH2 = GNode
                (size_t)p.n_prims * (kPrimBytes + (kBook2 > 0 ? kMotionBytes : 0));
     if (kBook2 > 0 && p.perlin_in_lds) lds += (size_t)p.n_perlin * sizeof(GPerlin);
@@ -1707,17 +1656,10 @@ hipError_t launch_width(const KParams &p, bool count, hipStream_t stream) {
     }
 }
 
-#if RRT_WAVEFRONT
-#include "rrt_wavefront.inc"
-#endif
-
 }  // namespace
 
 hipError_t launch_render_pass(const KParams &p, bool count, hipStream_t stream) {
     if (p.flags & kFlagF64) return launch_render_pass_f64(p, count, stream);  // the f64 books path
-#if RRT_WAVEFRONT  // measurement variant: book-1 BVH2 scenes through the wavefront prototype
-    if (!count && !p.prim_motion && p.bvh_width == 2 && p.n_nodes <= 65535u) return launch_wavefront(p, stream);
-#endif
     // Variant choice: BVH width, smallest LDS stack that holds the traversal, and the scene
     // staged in LDS when the BVH + spheres fit the per-block budget (RTOW: ~20-26 KB).
     // Book-2 scenes (moving spheres, checker / noise textures): BVH2 only (the host builds a

@@ -31,8 +31,8 @@ VARIANTS = {
     # rrt_books64.hip: the per-ray reciprocal root division, one class for every scene, f32 nodes in
     # LDS for every LDS scene, launch shape
     "f64_knobs": ["-DRRT_F64_DIVA=0", "-DRRT_F64_CLASSES=0", "-DRRT_F64_BLOCK=256", "-DRRT_F64_WAVES=2"],
-    # the wavefront prototype (rrt_wavefront.inc): a measurement variant, DESIGN.md §5
-    "wavefront": ["-DRRT_WAVEFRONT=1"],
+    # the f64 kernel's host-formed constants and widened sphere records switched off
+    "f64_host": ["-DRRT_F64_CAM64=0", "-DRRT_F64_HOST_INVR=0", "-DRRT_F64_WIDE_SPHERES=0"],
 }
 
 
