@@ -377,14 +377,21 @@ __device__ __forceinline__ double div_a64(double n, double a, double ra) {
 }
 
 // A sphere record widened to f64 while the block stages the scene in LDS (kF64LdsWide): center and
-// radius converted once (exact) instead of four f32 -> f64 conversions per sphere test.
+// r * r formed once instead of four f32 -> f64 conversions and a product per sphere test. The f32
+// radius squared is exact in f64 (48 significant bits), so r2 is the reference's r * r, and
+// sqrt(r2) its r again (a correctly rounded root of an exact square).
+#ifndef RRT_F64_R2
+#define RRT_F64_R2 1
+#endif
 struct alignas(16) Sphere64 {
-    double cx, cy, cz, r;
+    double cx, cy, cz, r2;  // r2 = r * r (RRT_F64_R2) or r
 };
 __device__ __forceinline__ D3 center_of(const float4 &c) { return f2d(c.x, c.y, c.z); }
 __device__ __forceinline__ D3 center_of(const Sphere64 &c) { return d3(c.cx, c.cy, c.cz); }
 __device__ __forceinline__ double radius_of(const float4 &c) { return (double)c.w; }
-__device__ __forceinline__ double radius_of(const Sphere64 &c) { return c.r; }
+__device__ __forceinline__ double radius_of(const Sphere64 &c) { return RRT_F64_R2 ? __builtin_sqrt(c.r2) : c.r2; }
+__device__ __forceinline__ double radius_sq_of(const float4 &c) { return (double)c.w * (double)c.w; }
+__device__ __forceinline__ double radius_sq_of(const Sphere64 &c) { return RRT_F64_R2 ? c.r2 : c.r2 * c.r2; }
 
 template <bool kCount, typename Rec>
 __device__ __forceinline__ void leaves64(const Rec *__restrict__ prims, Leaves lv, D3 o, D3 d, double a, Trav64 &t,
@@ -396,8 +403,7 @@ __device__ __forceinline__ void leaves64(const Rec *__restrict__ prims, Leaves l
         const Rec cr = prims[i];
         const D3 oc = sub(center_of(cr), o);
         const double h = dot(d, oc);
-        const double r = radius_of(cr);
-        const double c = dot(oc, oc) - r * r;
+        const double c = dot(oc, oc) - radius_sq_of(cr);
         const double disc = h * h - a * c;
         if (disc < 0.0) continue;
         const double sq = __builtin_sqrt(disc);
@@ -576,7 +582,8 @@ __device__ __forceinline__ void render64_body(const KParams &P) {
         for (uint32_t i = threadIdx.x; i < P.n_prims; i += kBlk) {
             const float4 c = P.prim_cr[i];
             if constexpr (kMode == kF64LdsWide)
-                reinterpret_cast<Sphere64 *>(dst + nn)[i] = Sphere64{(double)c.x, (double)c.y, (double)c.z, (double)c.w};
+                reinterpret_cast<Sphere64 *>(dst + nn)[i] = Sphere64{(double)c.x, (double)c.y, (double)c.z,
+                                                                         RRT_F64_R2 ? (double)c.w * (double)c.w : (double)c.w};
             else
                 reinterpret_cast<float4 *>(dst + nn)[i] = c;
         }
@@ -798,6 +805,19 @@ size_t lds64_bytes(const KParams &p, int mode) {
     return lds;
 }
 
+}  // namespace
+
+size_t f64_lds_min_bytes(uint32_t n_nodes, uint32_t n_prims, uint32_t stack_depth) {
+    KParams p{};
+    p.n_nodes = n_nodes;
+    p.n_prims = n_prims;
+    p.stack_depth = stack_depth;
+    p.inv_r_in_lds = 0u;
+    return lds64_bytes(p, kF64Lds);
+}
+
+namespace {
+
 template <int kMode, int kClass>
 hipError_t launch64(const KParams &p, bool count, hipStream_t stream) {
     const size_t lds = lds64_bytes(p, kMode);
@@ -824,9 +844,15 @@ hipError_t launch64_placed(const KParams &p, bool count, hipStream_t stream) {
     if (!p.scene_in_lds) return launch64<kF64Global, kClass>(p, count, stream);
     // the widened sphere records and the 1/r table join the staged scene while the block stays
     // within the 64 KB it may declare
+    // (widened records before the 1/r table: a sphere test reads a record, a hit reads 1/r)
     KParams q = p;
+    if (RRT_F64_WIDE_SPHERES) {
+        for (const uint32_t inv_r : {1u, 0u}) {
+            q.inv_r_in_lds = inv_r;
+            if (lds64_bytes(q, kF64LdsWide) <= 64u * 1024u) return launch64<kF64LdsWide, kClass>(q, count, stream);
+        }
+    }
     q.inv_r_in_lds = 1u;
-    if (RRT_F64_WIDE_SPHERES && lds64_bytes(q, kF64LdsWide) <= 64u * 1024u) return launch64<kF64LdsWide, kClass>(q, count, stream);
     if (lds64_bytes(q, kF64Lds) > 64u * 1024u) q.inv_r_in_lds = 0u;
     return launch64<kF64Lds, kClass>(q, count, stream);
 }

@@ -174,7 +174,7 @@ struct Builder {
     // node_cost 2 (a node visit ~ two sphere tests in this kernel) measured best: C2 +3.5 %
     // over the bvh.rs criterion, and the RTOW tree (203 nodes) still fits the LDS budget.
     bool sweep = true;
-    double node_cost = 2.0;
+    double node_cost = 2.0;  // kNodeCost (f32 kernel) or f64_node_cost() (f64 kernel), set by build_bvh
 
     // Binary SAH tree (bvh.rs:16-156 split choice), leaves of <= max_leaf spheres.
     struct BNode {
@@ -590,6 +590,20 @@ FlatBvh flatten4(const Builder &bd, int32_t root) {
 }
 
 
+// The SAH's node visit price in sphere tests (Builder::node_cost). The f32 kernel's is 2. The f64
+// kernel tests boxes in f32 and spheres in f64, so its node visit is cheaper in sphere tests, more
+// so when the nodes come from L2 as 32-B f16 records than from LDS: 1.5 for a scene it stages in
+// LDS (C2 f64 +3.2 % same-box against 2; lower prices grow the tree past the block's 64 KB), 0.5
+// for one it reads from global memory (C5 f64 +3.9 %; profiles/r4l_f64_sah_sweep.log, r4m_f64_sah_sweep.log: 1.4 / 1.6 and 0.25 / 0.75 within 0.3 %).
+// RRT_F64_SAH_CT_LDS / RRT_F64_SAH_CT_GLOBAL: experiments.
+constexpr double kNodeCost = 2.0;
+double env_or(const char *name, double v) {
+    const char *e = std::getenv(name);
+    return e ? std::atof(e) : v;
+}
+double f64_node_cost_lds() { return env_or("RRT_F64_SAH_CT_LDS", 1.5); }
+double f64_node_cost_global() { return env_or("RRT_F64_SAH_CT_GLOBAL", 0.5); }
+
 // Default BVH shape of scene creation (env knobs are for experiments).
 void bvh_defaults(uint32_t &width, uint32_t &max_leaf) {
     max_leaf = 3;
@@ -639,9 +653,12 @@ struct ExtView {
 // primitive in leaf order. The medium ranges are validated by the caller.
 // Whether nodes + primitive records (+ motion for book-2 kernels) are staged in LDS per block
 // (RRT_SCENE_IN_LDS=0 forces global memory).
+bool scene_lds_forced_off() {
+    const char *e = std::getenv("RRT_SCENE_IN_LDS");
+    return e && std::atoi(e) == 0;
+}
 bool scene_lds_fit(size_t node_bytes, size_t n_prims, bool book2) {
-    if (const char *e = std::getenv("RRT_SCENE_IN_LDS"))
-        if (std::atoi(e) == 0) return false;
+    if (scene_lds_forced_off()) return false;
     return node_bytes + n_prims * (rrt::kPrimBytes + (book2 ? rrt::kMotionBytes : 0)) <= rrt::kLdsSceneBudget;
 }
 
@@ -692,10 +709,12 @@ std::vector<uint32_t> unbounded_media(const RrtSphere *spheres, uint32_t n_spher
     return out;
 }
 
-// BVH2 node layout: the sign-ordered 80-B nodes when `lds_fit(bytes of those nodes)` says the
-// scene will be staged in LDS, else the 32-B f16 global-memory nodes.
+// BVH2 node layout: the sign-ordered 80-B nodes when `lds_fit(the tree in those nodes)` says the
+// scene will be staged in LDS, else the 32-B f16 global-memory nodes. node_cost: the SAH's node
+// visit price in sphere tests (Builder::node_cost).
 FlatBvh build_bvh(const RrtSphere *spheres, uint32_t n_spheres, const ExtView &ex, uint32_t width,
-                  uint32_t max_leaf, std::vector<uint32_t> &order, const std::function<bool(size_t)> &lds_fit) {
+                  uint32_t max_leaf, double node_cost, std::vector<uint32_t> &order,
+                  const std::function<bool(const FlatBvh &)> &lds_fit) {
     const float *motion = ex.motion;
     const uint32_t n_quads = ex.n_quads;
     std::vector<Aabb> boxes(n_spheres + (size_t)n_quads + ex.n_media);
@@ -731,6 +750,7 @@ FlatBvh build_bvh(const RrtSphere *spheres, uint32_t n_spheres, const ExtView &e
     for (uint32_t m : unb) bld.objs.erase(std::find(bld.objs.begin(), bld.objs.end(), n_spheres + n_quads + m));
     const uint32_t n_tree = (uint32_t)bld.objs.size();
     if (const char *e = std::getenv("RRT_BVH_SPLIT")) bld.sweep = std::strcmp(e, "binned") != 0;
+    bld.node_cost = node_cost;
     if (const char *e = std::getenv("RRT_SAH_CT")) bld.node_cost = std::atof(e);
     FlatBvh fb;
     if (n_tree == 0) {  // root with never-hit children
@@ -745,7 +765,7 @@ FlatBvh build_bvh(const RrtSphere *spheres, uint32_t n_spheres, const ExtView &e
         fb = flatten4(bld, root);
     } else {
         fb = flatten2<rrt::GNode>(bld, root);
-        if (!lds_fit(fb.bytes.size())) fb = flatten2<rrt::GNodeH>(bld, root);
+        if (!lds_fit(fb)) fb = flatten2<rrt::GNodeH>(bld, root);
     }
     order = bld.objs;
     for (uint32_t m : unb) order.push_back(n_spheres + n_quads + m);
@@ -1041,8 +1061,25 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
         return fail(RRT_E_INVALID, ">= 2^24 primitives or quads");
     if (!has_motion) ex.motion = nullptr;
     const size_t n_prims_all = (size_t)n_spheres + n_quads + n_media;
-    const FlatBvh fb = build_bvh(spheres, n_spheres, ex, width, max_leaf, order,
-                                 [&](size_t nb) { return scene_lds_fit(nb, n_prims_all, book2); });
+    // The f64 kernel: its own SAH node prices (f64_node_cost_*) and its own LDS budget (Node112
+    // nodes, the stack of its 512-thread block). A tree that does not fit the block is rebuilt at
+    // the global-memory price, and at the f32 price if that one needs more nodes than the f64
+    // kernel's 16-bit links and stack address.
+    auto f64_fit = [&](const FlatBvh &t) {
+        return !scene_lds_forced_off() &&
+               rrt::f64_lds_min_bytes(t.n_nodes, (uint32_t)n_prims_all, t.stack_need) <= 64u * 1024u;
+    };
+    FlatBvh fb;
+    if (!f64) {
+        fb = build_bvh(spheres, n_spheres, ex, width, max_leaf, kNodeCost, order,
+                       [&](const FlatBvh &t) { return scene_lds_fit(t.bytes.size(), n_prims_all, book2); });
+    } else {
+        fb = build_bvh(spheres, n_spheres, ex, width, max_leaf, f64_node_cost_lds(), order, f64_fit);
+        if (fb.stride != (uint32_t)sizeof(rrt::GNode)) {
+            fb = build_bvh(spheres, n_spheres, ex, width, max_leaf, f64_node_cost_global(), order, f64_fit);
+            if (fb.n_nodes > 65535u) fb = build_bvh(spheres, n_spheres, ex, width, max_leaf, kNodeCost, order, f64_fit);
+        }
+    }
     if (fb.stack_need > (uint32_t)rrt::kMaxStackDepth)
         return fail(RRT_E_INVALID, "BVH depth " + std::to_string(fb.max_depth) + " exceeds the LDS stack");
     if (f64 && fb.n_nodes > 65535u) return fail(RRT_E_INVALID, "RRT_FLAG_F64: more than 65535 BVH nodes");
@@ -1350,8 +1387,8 @@ int32_t rrt_build_bvh_ex(const RrtSphere *spheres, uint32_t n_spheres, const Rrt
     // layout holds the same tree and boxes, so a checker walks the same decisions)
     const bool book2 = ex.motion || ex.n_quads || ex.n_media;
     const size_t n_prims_all = (size_t)n_spheres + ex.n_quads + ex.n_media;
-    const FlatBvh fb = build_bvh(spheres, n_spheres, ex, width, max_leaf, order,
-                                 [&](size_t nb) { return scene_lds_fit(nb, n_prims_all, book2); });
+    const FlatBvh fb = build_bvh(spheres, n_spheres, ex, width, max_leaf, kNodeCost, order,
+                                 [&](const FlatBvh &t) { return scene_lds_fit(t.bytes.size(), n_prims_all, book2); });
     if (info) {
         *info = RrtBvhInfo{};
         info->n_nodes = fb.n_nodes;

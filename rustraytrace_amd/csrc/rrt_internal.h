@@ -285,6 +285,9 @@ hipError_t launch_quantize(const float *d_accum, uint8_t *d_rgb8, uint32_t n_pix
 // Implemented in rrt_books64.hip: one sample pass of the f64 books kernel (+ its chunk combine)
 // into p.accum64, and the f64 sums rounded to the f32 RGBA accum of the ABI.
 hipError_t launch_render_pass_f64(const KParams &p, bool count, hipStream_t stream);
+// LDS of the f64 kernel's block with the scene staged in its smallest form (Node112 nodes, f32
+// sphere records, no 1/r table): the host stages an f64 scene only when this is <= 64 KB
+size_t f64_lds_min_bytes(uint32_t n_nodes, uint32_t n_prims, uint32_t stack_depth);
 hipError_t launch_accum64_to_f32(const D4 *d_accum64, float4 *d_accum, uint32_t n_pixels, hipStream_t stream);
 
 }  // namespace rrt

@@ -2,6 +2,7 @@
 # Build experimental librrt_hip variants into variants/<name>/.
 #   BxW            block size x launch-bounds waves, e.g. 512x6
 #   name:FLAGS     arbitrary extra compile flags, e.g. "pt1:-DRRT_PHASE_TIMING=1"
+# F64_FLAGS (env) goes to the f64 kernel object only.
 cd "$(dirname "$0")/.."
 mkdir -p variants
 for cfg in "$@"; do
@@ -13,5 +14,5 @@ for cfg in "$@"; do
   fi
   out=variants/$name
   rm -rf $out && mkdir -p $out
-  make -s -C rustraytrace_amd/csrc OUT=../../$out CXXFLAGS_EXTRA="$flags" ../../$out/librrt_hip.so || exit 1
+  make -s -C rustraytrace_amd/csrc OUT=../../$out CXXFLAGS_EXTRA="$flags" F64_FLAGS="${F64_FLAGS:-}" ../../$out/librrt_hip.so || exit 1
 done
