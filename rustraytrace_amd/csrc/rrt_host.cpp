@@ -590,19 +590,24 @@ FlatBvh flatten4(const Builder &bd, int32_t root) {
 }
 
 
-// The SAH's node visit price in sphere tests (Builder::node_cost). The f32 kernel's is 2. The f64
-// kernel tests boxes in f32 and spheres in f64, so its node visit is cheaper in sphere tests, more
-// so when the nodes come from L2 as 32-B f16 records than from LDS: 1.5 for a scene it stages in
-// LDS (C2 f64 +3.2 % same-box against 2; lower prices grow the tree past the block's 64 KB), 0.5
-// for one it reads from global memory (C5 f64 +3.9 %; profiles/r4l_f64_sah_sweep.log, r4m_f64_sah_sweep.log: 1.4 / 1.6 and 0.25 / 0.75 within 0.3 %).
-// RRT_F64_SAH_CT_LDS / RRT_F64_SAH_CT_GLOBAL: experiments.
+// The BVH's shape by kernel and node placement (scene_bvh). A scene staged in LDS is built with
+// leaves of up to max_leaf (3) primitives at the SAH node price (Builder::node_cost, in sphere
+// tests) of the kernel: 2 for the f32 kernel (a node visit ~ two sphere tests there), 1.5 for the
+// f64 kernel, which tests boxes in f32 and spheres in f64 (C2 f64 +3.2 % same-box against 2; lower
+// prices grow the tree past its block's 64 KB; profiles/r4l_f64_sah_sweep.log, r4m_f64_sah_sweep.log).
+// A scene read from L2 — 32-B f16 nodes, primitive records gathered per lane — is split down to
+// single-primitive leaves (the price is moot there): a node visit is two 16-B loads, a primitive
+// test at least as many plus its arithmetic, and book-2 primitives cost more than a sphere test.
+// Same-box against the price-2, 3-primitive tree: final_scene 9.86 -> 11.0 Grays/s, bouncing
+// spheres +3.1 %, C5 +0.7 %, C5 f64 +3.7 % (profiles/r4n_*, r4o_leaf_sweep.log).
+// RRT_SAH_CT (every build), RRT_F64_SAH_CT_LDS, RRT_MAX_LEAF_GLOBAL: experiments.
 constexpr double kNodeCost = 2.0;
 double env_or(const char *name, double v) {
     const char *e = std::getenv(name);
     return e ? std::atof(e) : v;
 }
 double f64_node_cost_lds() { return env_or("RRT_F64_SAH_CT_LDS", 1.5); }
-double f64_node_cost_global() { return env_or("RRT_F64_SAH_CT_GLOBAL", 0.5); }
+uint32_t max_leaf_global() { return (uint32_t)std::max(1.0, env_or("RRT_MAX_LEAF_GLOBAL", 1)); }
 
 // Default BVH shape of scene creation (env knobs are for experiments).
 void bvh_defaults(uint32_t &width, uint32_t &max_leaf) {
@@ -770,6 +775,29 @@ FlatBvh build_bvh(const RrtSphere *spheres, uint32_t n_spheres, const ExtView &e
     order = bld.objs;
     for (uint32_t m : unb) order.push_back(n_spheres + n_quads + m);
     fb.n_unbounded = (uint32_t)unb.size();
+    return fb;
+}
+
+// The scene's BVH2 (the shapes above): first the LDS shape, kept when the kernel's LDS fit takes
+// its sign-ordered nodes; else the global-memory shape in f16 nodes, and for the f64 kernel the LDS
+// shape in f16 nodes if the global one needs more nodes than its 16-bit links and stack address.
+// Width 4 (an experiment) keeps the f32 LDS shape.
+FlatBvh scene_bvh(const RrtSphere *spheres, uint32_t n_spheres, const ExtView &ex, uint32_t width,
+                  uint32_t max_leaf, bool book2, bool f64, std::vector<uint32_t> &order) {
+    const size_t n_prims_all = (size_t)n_spheres + ex.n_quads + ex.n_media;
+    std::function<bool(const FlatBvh &)> fit = [&](const FlatBvh &t) {
+        return scene_lds_fit(t.bytes.size(), n_prims_all, book2);
+    };
+    if (f64)
+        fit = [&](const FlatBvh &t) {
+            return !scene_lds_forced_off() &&
+                   rrt::f64_lds_min_bytes(t.n_nodes, (uint32_t)n_prims_all, t.stack_need) <= 64u * 1024u;
+        };
+    if (width != 2) return build_bvh(spheres, n_spheres, ex, width, max_leaf, kNodeCost, order, fit);
+    FlatBvh fb = build_bvh(spheres, n_spheres, ex, width, max_leaf, f64 ? f64_node_cost_lds() : kNodeCost, order, fit);
+    if (fb.stride == (uint32_t)sizeof(rrt::GNode)) return fb;
+    fb = build_bvh(spheres, n_spheres, ex, width, std::min(max_leaf, max_leaf_global()), kNodeCost, order, fit);
+    if (f64 && fb.n_nodes > 65535u) fb = build_bvh(spheres, n_spheres, ex, width, max_leaf, kNodeCost, order, fit);
     return fb;
 }
 
@@ -1060,26 +1088,7 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
         (uint64_t)n_quads + ex.n_bquads + ex.n_lights >= (1u << 24))
         return fail(RRT_E_INVALID, ">= 2^24 primitives or quads");
     if (!has_motion) ex.motion = nullptr;
-    const size_t n_prims_all = (size_t)n_spheres + n_quads + n_media;
-    // The f64 kernel: its own SAH node prices (f64_node_cost_*) and its own LDS budget (Node112
-    // nodes, the stack of its 512-thread block). A tree that does not fit the block is rebuilt at
-    // the global-memory price, and at the f32 price if that one needs more nodes than the f64
-    // kernel's 16-bit links and stack address.
-    auto f64_fit = [&](const FlatBvh &t) {
-        return !scene_lds_forced_off() &&
-               rrt::f64_lds_min_bytes(t.n_nodes, (uint32_t)n_prims_all, t.stack_need) <= 64u * 1024u;
-    };
-    FlatBvh fb;
-    if (!f64) {
-        fb = build_bvh(spheres, n_spheres, ex, width, max_leaf, kNodeCost, order,
-                       [&](const FlatBvh &t) { return scene_lds_fit(t.bytes.size(), n_prims_all, book2); });
-    } else {
-        fb = build_bvh(spheres, n_spheres, ex, width, max_leaf, f64_node_cost_lds(), order, f64_fit);
-        if (fb.stride != (uint32_t)sizeof(rrt::GNode)) {
-            fb = build_bvh(spheres, n_spheres, ex, width, max_leaf, f64_node_cost_global(), order, f64_fit);
-            if (fb.n_nodes > 65535u) fb = build_bvh(spheres, n_spheres, ex, width, max_leaf, kNodeCost, order, f64_fit);
-        }
-    }
+    const FlatBvh fb = scene_bvh(spheres, n_spheres, ex, width, max_leaf, book2, f64, order);
     if (fb.stack_need > (uint32_t)rrt::kMaxStackDepth)
         return fail(RRT_E_INVALID, "BVH depth " + std::to_string(fb.max_depth) + " exceeds the LDS stack");
     if (f64 && fb.n_nodes > 65535u) return fail(RRT_E_INVALID, "RRT_FLAG_F64: more than 65535 BVH nodes");
@@ -1383,12 +1392,11 @@ int32_t rrt_build_bvh_ex(const RrtSphere *spheres, uint32_t n_spheres, const Rrt
     if ((width != 2 && width != 4) || max_leaf > (width == 2 ? rrt::kMaxLeafPrims : 15u))
         return fail(RRT_E_INVALID, "width must be 2 or 4, max_leaf <= 7 (width 2) or 15 (width 4)");
     std::vector<uint32_t> order;
-    // the layout scene creation would pick (its book-2 test also counts book-2 materials; either
-    // layout holds the same tree and boxes, so a checker walks the same decisions)
+    // the tree and layout scene creation would pick (scene_bvh), except that scene creation's
+    // book-2 test also counts book-2 materials, whose motion bytes can tip the LDS fit of a scene
+    // with such materials and no book-2 geometry (then the node price and the tree differ too)
     const bool book2 = ex.motion || ex.n_quads || ex.n_media;
-    const size_t n_prims_all = (size_t)n_spheres + ex.n_quads + ex.n_media;
-    const FlatBvh fb = build_bvh(spheres, n_spheres, ex, width, max_leaf, kNodeCost, order,
-                                 [&](const FlatBvh &t) { return scene_lds_fit(t.bytes.size(), n_prims_all, book2); });
+    const FlatBvh fb = scene_bvh(spheres, n_spheres, ex, width, max_leaf, book2, false, order);
     if (info) {
         *info = RrtBvhInfo{};
         info->n_nodes = fb.n_nodes;

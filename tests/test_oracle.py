@@ -420,9 +420,11 @@ def test_axis_parallel_rays_hit_through_straddling_boxes():
 
 
 def test_bvh2_node_layouts_hold_the_same_tree(monkeypatch):
-    """RTOW fits the LDS budget: 80-B sign-ordered nodes; C5's 10k spheres do not: 32-B f16 nodes.
-    Forcing global memory on RTOW gives the 32-B layout of the same tree: same links, and every f16
-    box holds its f32 box (rounded outward, no subnormal planes); a never-hit child stays never-hit."""
+    """RTOW fits the LDS budget: 80-B sign-ordered nodes; C5's 10k spheres do not: 32-B f16 nodes,
+    in the global-memory shape (rrt_host.cpp scene_bvh: single-primitive leaves). Forcing global
+    memory on RTOW with the LDS shape's leaves (RRT_MAX_LEAF_GLOBAL=3) gives the 32-B layout of the
+    same tree: same links, and every f16 box holds its f32 box (rounded outward, no subnormal
+    planes); a never-hit child stays never-hit."""
     from rustraytrace_amd.render import build_bvh, decode_bvh2
 
     sc = rrt.rtow(image_width=32, samples_per_pixel=2)
@@ -431,6 +433,8 @@ def test_bvh2_node_layouts_hold_the_same_tree(monkeypatch):
     c5 = rrt.config_scene("C5", image_width=32, samples_per_pixel=2)
     assert build_bvh(c5)[2]["node_stride"] == 32
     monkeypatch.setenv("RRT_SCENE_IN_LDS", "0")
+    assert build_bvh(sc)[2]["max_leaf_size"] == 1 and info["max_leaf_size"] == 3  # the global shape
+    monkeypatch.setenv("RRT_MAX_LEAF_GLOBAL", "3")
     nodes_g, order_g, info_g = build_bvh(sc)
     assert info_g["node_stride"] == 32 and nodes_g.size == 32 * info_g["n_nodes"] and np.array_equal(order, order_g)
     lo, hi, first, count = decode_bvh2(nodes, 80)
