@@ -100,10 +100,9 @@ __device__ __forceinline__ D3 refract(D3 uv, D3 n, double e) {
     const D3 par = muls(n, -__builtin_sqrt(__builtin_fabs(1.0 - dot(perp, perp))));
     return add(perp, par);
 }
-// material.rs:75-80 Schlick; powi(5) = x * ((x*x) * (x*x)) (LLVM's repeated squaring)
-__device__ __forceinline__ double reflectance(double cosine, double ri) {
-    double r0 = (1.0 - ri) / (1.0 + ri);
-    r0 = r0 * r0;
+// material.rs:75-80 Schlick at r0 = ((1 - ri) / (1 + ri))^2; powi(5) = x * ((x*x) * (x*x)) (LLVM's
+// repeated squaring)
+__device__ __forceinline__ double reflectance_r0(double cosine, double r0) {
     const double x = 1.0 - cosine;
     const double x2 = x * x;
     return r0 + (1.0 - r0) * (x * (x2 * x2));
@@ -508,12 +507,24 @@ __device__ __forceinline__ bool shade64(const KParams &P, const Rec *prims, cons
         att = albedo;
     } else if (kClass != kF64Diffuse && kind == 2) {  // Dielectric (material.rs:83-102)
         const double eta = (double)__int_as_float(m.b.y);
-        const double ri = front ? 1.0 / eta : eta;
+#ifndef RRT_F64_DIEL_HOST
+#define RRT_F64_DIEL_HOST 1
+#endif
+        double ri, r0;
+        if (RRT_F64_DIEL_HOST) {  // 1 / eta and both r0 formed on the host (rrt_host.cpp dielectric_consts64)
+            const double4 k = P.prim_diel64[prim];
+            ri = front ? k.x : eta;
+            r0 = front ? k.y : k.z;
+        } else {
+            ri = front ? 1.0 / eta : eta;
+            r0 = (1.0 - ri) / (1.0 + ri);
+            r0 = r0 * r0;
+        }
         const D3 ud = unit_vector(ps.d);
         const double c = rmin(-dot(ud, nrm), 1.0);
         const double sn = __builtin_sqrt(1.0 - c * c);
         const bool cannot = ri * sn > 1.0;
-        if (cannot || reflectance(c, ri) > rnd64(ps.rng)) dir = reflect(ud, nrm);
+        if (cannot || reflectance_r0(c, r0) > rnd64(ps.rng)) dir = reflect(ud, nrm);
         else dir = refract(ud, nrm, ri);
         att = d3(1.0, 1.0, 1.0);
     } else {  // Lambertian, plain or image-textured (material.rs:28-40; the_next_week/material.rs:41-53)

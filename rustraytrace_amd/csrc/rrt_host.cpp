@@ -609,6 +609,42 @@ double env_or(const char *name, double v) {
 double f64_node_cost_lds() { return env_or("RRT_F64_SAH_CT_LDS", 1.5); }
 uint32_t max_leaf_global() { return (uint32_t)std::max(1.0, env_or("RRT_MAX_LEAF_GLOBAL", 1)); }
 
+// A dielectric's scatter (material.rs:83-102) divides twice per hit in f32: ri = 1 / eta on a
+// front face, and Schlick's r0 = (1 - ri) / (1 + ri) squared (material.rs:75-80). Both depend on
+// the material and the face only, so the host forms them once, in the same correctly rounded f32
+// operations in the same order (no contraction: volatile stores round each step), into the
+// dielectric's unused albedo slots: a = (1 / eta, r0(1 / eta), r0(eta), fuzz). The f64 kernel
+// ignores them. RRT_DIEL_HOST=0: the kernel divides (A/B).
+#ifndef RRT_DIEL_HOST
+#define RRT_DIEL_HOST 1
+#endif
+void dielectric_consts(float eta, float &inv_eta, float &r0_front, float &r0_back) {
+    auto r0sq = [](float ri) {
+        volatile float num = 1.0f - ri, den = 1.0f + ri;
+        volatile float q = num / den;
+        volatile float q2 = q * q;
+        return (float)q2;
+    };
+    volatile float inv = 1.0f / eta;
+    inv_eta = inv;
+    r0_front = r0sq(inv_eta);
+    r0_back = r0sq(eta);
+}
+
+// The same constants in f64 for the f64 kernel (material.rs:88-99 in the reference's f64).
+void dielectric_consts64(double eta, double &inv_eta, double &r0_front, double &r0_back) {
+    auto r0sq = [](double ri) {
+        volatile double num = 1.0 - ri, den = 1.0 + ri;
+        volatile double q = num / den;
+        volatile double q2 = q * q;
+        return (double)q2;
+    };
+    volatile double inv = 1.0 / eta;
+    inv_eta = inv;
+    r0_front = r0sq(inv_eta);
+    r0_back = r0sq(eta);
+}
+
 // Default BVH shape of scene creation (env knobs are for experiments).
 void bvh_defaults(uint32_t &width, uint32_t &max_leaf) {
     max_leaf = 3;
@@ -810,6 +846,7 @@ struct RrtScene {
     float4 *d_prim_cr = nullptr;
     rrt::GMaterial *d_prim_mtl = nullptr;
     double *d_prim_inv_r64 = nullptr;  // f64 scenes: 1 / r per leaf-order sphere
+    double4 *d_prim_diel64 = nullptr;  // f64 scenes: dielectric constants per leaf-order sphere
     float4 *d_prim_motion = nullptr;
     rrt::GPerlin *d_perlin = nullptr;
     rrt::GQuad *d_quads = nullptr;
@@ -841,6 +878,7 @@ void free_scene(RrtScene *s) {
     (void)hipFree(s->d_prim_cr);
     (void)hipFree(s->d_prim_mtl);
     (void)hipFree(s->d_prim_inv_r64);
+    (void)hipFree(s->d_prim_diel64);
     (void)hipFree(s->d_prim_motion);
     (void)hipFree(s->d_perlin);
     (void)hipFree(s->d_quads);
@@ -1106,6 +1144,11 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
         std::memcpy(&ref_bits, &m.ref_idx, 4);
         mats[i].a = make_float4(m.albedo_fuzz[0], m.albedo_fuzz[1], m.albedo_fuzz[2], fuzz);
         mats[i].b = make_int4((int)m.kind, ref_bits, (int)m._pad[0], (int)m._pad[1]);
+        if (m.kind == RRT_MAT_DIELECTRIC && RRT_DIEL_HOST) {  // the f32 kernel's per-material constants
+            float inv_eta, r0_front, r0_back;
+            dielectric_consts(m.ref_idx, inv_eta, r0_front, r0_back);
+            mats[i].a = make_float4(inv_eta, r0_front, r0_back, fuzz);
+        }
     }
     // Spheres in BVH leaf order, each with a copy of its material record: a hit reads one
     // 32-B record at the primitive's index (no dependent material-index fetch).
@@ -1228,6 +1271,16 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
             std::vector<double> inv_r(n_prims);
             for (uint32_t i = 0; i < n_prims; ++i) inv_r[i] = 1.0 / (double)prim_cr[i].w;
             if ((rc = upload(&s->d_prim_inv_r64, inv_r.data(), inv_r.size(), "sphere 1/r"))) break;
+            std::vector<double4> diel(n_prims, make_double4(0.0, 0.0, 0.0, 0.0));
+            for (uint32_t i = 0; i < n_prims; ++i) {
+                if (prim_mtl[i].b.x != RRT_MAT_DIELECTRIC) continue;
+                float eta32;
+                std::memcpy(&eta32, &prim_mtl[i].b.y, sizeof(float));
+                double inv_eta, r0_front, r0_back;
+                dielectric_consts64((double)eta32, inv_eta, r0_front, r0_back);
+                diel[i] = make_double4(inv_eta, r0_front, r0_back, 0.0);
+            }
+            if ((rc = upload(&s->d_prim_diel64, diel.data(), diel.size(), "dielectric constants"))) break;
         }
         if (n_perlin && (rc = upload(&s->d_perlin, perlin.data(), perlin.size(), "Perlin tables"))) break;
         if (!gquads.empty() && (rc = upload(&s->d_quads, gquads.data(), gquads.size(), "quads"))) break;
@@ -1257,6 +1310,7 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
     p.prim_cr = s->d_prim_cr;
     p.prim_mtl = s->d_prim_mtl;
     p.prim_inv_r64 = s->d_prim_inv_r64;
+    p.prim_diel64 = s->d_prim_diel64;
     p.prim_motion = s->d_prim_motion;
     p.perlin = s->d_perlin;
     p.n_perlin = n_perlin;

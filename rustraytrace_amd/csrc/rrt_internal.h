@@ -232,6 +232,9 @@ struct KParams {
     // the camera block widened to f64 on the host, as camera.rs:136-180 forms it from the f32 ABI
     // values: pixel00, delta_u, delta_v, center, defocus_disk_u = u * radius, defocus_disk_v
     double cam64[6][3];
+    // per leaf-order primitive, a dielectric's (1 / eta, r0(1 / eta), r0(eta), 0) in f64, formed on
+    // the host in the reference's operations (material.rs:75-102); zeros for other materials
+    const double4 *prim_diel64;
 };
 
 // RRT_FLAG_F64 (include/rrt_hip.h): the f64 books-arithmetic kernel (rrt_books64.hip)

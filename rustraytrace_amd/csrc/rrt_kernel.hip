@@ -116,15 +116,30 @@ __device__ __forceinline__ V3 refract(V3 uv, V3 n, float e) {
     return add(perp, par);
 }
 
-// material.rs:75-80 Schlick; powi(5) expands to x*((x*x)*(x*x)).
-__device__ __forceinline__ float reflectance(float cosine, float ri) {
-    float r0 = (1.0f - ri) / (1.0f + ri);
-    r0 = r0 * r0;
+// material.rs:75-80 Schlick at a given r0 = ((1 - ri) / (1 + ri))^2; powi(5) expands to x*((x*x)*(x*x)).
+__device__ __forceinline__ float reflectance_r0(float cosine, float r0) {
     const float x = 1.0f - cosine;
     const float x2 = x * x;
     const float x4 = x2 * x2;
     const float x5 = x * x4;
     return r0 + (1.0f - r0) * x5;
+}
+
+// A dielectric hit's (ri, r0): from the material record the host formed (rrt_host.cpp
+// dielectric_consts: a = (1 / eta, r0(1 / eta), r0(eta)), the same f32 operations), or divided here
+#ifndef RRT_DIEL_HOST
+#define RRT_DIEL_HOST 1
+#endif
+__device__ __forceinline__ void dielectric_ri_r0(const GMaterial &m, bool front, float &ri, float &r0) {
+    const float eta = __int_as_float(m.b.y);
+    if (RRT_DIEL_HOST) {
+        ri = front ? m.a.x : eta;
+        r0 = front ? m.a.y : m.a.z;
+    } else {
+        ri = front ? (1.0f / eta) : eta;
+        const float q = (1.0f - ri) / (1.0f + ri);
+        r0 = q * q;
+    }
 }
 
 // ---- deterministic f32 acos / atan2 for sphere UV (sphere.rs:46-52) -------------------------
@@ -956,14 +971,14 @@ __device__ __forceinline__ bool shade(const KParams &P, const PR &prims, const G
             cnt.d0 += wave_slot();
             cnt.d1 += 1;
         }
-        const float eta = __int_as_float(m.b.y);
-        const float ri = front ? (1.0f / eta) : eta;
+        float ri, r0;
+        dielectric_ri_r0(m, front, ri, r0);
         const V3 ud = unit(ps.d);
         float c = -dot(ud, nrm);
         c = (c < 1.0f) ? c : 1.0f;
         const float sn = __builtin_sqrtf(1.0f - c * c);
         const bool cannot = ri * sn > 1.0f;
-        if (cannot || reflectance(c, ri) > rnd(ps.rng)) dir = reflect(ud, nrm);
+        if (cannot || reflectance_r0(c, r0) > rnd(ps.rng)) dir = reflect(ud, nrm);
         else dir = refract(ud, nrm, ri);
         att = v3(1.0f, 1.0f, 1.0f);
     }
@@ -1107,14 +1122,14 @@ __device__ __forceinline__ bool shade_b3(const KParams &P, const PR &prims, cons
             att = v3(m.a.x, m.a.y, m.a.z);
             // book 3 has no absorption test: the skip_pdf ray is followed whatever its direction
         } else {
-            const float eta = __int_as_float(m.b.y);
-            const float ri = front ? (1.0f / eta) : eta;
+            float ri, r0;
+            dielectric_ri_r0(m, front, ri, r0);
             const V3 ud = unit(ps.d);
             float c = -dot(ud, nrm);
             c = (c < 1.0f) ? c : 1.0f;
             const float sn = __builtin_sqrtf(1.0f - c * c);
             const bool cannot = ri * sn > 1.0f;
-            if (cannot || reflectance(c, ri) > rnd(ps.rng)) dir = reflect(ud, nrm);
+            if (cannot || reflectance_r0(c, r0) > rnd(ps.rng)) dir = reflect(ud, nrm);
             else dir = refract(ud, nrm, ri);
             att = v3(1.0f, 1.0f, 1.0f);
         }

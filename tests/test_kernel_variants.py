@@ -32,7 +32,10 @@ VARIANTS = {
     # LDS for every LDS scene, launch shape
     "f64_knobs": ["-DRRT_F64_DIVA=0", "-DRRT_F64_CLASSES=0", "-DRRT_F64_BLOCK=256", "-DRRT_F64_WAVES=2"],
     # the f64 kernel's host-formed constants and widened sphere records switched off
-    "f64_host": ["-DRRT_F64_CAM64=0", "-DRRT_F64_HOST_INVR=0", "-DRRT_F64_WIDE_SPHERES=0"],
+    "f64_host": ["-DRRT_F64_CAM64=0", "-DRRT_F64_HOST_INVR=0", "-DRRT_F64_WIDE_SPHERES=0", "-DRRT_F64_R2=0",
+                 "-DRRT_F64_DIEL_HOST=0"],
+    # the f32 kernel dividing for its dielectric constants (host-formed by default)
+    "diel_kernel": ["-DRRT_DIEL_HOST=0"],
 }
 
 
