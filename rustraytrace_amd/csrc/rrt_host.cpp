@@ -631,6 +631,23 @@ void dielectric_consts(float eta, float &inv_eta, float &r0_front, float &r0_bac
     r0_back = r0sq(eta);
 }
 
+// Russian roulette's 1 / pr (camera.rs:189-200) for an attenuation that is a material constant
+// (a plain Lambertian's or a metal's albedo): pr = max component clamped to [0.05, 0.95], then the
+// f32 quotient the kernel would form. Only the f32 book-1 kernel reads it (b.y); the f64 kernel and
+// book-2 materials keep b.y's own meaning.
+#ifndef RRT_PR_HOST
+#define RRT_PR_HOST 1
+#endif
+float rr_inv_pr(float ax, float ay, float az) {
+    float pr = ax;
+    if (ay > pr) pr = ay;
+    if (az > pr) pr = az;
+    if (pr < 0.05f) pr = 0.05f;
+    if (pr > 0.95f) pr = 0.95f;
+    volatile float q = 1.0f / pr;
+    return q;
+}
+
 // The same constants in f64 for the f64 kernel (material.rs:88-99 in the reference's f64).
 void dielectric_consts64(double eta, double &inv_eta, double &r0_front, double &r0_back) {
     auto r0sq = [](double ri) {
@@ -1144,6 +1161,10 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
         std::memcpy(&ref_bits, &m.ref_idx, 4);
         mats[i].a = make_float4(m.albedo_fuzz[0], m.albedo_fuzz[1], m.albedo_fuzz[2], fuzz);
         mats[i].b = make_int4((int)m.kind, ref_bits, (int)m._pad[0], (int)m._pad[1]);
+        if ((m.kind == RRT_MAT_LAMBERTIAN || m.kind == RRT_MAT_METAL) && RRT_PR_HOST) {
+            const float inv_pr = rr_inv_pr(m.albedo_fuzz[0], m.albedo_fuzz[1], m.albedo_fuzz[2]);
+            std::memcpy(&mats[i].b.y, &inv_pr, sizeof(float));  // ref_idx: a dielectric's only
+        }
         if (m.kind == RRT_MAT_DIELECTRIC && RRT_DIEL_HOST) {  // the f32 kernel's per-material constants
             float inv_eta, r0_front, r0_back;
             dielectric_consts(m.ref_idx, inv_eta, r0_front, r0_back);
@@ -1211,10 +1232,15 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
         prim_mtl[i] = mats[sp.material_index];
         if (book2 || f64) {  // the f64 kernel forms r * r in f64 (sphere.rs:29)
             prim_cr[i] = make_float4(sp.center_radius[0], sp.center_radius[1], sp.center_radius[2], r);
-        } else {  // book-1 kernel layout: r * r in the record (one multiply less per test), r in b.w
+        } else {  // book-1 kernel layout: r * r in the record (one multiply less per test), 1 / r in b.w
+#ifndef RRT_INVR_HOST
+#define RRT_INVR_HOST 1
+#endif
             const volatile float r2 = r * r;  // f32, rounded once like the kernel's r * r
+            const volatile float inv_r = 1.0f / r;  // the kernel's correctly rounded quotient
+            const float bw = RRT_INVR_HOST ? (float)inv_r : r;
             prim_cr[i] = make_float4(sp.center_radius[0], sp.center_radius[1], sp.center_radius[2], r2);
-            std::memcpy(&prim_mtl[i].b.w, &r, sizeof(float));
+            std::memcpy(&prim_mtl[i].b.w, &bw, sizeof(float));
         }
         if (motion) {
             const float *m = motion + 4 * (size_t)order[i];

@@ -293,7 +293,8 @@ struct Prims {
     static constexpr bool kHasQuads = kBook2 >= 2;
     static constexpr bool kHasMedia = kBook2 >= 3;
     // Book-1 scenes store r * r (f32, rounded as the test would round it) in the record's w and
-    // the radius in the material record's b.w (rrt_host.cpp): one multiply less per sphere test.
+    // 1 / r (the normal's IEEE quotient, sphere.rs:48 through vec3.rs:142-148) in the material
+    // record's b.w (rrt_host.cpp): one multiply less per sphere test, one division less per hit.
     static constexpr bool kR2 = kBook2 <= 0;
     __device__ __forceinline__ float4 at(int i) const {
         float4 m;
@@ -922,8 +923,12 @@ __device__ __forceinline__ bool shade(const KParams &P, const PR &prims, const G
             outward = v3(qn.x, qn.y, qn.z);
         }
     } else {
-        const float r = PR::kR2 ? __int_as_float(mtl[prim].b.w) : cr.w;
-        const float inv_r = 1.0f / r;
+#ifndef RRT_INVR_HOST
+#define RRT_INVR_HOST 1
+#endif
+        const float inv_r = !PR::kR2        ? 1.0f / cr.w
+                            : RRT_INVR_HOST ? __int_as_float(mtl[prim].b.w)
+                                            : 1.0f / __int_as_float(mtl[prim].b.w);
         outward = v3((p.x - cr.x) * inv_r, (p.y - cr.y) * inv_r, (p.z - cr.z) * inv_r);
     }
     const bool front = dot(ps.d, outward) < 0.0f;
@@ -989,7 +994,17 @@ __device__ __forceinline__ bool shade(const KParams &P, const PR &prims, const G
         if (pr < 0.05f) pr = 0.05f;
         if (pr > 0.95f) pr = 0.95f;
         if (rnd(ps.rng) > pr) return true;
-        ps.T = muls(mul(ps.T, att), 1.0f / pr);
+        // Book-1 scenes without image textures: a Lambertian's or a metal's att is its albedo, so
+        // 1 / pr is a material constant the host formed in the same operations (rrt_host.cpp
+        // rr_inv_pr, in the record's unused b.y); a dielectric's att is (1, 1, 1): pr = 0.95. (The
+        // textured classes divide: the select costs C4's 80-VGPR class a spill.)
+#ifndef RRT_PR_HOST
+#define RRT_PR_HOST 1
+#endif
+        float inv_pr;
+        if (RRT_PR_HOST && kBook2 == kBook1Untextured) inv_pr = kind == 2 ? 1.0f / 0.95f : __int_as_float(m.b.y);
+        else inv_pr = 1.0f / pr;
+        ps.T = muls(mul(ps.T, att), inv_pr);
     } else {
         ps.T = mul(ps.T, att);
     }
