@@ -1246,6 +1246,10 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
             const float *m = motion + 4 * (size_t)order[i];
             prim_motion[i] = make_float4(m[0], m[1], m[2], 0.0f);
         }
+        if (book2 && RRT_INVR_HOST) {  // books 2 / 3: 1 / r in the motion record's w (xyz: the motion)
+            const volatile float inv_r = 1.0f / r;
+            prim_motion[i].w = inv_r;
+        }
     }
     // Media: boundary quads follow the scene's quads in the GQuad array.
     std::vector<rrt::GMedium> gmedia(n_media);

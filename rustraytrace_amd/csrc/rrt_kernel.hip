@@ -926,9 +926,11 @@ __device__ __forceinline__ bool shade(const KParams &P, const PR &prims, const G
 #ifndef RRT_INVR_HOST
 #define RRT_INVR_HOST 1
 #endif
-        const float inv_r = !PR::kR2        ? 1.0f / cr.w
-                            : RRT_INVR_HOST ? __int_as_float(mtl[prim].b.w)
-                                            : 1.0f / __int_as_float(mtl[prim].b.w);
+        // 1 / r from the host: book 1 in the material record's b.w, books 2 / 3 in the motion
+        // record's w (a sphere's motion is xyz only)
+        const float inv_r = !RRT_INVR_HOST ? 1.0f / (PR::kR2 ? __int_as_float(mtl[prim].b.w) : cr.w)
+                            : PR::kR2      ? __int_as_float(mtl[prim].b.w)
+                                           : qn.w;
         outward = v3((p.x - cr.x) * inv_r, (p.y - cr.y) * inv_r, (p.z - cr.z) * inv_r);
     }
     const bool front = dot(ps.d, outward) < 0.0f;
@@ -1117,7 +1119,7 @@ __device__ __forceinline__ bool shade_b3(const KParams &P, const PR &prims, cons
             outward = v3(qn.x, qn.y, qn.z);
         }
     } else {
-        const float inv_r = 1.0f / cr.w;
+        const float inv_r = RRT_INVR_HOST ? qn.w : 1.0f / cr.w;  // 1 / r from the host (shade)
         outward = v3((p.x - cr.x) * inv_r, (p.y - cr.y) * inv_r, (p.z - cr.z) * inv_r);
     }
     const bool front = (cr.w < 0.0f && (int)(-cr.w) - 1 >= (int)prims.n_quads) ? true : dot(ps.d, outward) < 0.0f;
