@@ -28,7 +28,7 @@ if [[ $STEPS == *stats* ]]; then
   for c in C2 C4 C5; do
     run kstats_$c 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG}_$c -o run --output-format csv -- python3 bench.py --config $c --steps 5 --warmup 2 --no-cpu-baseline --no-breakdown --no-extra --no-f64
     cp gpurun_out/prof_${TAG}_$c/run_kernel_stats.csv gpurun_out/profiles/${TAG}_${c}_kernel_stats.csv
-    tail -n 1 gpurun_out/kstats_$c.log > gpurun_out/profiles/${TAG}_${c}_kstats_bench.json
+    grep '^{"metric"' gpurun_out/kstats_$c.log | tail -n 1 > gpurun_out/profiles/${TAG}_${c}_kstats_bench.json
   done
 fi
 for spec in ${CONFIGS:-C2:512 C4:1024 C5:256 NW9:64:1080}; do
