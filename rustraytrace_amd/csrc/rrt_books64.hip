@@ -237,13 +237,27 @@ __device__ double rrt_atan2_64(double y, double x) {
     }
 }
 
+// x / c for the constant divisors 2 pi and pi (rrt_kernel.hip div_by_const in f64): q = x RN(1/c)
+// and Markstein's fma correction, the IEEE quotient away from underflow (8e8 random f64 arguments
+// in [2^-60, 8) against the CPU's division, tests/test_div_const.py); phi and theta are 0 or
+// far above it. RRT_DIV_CONST=0: the IEEE division.
+#ifndef RRT_DIV_CONST
+#define RRT_DIV_CONST 1
+#endif
+__device__ __forceinline__ double div_by_const64(double x, double c) {
+    if (!RRT_DIV_CONST) return x / c;
+    const double rc = 1.0 / c;  // folded: RN(1/c)
+    const double q = x * rc;
+    return __builtin_fma(__builtin_fma(-q, c, x), rc, q);
+}
+
 // ImageTexture::value (texture.rs:89-109) at get_sphere_uv(outward) (the_next_week/sphere.rs:46-52):
 // theta = acos(-y), phi = atan2(-z, x) + pi, u = phi / (2 pi), v = theta / pi.
 __device__ __forceinline__ D3 texel64(const KParams &P, int tex, D3 outward) {
     const double theta = rrt_acos64(-outward.y);
     const double phi = rrt_atan2_64(-outward.z, outward.x) + kPiD;
-    double u = phi / (2.0 * kPiD);
-    double v = theta / kPiD;
+    double u = div_by_const64(phi, 2.0 * kPiD);
+    double v = div_by_const64(theta, kPiD);
     const GTexture t = P.texs[tex];
     if (t.height <= 0) return d3(0.0, 1.0, 1.0);              // texture.rs:91-93
     u = u < 0.0 ? 0.0 : (u > 1.0 ? 1.0 : u);                   // Interval::clamp

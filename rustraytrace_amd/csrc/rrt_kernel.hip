@@ -147,6 +147,21 @@ __device__ __forceinline__ void dielectric_ri_r0(const GMaterial &m, bool front,
 constexpr float kPi = 3.14159265358979323846f;
 constexpr float kPiO2 = 1.57079632679489661923f;
 constexpr float kPiO4 = 0.78539816339744830962f;
+// x / c for the texture coordinates' constant divisors (2 pi, pi; the_next_week/sphere.rs:50-51):
+// q = x RN(1/c), then one fma correction of the remainder (Markstein's step), three instructions
+// against the IEEE expansion's ten. It returns the IEEE quotient for x = 0 and every f32 x in
+// [2^-100, 8] (exhaustive for both divisors, tests/test_div_const.py; over all positive floats the
+// only differences lie below 3.1e-32, where the remainder underflows); phi is 0 or >= 2^-22
+// (atan2 + pi), theta 0 or >= 3e-4 (acos). RRT_DIV_CONST=0: the IEEE division.
+#ifndef RRT_DIV_CONST
+#define RRT_DIV_CONST 1
+#endif
+__device__ __forceinline__ float div_by_const(float x, float c) {
+    if (!RRT_DIV_CONST) return x / c;
+    const float rc = 1.0f / c;  // folded: RN(1/c)
+    const float q = x * rc;
+    return __builtin_fmaf(__builtin_fmaf(-q, c, x), rc, q);
+}
 
 __device__ __forceinline__ float asin_core(float x) {  // |x| <= 0.5 polynomial, z = x*x
     const float z = x * x;
@@ -956,7 +971,7 @@ __device__ __forceinline__ bool shade(const KParams &P, const PR &prims, const G
         if (kBook2 != kBook1Untextured && kind == 3) {  // ImageTexture at the sphere's (u, v) (sphere.rs:46-52)
             const float theta = rrt_acosf(-outward.y);
             const float phi = rrt_atan2f(-outward.z, outward.x) + kPi;
-            att = texel(P, m.b.z, phi / (2.0f * kPi), theta / kPi);
+            att = texel(P, m.b.z, div_by_const(phi, 2.0f * kPi), div_by_const(theta, kPi));
         } else if (kBook2 > 0 && kind == 5) {  // CheckerTexture at p
             att = checker_even(m.a.w, p) ? v3(m.a.x, m.a.y, m.a.z)
                                          : v3(__int_as_float(m.b.y), __int_as_float(m.b.z), __int_as_float(m.b.w));
@@ -1171,7 +1186,7 @@ __device__ __forceinline__ bool shade_b3(const KParams &P, const PR &prims, cons
     if (kind == 3) {
         const float theta = rrt_acosf(-outward.y);
         const float phi = rrt_atan2f(-outward.z, outward.x) + kPi;
-        att = texel(P, m.b.z, phi / (2.0f * kPi), theta / kPi);
+        att = texel(P, m.b.z, div_by_const(phi, 2.0f * kPi), div_by_const(theta, kPi));
     } else if (kind == 5) {
         att = checker_even(m.a.w, p) ? v3(m.a.x, m.a.y, m.a.z)
                                      : v3(__int_as_float(m.b.y), __int_as_float(m.b.z), __int_as_float(m.b.w));
