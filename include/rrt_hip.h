@@ -550,6 +550,12 @@ int32_t rrt_device_count(int32_t *count);
  * library: without it n_gpus must not exceed the visible devices. Process-wide. */
 void rrt_testing_device_wrap(int32_t on);
 
+/* Test support, not part of the drop-in: runs the f32 kernel's short reciprocal (v_rcp_f32 + one
+ * fma Newton step) over every f32 bit pattern against the IEEE quotient; mismatches (2 x u64): [0] = patterns
+ * with |s| in [2^-126, 2^126), +-0, +-inf or NaN whose reciprocal differs, mismatches[1] = patterns
+ * with |s| < 2^126 or NaN whose clamped ray slope differs (tests/test_gpu_recip.py: both 0). */
+int32_t rrt_testing_recip_check(uint64_t *mismatches);
+
 #ifdef __cplusplus
 }
 #endif

@@ -78,8 +78,24 @@ __device__ __forceinline__ V3 cross(V3 a, V3 b) {  // vec3.rs cross
     return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }
 // vec3.rs:168-170 unit_vector = v * (1/len)  (Div<f64> is `(1.0/rhs) * self`, vec3.rs:142-148)
+// 1 / s correctly rounded in three instructions instead of the IEEE expansion's twelve: v_rcp_f32
+// (1 ulp) and one Newton step by fma. It is the IEEE quotient for every s with |s| in [2^-126,
+// 2^126) (exhaustive on the device: rrt_testing_recip_check, tests/test_gpu_recip.py); for s = +-0,
+// +-inf and NaN the step's residual is NaN and the estimate, exact there, is kept. The kernel takes
+// it for reciprocals of square roots of |v|^2 (>= 2^-75) and of probabilities in [0.05, 0.95].
+// RRT_RCP=0: the IEEE division.
+#ifndef RRT_RCP
+#define RRT_RCP 1
+#endif
+__device__ __forceinline__ float recip_rn(float s) {
+    if (!RRT_RCP) return 1.0f / s;
+    const float r = __builtin_amdgcn_rcpf(s);
+    const float e = __builtin_fmaf(-s, r, 1.0f);
+    return e == e ? __builtin_fmaf(e, r, r) : r;
+}
+
 __device__ __forceinline__ V3 unit(V3 v) {
-    const float inv = 1.0f / __builtin_sqrtf(dot(v, v));
+    const float inv = recip_rn(__builtin_sqrtf(dot(v, v)));
     return muls(v, inv);
 }
 
@@ -99,7 +115,7 @@ __device__ __forceinline__ V3 random_unit_vector(RngState &s, C &cnt) {
         lensq = __builtin_fmaf(pz, pz, __builtin_fmaf(py, py, px * px));
         if (0.0f < lensq && lensq <= 1.0f) break;
     }
-    const float inv = 1.0f / __builtin_sqrtf(lensq);
+    const float inv = recip_rn(__builtin_sqrtf(lensq));
     return v3(px * inv, py * inv, pz * inv);
 }
 
@@ -248,13 +264,20 @@ struct RayK {
 
 // minNum / maxNum semantics (a NaN direction gives +2^64, as in the oracle's std::fmin/fmax)
 __device__ __forceinline__ float clamp_inv(float v) { return __builtin_fmaxf(__builtin_fminf(v, 0x1.0p64f), -0x1.0p64f); }
+// clamp_inv(1 / s) through recip_rn: |s| below 2^-126 (subnormal or zero, where the hardware
+// estimate is flushed) has |1 / s| > 2^126 and takes +-2^64 by its sign. Equal to
+// clamp_inv(1.0f / s) for every s with |s| < 2^126, NaN included (rrt_testing_recip_check).
+__device__ __forceinline__ float clamped_slope(float s) {
+    if (!RRT_RCP) return clamp_inv(1.0f / s);
+    return __builtin_fabsf(s) < 0x1.0p-126f ? __builtin_copysignf(0x1.0p64f, s) : clamp_inv(recip_rn(s));
+}
 
 __device__ __forceinline__ RayK ray_consts(V3 o, V3 d) {
     RayK r;
     // aabb.rs:58 adinv, hoisted per ray, clamped to +-2^64: a zero component then gives a huge
     // finite slope, so fma(P, inv, -o*inv) keeps the sign of (P - o). Unclamped, inf * P - inf * o
     // is NaN or -inf, and a slab that straddles o (lo < 0 < hi about o's sign) rejects the ray.
-    r.inv = v3(clamp_inv(1.0f / d.x), clamp_inv(1.0f / d.y), clamp_inv(1.0f / d.z));
+    r.inv = v3(clamped_slope(d.x), clamped_slope(d.y), clamped_slope(d.z));
     r.oi = v3(o.x * r.inv.x, o.y * r.inv.y, o.z * r.inv.z);
     r.ox = r.inv.x < 0.0f ? 4u : 0u;
     r.oy = r.inv.y < 0.0f ? 16u : 12u;
@@ -1020,7 +1043,7 @@ __device__ __forceinline__ bool shade(const KParams &P, const PR &prims, const G
 #endif
         float inv_pr;
         if (RRT_PR_HOST && kBook2 == kBook1Untextured) inv_pr = kind == 2 ? 1.0f / 0.95f : __int_as_float(m.b.y);
-        else inv_pr = 1.0f / pr;
+        else inv_pr = recip_rn(pr);
         ps.T = muls(mul(ps.T, att), inv_pr);
     } else {
         ps.T = mul(ps.T, att);
@@ -1764,5 +1787,30 @@ hipError_t launch_quantize(const float *d_accum, uint8_t *d_rgb8, uint32_t n_pix
     return hipGetLastError();
 }
 hipError_t launch_render_counting(const KParams &p, hipStream_t stream) { return launch_render_kernel(p, true, stream); }
+
+namespace {
+// Every f32 bit pattern: out[0] counts s with |s| in [2^-126, 2^126), +-0, +-inf or NaN whose
+// recip_rn(s) is not the IEEE 1.0f / s (NaN results compare equal); out[1] counts s with |s| <
+// 2^126 or NaN whose clamped_slope(s) is not clamp_inv(1.0f / s).
+__global__ __launch_bounds__(256) void rrt_recip_check(unsigned long long *out) {
+    uint32_t bad0 = 0, bad1 = 0;
+    for (uint64_t k = blockIdx.x * 256ull + threadIdx.x; k < (1ull << 32); k += (uint64_t)gridDim.x * 256ull) {
+        const uint32_t u = (uint32_t)k, a = u & 0x7fffffffu;
+        const float s = __uint_as_float(u);
+        auto same = [](float x, float y) { return __float_as_uint(x) == __float_as_uint(y) || (x != x && y != y); };
+        const bool normal = a >= 0x00800000u && a < 0x7e800000u;
+        const bool special = a == 0u || a >= 0x7f800000u;
+        if ((normal || special) && !same(recip_rn(s), 1.0f / s)) ++bad0;
+        if ((a < 0x7e800000u || a > 0x7f800000u) && !same(clamped_slope(s), clamp_inv(1.0f / s))) ++bad1;
+    }
+    if (bad0) atomicAdd(&out[0], (unsigned long long)bad0);
+    if (bad1) atomicAdd(&out[1], (unsigned long long)bad1);
+}
+}  // namespace
+
+hipError_t launch_recip_check(unsigned long long *d_out, hipStream_t stream) {
+    hipLaunchKernelGGL(rrt_recip_check, dim3(16384), dim3(256), 0, stream, d_out);
+    return hipGetLastError();
+}
 
 }  // namespace rrt

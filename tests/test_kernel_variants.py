@@ -35,7 +35,7 @@ VARIANTS = {
     "f64_host": ["-DRRT_F64_CAM64=0", "-DRRT_F64_HOST_INVR=0", "-DRRT_F64_WIDE_SPHERES=0", "-DRRT_F64_R2=0",
                  "-DRRT_F64_DIEL_HOST=0"],
     # the f32 kernel dividing for its dielectric constants, 1 / r and 1 / pr (host-formed by default)
-    "diel_kernel": ["-DRRT_DIEL_HOST=0", "-DRRT_INVR_HOST=0", "-DRRT_PR_HOST=0", "-DRRT_DIV_CONST=0"],
+    "diel_kernel": ["-DRRT_DIEL_HOST=0", "-DRRT_INVR_HOST=0", "-DRRT_PR_HOST=0", "-DRRT_DIV_CONST=0", "-DRRT_RCP=0"],
 }
 
 
