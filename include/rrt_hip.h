@@ -551,9 +551,10 @@ int32_t rrt_device_count(int32_t *count);
 void rrt_testing_device_wrap(int32_t on);
 
 /* Test support, not part of the drop-in: runs the f32 kernel's short reciprocal (v_rcp_f32 + one
- * fma Newton step) over every f32 bit pattern against the IEEE quotient; mismatches (2 x u64): [0] = patterns
- * with |s| in [2^-126, 2^126), +-0, +-inf or NaN whose reciprocal differs, mismatches[1] = patterns
- * with |s| < 2^126 or NaN whose clamped ray slope differs (tests/test_gpu_recip.py: both 0). */
+ * fma Newton step) and short square root over every f32 bit pattern against the IEEE results;
+ * mismatches (3 x u64): [0] patterns with |s| in [2^-126, 2^126), +-0, +-inf or NaN whose
+ * reciprocal differs, [1] patterns with |s| < 2^126 or NaN whose clamped ray slope differs, [2]
+ * patterns +0 or >= 2^-96 whose square root differs (tests/test_gpu_recip.py: all 0). */
 int32_t rrt_testing_recip_check(uint64_t *mismatches);
 
 #ifdef __cplusplus

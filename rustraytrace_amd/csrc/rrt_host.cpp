@@ -1656,15 +1656,14 @@ extern "C" void rrt_testing_device_wrap(int32_t on) { g_device_wrap.store(on != 
 extern "C" int32_t rrt_testing_recip_check(uint64_t *mismatches) {
     if (!mismatches) return fail(RRT_E_INVALID, "null mismatches");
     unsigned long long *d = nullptr;
-    HIP_TRY(hipMalloc((void **)&d, 2 * sizeof(unsigned long long)), "hipMalloc");
-    hipError_t e = hipMemset(d, 0, 2 * sizeof(unsigned long long));
+    HIP_TRY(hipMalloc((void **)&d, 3 * sizeof(unsigned long long)), "hipMalloc");
+    hipError_t e = hipMemset(d, 0, 3 * sizeof(unsigned long long));
     if (e == hipSuccess) e = rrt::launch_recip_check(d, nullptr);
-    unsigned long long h[2] = {0, 0};
+    unsigned long long h[3] = {0, 0, 0};
     if (e == hipSuccess) e = hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost);
     (void)hipFree(d);
     if (e != hipSuccess) return fail(RRT_E_HIP, std::string("rrt_testing_recip_check: ") + hipGetErrorString(e));
-    mismatches[0] = h[0];
-    mismatches[1] = h[1];
+    for (int i = 0; i < 3; ++i) mismatches[i] = h[i];
     return RRT_OK;
 }
 static bool device_wrap() { return g_device_wrap.load(); }

@@ -286,7 +286,8 @@ hipError_t launch_render_counting(const KParams &p, hipStream_t stream);
 // render_io quantiser on the device (d_accum: n_pixels x float4; d_rgb8: n_pixels x 3 B).
 hipError_t launch_quantize(const float *d_accum, uint8_t *d_rgb8, uint32_t n_pixels, float scale, hipStream_t stream);
 // Test support (rrt_testing_recip_check): the kernel's recip_rn / clamped_slope against the IEEE
-// quotient over every f32 bit pattern; d_out: 2 zeroed u64 mismatch counters
+// quotient (and sqrt_rn_big against the IEEE sqrt) over every f32 bit pattern; d_out: 3 zeroed u64
+// mismatch counters
 hipError_t launch_recip_check(unsigned long long *d_out, hipStream_t stream);
 // Implemented in rrt_books64.hip: one sample pass of the f64 books kernel (+ its chunk combine)
 // into p.accum64, and the f64 sums rounded to the f32 RGBA accum of the ABI.

@@ -94,6 +94,20 @@ __device__ __forceinline__ float recip_rn(float s) {
     return e == e ? __builtin_fmaf(e, r, r) : r;
 }
 
+// sqrt(x) correctly rounded for x = 0 or x >= 2^-96 (and +inf, NaN): v_sqrt_f32 and the choice
+// between its one-ulp neighbours by the sign of the fma remainders — the compiler's own correction
+// without the rescaling of small arguments (exhaustive on the device, rrt_testing_recip_check). The
+// kernel takes it where the argument is provably 0 or >= 2^-46: |p|^2 of the rejection loop, and
+// 1 - c^2 / |1 - |perp|^2| (0 or multiples of 2^-24 near 1). RRT_RCP=0: the library sqrt.
+__device__ __forceinline__ float sqrt_rn_big(float x) {
+    if (!RRT_RCP) return __builtin_sqrtf(x);
+    float s = __builtin_amdgcn_sqrtf(x);
+    const float sm = __uint_as_float(__float_as_uint(s) - 1u), sp = __uint_as_float(__float_as_uint(s) + 1u);
+    const float rm = __builtin_fmaf(-sm, s, x), rp = __builtin_fmaf(-sp, s, x);
+    s = rm <= 0.0f ? sm : s;
+    return rp > 0.0f ? sp : s;
+}
+
 __device__ __forceinline__ V3 unit(V3 v) {
     const float inv = recip_rn(__builtin_sqrtf(dot(v, v)));
     return muls(v, inv);
@@ -115,7 +129,7 @@ __device__ __forceinline__ V3 random_unit_vector(RngState &s, C &cnt) {
         lensq = __builtin_fmaf(pz, pz, __builtin_fmaf(py, py, px * px));
         if (0.0f < lensq && lensq <= 1.0f) break;
     }
-    const float inv = recip_rn(__builtin_sqrtf(lensq));
+    const float inv = recip_rn(sqrt_rn_big(lensq));  // lensq >= 2^-46
     return v3(px * inv, py * inv, pz * inv);
 }
 
@@ -128,7 +142,7 @@ __device__ __forceinline__ V3 refract(V3 uv, V3 n, float e) {
     c = (c < 1.0f) ? c : 1.0f;
     const V3 perp = muls(add(uv, muls(n, c)), e);
     const float k = __builtin_fabsf(1.0f - dot(perp, perp));
-    const V3 par = muls(n, -__builtin_sqrtf(k));
+    const V3 par = muls(n, -sqrt_rn_big(k));  // k = 0 or >= 2^-24
     return add(perp, par);
 }
 
@@ -1021,7 +1035,7 @@ __device__ __forceinline__ bool shade(const KParams &P, const PR &prims, const G
         const V3 ud = unit(ps.d);
         float c = -dot(ud, nrm);
         c = (c < 1.0f) ? c : 1.0f;
-        const float sn = __builtin_sqrtf(1.0f - c * c);
+        const float sn = sqrt_rn_big(1.0f - c * c);  // 0 or >= 2^-24
         const bool cannot = ri * sn > 1.0f;
         if (cannot || reflectance_r0(c, r0) > rnd(ps.rng)) dir = reflect(ud, nrm);
         else dir = refract(ud, nrm, ri);
@@ -1182,7 +1196,7 @@ __device__ __forceinline__ bool shade_b3(const KParams &P, const PR &prims, cons
             const V3 ud = unit(ps.d);
             float c = -dot(ud, nrm);
             c = (c < 1.0f) ? c : 1.0f;
-            const float sn = __builtin_sqrtf(1.0f - c * c);
+            const float sn = sqrt_rn_big(1.0f - c * c);  // 0 or >= 2^-24
             const bool cannot = ri * sn > 1.0f;
             if (cannot || reflectance_r0(c, r0) > rnd(ps.rng)) dir = reflect(ud, nrm);
             else dir = refract(ud, nrm, ri);
@@ -1791,9 +1805,10 @@ hipError_t launch_render_counting(const KParams &p, hipStream_t stream) { return
 namespace {
 // Every f32 bit pattern: out[0] counts s with |s| in [2^-126, 2^126), +-0, +-inf or NaN whose
 // recip_rn(s) is not the IEEE 1.0f / s (NaN results compare equal); out[1] counts s with |s| <
-// 2^126 or NaN whose clamped_slope(s) is not clamp_inv(1.0f / s).
+// 2^126 or NaN whose clamped_slope(s) is not clamp_inv(1.0f / s); out[2] counts s = +0 or s >=
+// 2^-96 (+inf and positive NaN patterns included) whose sqrt_rn_big(s) is not the IEEE sqrt.
 __global__ __launch_bounds__(256) void rrt_recip_check(unsigned long long *out) {
-    uint32_t bad0 = 0, bad1 = 0;
+    uint32_t bad0 = 0, bad1 = 0, bad2 = 0;
     for (uint64_t k = blockIdx.x * 256ull + threadIdx.x; k < (1ull << 32); k += (uint64_t)gridDim.x * 256ull) {
         const uint32_t u = (uint32_t)k, a = u & 0x7fffffffu;
         const float s = __uint_as_float(u);
@@ -1802,9 +1817,11 @@ __global__ __launch_bounds__(256) void rrt_recip_check(unsigned long long *out) 
         const bool special = a == 0u || a >= 0x7f800000u;
         if ((normal || special) && !same(recip_rn(s), 1.0f / s)) ++bad0;
         if ((a < 0x7e800000u || a > 0x7f800000u) && !same(clamped_slope(s), clamp_inv(1.0f / s))) ++bad1;
+        if ((u == 0u || (u >= 0x0f800000u && u < 0x80000000u)) && !same(sqrt_rn_big(s), __builtin_sqrtf(s))) ++bad2;
     }
     if (bad0) atomicAdd(&out[0], (unsigned long long)bad0);
     if (bad1) atomicAdd(&out[1], (unsigned long long)bad1);
+    if (bad2) atomicAdd(&out[2], (unsigned long long)bad2);
 }
 }  // namespace
 
