@@ -36,7 +36,8 @@ extern "C" {
  * 7: RRT_FLAG_F64 (the books path's f64 arithmetic), rrt_hip_render_f64, rrt_render_tile_f64_async,
  * rrt_quantize_accum_books_f64; 8: RrtTile bands dealt in serpentine order (was b % n_ranks);
  * 9: rrt_accum_chunk() = 256 and the frame's chunk halved while S <= 2K down to a quarter (frames
- * over 512 samples sum in chunks of 256; was 128), rrt_testing_device_wrap. */
+ * over 512 samples sum in chunks of 256; was 128), rrt_testing_device_wrap, rrt_testing_recip_check
+ * (test-only entry points, no drop-in counterpart). */
 #define RRT_ABI_VERSION 9u
 
 /* ---- scene ABI (== src/gpu/mod.rs:13-42) ------------------------------------------ */

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-4 batch 21: short square root where the argument is provably 0 or >= 2^-46 (rejection-loop
+# Round-4 batch 21/22: short square roots (provable domains; then wave-uniform gated in the leaf loops and unit()):
 # |p|^2, dielectric 1 - c^2, refraction): exhaustive device check, parity, A/B against the previous
 # commit's library (variants/prev) on C2, C5.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
