@@ -108,8 +108,17 @@ __device__ __forceinline__ float sqrt_rn_big(float x) {
     return rp > 0.0f ? sp : s;
 }
 
+// sqrt(x) correctly rounded for any x: sqrt_rn_big unless an active lane of the wave holds a
+// nonzero |x| < 2^-96 (a wave-uniform branch to the library sequence; sqrt_rn_big differs from the
+// IEEE root only on positive and negative arguments below 2^-96 other than +-0, per the device check)
+__device__ __forceinline__ float sqrt_rn(float x) {
+    if (!RRT_RCP) return __builtin_sqrtf(x);
+    if (__ballot(__builtin_fabsf(x) < 0x1.0p-96f && x != 0.0f) == 0) return sqrt_rn_big(x);
+    return __builtin_sqrtf(x);
+}
+
 __device__ __forceinline__ V3 unit(V3 v) {
-    const float inv = recip_rn(__builtin_sqrtf(dot(v, v)));
+    const float inv = recip_rn(sqrt_rn(dot(v, v)));
     return muls(v, inv);
 }
 
@@ -500,7 +509,7 @@ __device__ __forceinline__ void test_prims(const PR &prim_cr, int first, int cou
         const float c = dot(oc, oc) - (PR::kR2 ? cr.w : cr.w * cr.w);
         const float disc = __builtin_fmaf(h, h, -(a * c));
         if (disc < 0.0f) continue;
-        const float sq = __builtin_sqrtf(disc);
+        const float sq = sqrt_rn(disc);
         float root = (h - sq) / a;
         if (!(0.001f < root && root < closest)) {
             root = (h + sq) / a;
@@ -565,7 +574,7 @@ __device__ __forceinline__ void test_range(const PR &prim_cr, int first, int cou
         // when no lane takes it.
         if (disc < 0.0f) continue;
         if constexpr (RRT_PHASE_TIMING == 3) cnt.d2 += 1;
-        const float sq = __builtin_sqrtf(disc);
+        const float sq = sqrt_rn(disc);
         float root = div_by_a<kFastDiv>(h - sq, rk);
         if (!(0.001f < root)) root = div_by_a<kFastDiv>(h + sq, rk);
         if (0.001f < root && root < closest) {
