@@ -426,6 +426,16 @@ def load_issue(path, config, W, S, lib_path):
                         f"VALU wave-instructions / (1024 SIMDs x cycles)"}
 
 
+def device_shortfall(backend: str, local_rank: int, n_devices: int):
+    """Under RCCL each rank owns GPU `local_rank`: a box with fewer devices cannot run the job, so
+    the rank stops with this message before init_process_group (where it would wait in the
+    rendezvous for ranks that never come) and the launcher returns non-zero. None = runnable."""
+    if backend == "nccl" and local_rank >= n_devices:
+        return (f"bench.py: rank with LOCAL_RANK={local_rank} needs GPU {local_rank} but {n_devices} HIP "
+                f"device(s) are visible (RCCL runs one process per GPU)")
+    return None
+
+
 def main():
     args = parse()
     cmd = launcher_command(args, sys.argv[1:], os.environ)
@@ -446,6 +456,10 @@ def main():
     # RCCL ("nccl") between one process per GPU. RRT_BENCH_BACKEND=gloo is a rehearsal mode for
     # ranks sharing a GPU (device = local rank mod device count; host copies for the gather).
     backend = os.environ.get("RRT_BENCH_BACKEND", "nccl")
+    short = device_shortfall(backend, local, torch.cuda.device_count())  # counts without a GPU context
+    if short:
+        print(short, file=sys.stderr, flush=True)
+        sys.exit(2)
     device = local % max(1, torch.cuda.device_count()) if backend == "gloo" else local
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")

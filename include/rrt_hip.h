@@ -551,11 +551,20 @@ int32_t rrt_device_count(int32_t *count);
  * library: without it n_gpus must not exceed the visible devices. Process-wide. */
 void rrt_testing_device_wrap(int32_t on);
 
+/* Test support, not part of the drop-in: forces the LDS layout in which the f64 books kernel
+ * (RRT_FLAG_F64) stages a scene that fits its block — bit 0: f64-widened sphere records, bit 1: the
+ * 1/r table, bit 2: the f32 pre-test records beside widened ones (with bit 0) — instead of its
+ * automatic choice; -1 (the default at every load) restores it. A forced layout over the block's
+ * 64 KB fails the render. Every layout renders the same bits (tests/test_gpu_books64.py).
+ * Process-wide. */
+void rrt_testing_f64_layout(int32_t layout);
+
 /* Test support, not part of the drop-in: runs the f32 kernel's short reciprocal (v_rcp_f32 + one
  * fma Newton step) and short square root over every f32 bit pattern against the IEEE results;
  * mismatches (3 x u64): [0] patterns with |s| in [2^-126, 2^126), +-0, +-inf or NaN whose
  * reciprocal differs, [1] patterns with |s| < 2^126 or NaN whose clamped ray slope differs, [2]
- * patterns +0 or >= 2^-96 whose square root differs (tests/test_gpu_recip.py: all 0). */
+ * patterns +-0 or |s| >= 2^-96 of either sign (negatives, infinities and NaN included) whose square
+ * root differs from the IEEE one (tests/test_gpu_recip.py: all 0). */
 int32_t rrt_testing_recip_check(uint64_t *mismatches);
 
 #ifdef __cplusplus

@@ -79,6 +79,7 @@ EXPORTED_SYMBOLS = (
     "rrt_render_tile_f64_async",
     "rrt_quantize_accum_books_f64",
     "rrt_testing_device_wrap",
+    "rrt_testing_f64_layout",
     "rrt_testing_recip_check",
 )
 
@@ -255,6 +256,7 @@ def load() -> ctypes.CDLL:
         "rrt_render_tile_f64_async": (c_int32, [P, P, P, P]),
         "rrt_quantize_accum_books_f64": (c_int32, [c_uint32, c_uint32, P, c_uint32, P]),
         "rrt_testing_device_wrap": (None, [c_int32]),
+        "rrt_testing_f64_layout": (None, [c_int32]),
         "rrt_testing_recip_check": (c_int32, [P]),
     }
     experiment = "RRT_LIB_PATH" in os.environ  # A/B of older builds: tolerate symbols they lack

@@ -31,6 +31,7 @@
 // rounded outward and grown by the f32 slab bound, tested in f64: conservative) as the f32 kernel.
 #include "rrt_internal.h"
 
+#include <atomic>
 #include <cstdlib>
 #include <type_traits>
 
@@ -39,9 +40,31 @@ namespace {
 
 #include "rrt_device.h"
 #include "rrt_box32.h"
+#include "rrt_sphere32.h"
 
 // issue priority by loop phase (as rrt_kernel.hip: refill 2, node steps 1, leaf batches 2, shading 0)
 constexpr int kPrioRefill = 2, kPrioNode = 1, kPrioLeaf = 2, kPrioShade = 0;
+
+// Debug builds only (-DRRT_F64_STATS=1..4 in F64_FLAGS, never the shipped library): per-wave
+// statistics written into counter slots 2..4 by the non-counting kernel.
+//   1: s_memtime cycles in refill + ray start / the traversal loop (nodes + leaves) / shading
+//   2: leaf batches (wave): sum of the batch's largest lane range (f64 sphere-test iterations the
+//      wave runs) / sum of the largest lane count of tests with disc >= 0 / number of batches
+//   3: lane f64 sphere tests / those with disc >= 0 / those that update the closest hit
+//   4: node-step wave-iterations / sum of stepping lanes / leaf-batch wave-iterations x 64
+//   5: spheres the f32 pre-test keeps / their f64 disc >= 0 / lane sphere tests (ranges)
+#ifndef RRT_F64_STATS
+#define RRT_F64_STATS 0
+#endif
+// Debug builds only: random_unit_vector takes its first candidate (prices the rejection loop)
+#ifndef RRT_DEBUG_NOREJECT
+#define RRT_DEBUG_NOREJECT 0
+#endif
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, off, 64));
+    return v;
+}
 
 struct D3 {
     double x, y, z;
@@ -84,7 +107,7 @@ __device__ __forceinline__ D3 random_unit_vector(RngState &s) {
         b = draw_centred(s);
         c = draw_centred(s);
         const uint64_t S = sq_i24(a) + sq_i24(b) + sq_i24(c);
-        if (S - 1u < (1ull << 46)) break;  // 0 < S <= 2^46
+        if (RRT_DEBUG_NOREJECT || S - 1u < (1ull << 46)) break;  // 0 < S <= 2^46
     }
     const double x = centred_to_pm1(a), y = centred_to_pm1(b), z = centred_to_pm1(c);
     const double lensq = x * x + y * y + z * z;
@@ -252,14 +275,16 @@ __device__ __forceinline__ double div_by_const64(double x, double c) {
 }
 
 // ImageTexture::value (texture.rs:89-109) at get_sphere_uv(outward) (the_next_week/sphere.rs:46-52):
-// theta = acos(-y), phi = atan2(-z, x) + pi, u = phi / (2 pi), v = theta / pi.
-__device__ __forceinline__ D3 texel64(const KParams &P, int tex, D3 outward) {
+// theta = acos(-y), phi = atan2(-z, x) + pi, u = phi / (2 pi), v = theta / pi. The texel's bytes
+// r | g << 8 | b << 16 (value = (1/255) byte, rtw_image.rs:46-55), or 0x1000000 for a texture with no
+// data (the solid cyan (0, 1, 1) of texture.rs:91-93).
+__device__ __forceinline__ uint32_t texel_bytes64(const KParams &P, int tex, D3 outward) {
     const double theta = rrt_acos64(-outward.y);
     const double phi = rrt_atan2_64(-outward.z, outward.x) + kPiD;
     double u = div_by_const64(phi, 2.0 * kPiD);
     double v = div_by_const64(theta, kPiD);
     const GTexture t = P.texs[tex];
-    if (t.height <= 0) return d3(0.0, 1.0, 1.0);              // texture.rs:91-93
+    if (t.height <= 0) return 0x1000000u;                      // texture.rs:91-93: (0, 1, 1)
     u = u < 0.0 ? 0.0 : (u > 1.0 ? 1.0 : u);                   // Interval::clamp
     v = 1.0 - (v < 0.0 ? 0.0 : (v > 1.0 ? 1.0 : v));
     auto as_i32 = [](double x) -> int {                        // Rust `as i32`: saturating, NaN -> 0
@@ -273,8 +298,53 @@ __device__ __forceinline__ D3 texel64(const KParams &P, int tex, D3 outward) {
     i = i < 0 ? 0 : (i < t.width ? i : t.width - 1);           // rtw_image.rs:51-52, 70-78
     j = j < 0 ? 0 : (j < t.height ? j : t.height - 1);
     const uint8_t *px = P.tex_pool + t.offset + ((size_t)j * t.width + i) * 3;
+    return (uint32_t)px[0] | ((uint32_t)px[1] << 8) | ((uint32_t)px[2] << 16);
+}
+__device__ __forceinline__ double texel_channel64(uint32_t byte) {
     const double cs = 1.0 / 255.0;
-    return d3(cs * (double)px[0], cs * (double)px[1], cs * (double)px[2]);
+    return cs * (double)byte;
+}
+__device__ __forceinline__ D3 texel_value64(uint32_t bytes) {
+    if (bytes == 0x1000000u) return d3(0.0, 1.0, 1.0);
+    return d3(texel_channel64(bytes & 0xffu), texel_channel64((bytes >> 8) & 0xffu), texel_channel64(bytes >> 16));
+}
+
+// ---- the throughput product back to front (camera.rs:182-209's recursion) -----------------------
+// BOOKS returns attenuation * ray_color(scattered) [/ p] up its recursion, so a path's radiance is
+// L_k = (att_k (.) L_{k+1}) [* (1/p_k) for k >= 5] from the end of the path back to the camera ray:
+// each scatter's attenuation is kept in the lane's history (global memory, [bounce][lane slot], 12 B:
+// an attenuation is an f32 albedo, (1, 1, 1), or a texel's bytes — stored negated, the sign marks
+// them) and the product is formed back to front when a path ends with radiance (sky, background or
+// a light). The same roundings as the recursion, in the same order: the kernel's per-sample radiance
+// equals BOOKS' bit for bit. RRT_F64_B2F=0: the throughput carried front to back (a few ulps off).
+#ifndef RRT_F64_B2F
+#define RRT_F64_B2F 1
+#endif
+struct Att32 {
+    float x, y, z;
+};
+__device__ __forceinline__ double att_decode(float f) {
+    return (__float_as_uint(f) >> 31) ? texel_channel64((uint32_t)(-f)) : (double)f;
+}
+// camera.rs:191-195: max of the attenuation's components, clamped to [0.05, 0.95]
+__device__ __forceinline__ double rr_probability64(D3 att) {
+    double pr = att.x;
+    if (att.y > pr) pr = att.y;
+    if (att.z > pr) pr = att.z;
+    if (pr < 0.05) pr = 0.05;
+    if (pr > 0.95) pr = 0.95;
+    return pr;
+}
+template <bool kTex>
+__device__ __forceinline__ D3 fold_back64(const Att32 *__restrict__ hist, uint32_t lanes, uint32_t slot, uint32_t n,
+                                          D3 L) {
+    for (uint32_t k = n; k-- > 0;) {
+        const Att32 a = hist[(size_t)k * lanes + slot];
+        const D3 att = kTex ? d3(att_decode(a.x), att_decode(a.y), att_decode(a.z)) : f2d(a.x, a.y, a.z);
+        L = mul(att, L);
+        if (k >= 5u) L = muls(L, 1.0 / rr_probability64(att));  // Div<f64>: (1/p) * v (vec3.rs:142-148)
+    }
+    return L;
 }
 
 // Per-ray constants of the box test (rrt_box32.h: f32 arithmetic on the f32 / f16 planes, widened
@@ -406,23 +476,55 @@ __device__ __forceinline__ double radius_of(const Sphere64 &c) { return RRT_F64_
 __device__ __forceinline__ double radius_sq_of(const float4 &c) { return (double)c.w * (double)c.w; }
 __device__ __forceinline__ double radius_sq_of(const Sphere64 &c) { return RRT_F64_R2 ? c.r2 : c.r2 * c.r2; }
 
+// The f32 pre-test (rrt_sphere32.h) over the lane's range first: it marks the spheres whose f64
+// discriminant may be >= 0, and the f64 test runs over the marked ones only, in index order (the
+// unmarked ones would `continue` in it). The wave runs the f64 body max-over-lanes of the marked
+// counts instead of the range lengths (C2: 1.17 against 2.21 iterations per leaf batch, measured by
+// RRT_F64_STATS=2). RRT_F64_SPHERE32=0: every sphere runs the f64 test.
+#ifndef RRT_F64_SPHERE32
+#define RRT_F64_SPHERE32 1
+#endif
+#ifndef RRT_F64_S32_HOLD
+#define RRT_F64_S32_HOLD 0
+#endif
 template <bool kCount, typename Rec>
-__device__ __forceinline__ void leaves64(const Rec *__restrict__ prims, Leaves lv, D3 o, D3 d, double a, Trav64 &t,
+__device__ __forceinline__ void leaves64(const Rec *__restrict__ prims, const float4 *__restrict__ recs32, Leaves lv,
+                                         D3 o, D3 d, double a, const RaySphere32 &r32, bool pre, Trav64 &t,
                                          Counters &cnt) {
     const double ra = RRT_F64_DIVA ? recip_a64(a) : 0.0;
     const int first = (int)(lv & kLinkFirstMask), count = (int)(lv >> kLinkCountShift);
-    for (int i = first; i < first + count; ++i) {
-        if (kCount) cnt.spheres++;
+    uint32_t todo = (1u << count) - 1u;
+    if (RRT_F64_SPHERE32 && pre) {
+        // the ray's f32 constants: held from the ray start, or formed here per batch (fewer VGPRs
+        // live across the node steps)
+        const RaySphere32 rs = RRT_F64_S32_HOLD ? r32 : sphere32_ray(o.x, o.y, o.z, d.x, d.y, d.z);
+        todo = 0;
+        for (int j = 0; j < count; ++j) {
+            const float4 c = recs32[first + j];
+            if (!sphere32_miss(rs, c.x, c.y, c.z, c.w)) todo |= 1u << j;
+        }
+    }
+    if (kCount) cnt.spheres += (uint32_t)count;
+    if (RRT_F64_STATS == 5) {
+        cnt.d2 += (uint32_t)count;
+        cnt.d0 += (uint32_t)__popc(todo);
+    }
+    while (todo != 0) {
+        const int i = first + __builtin_ctz(todo);
+        todo &= todo - 1u;
         const Rec cr = prims[i];
         const D3 oc = sub(center_of(cr), o);
         const double h = dot(d, oc);
         const double c = dot(oc, oc) - radius_sq_of(cr);
         const double disc = h * h - a * c;
+        if (RRT_F64_STATS == 3) cnt.d0++;
         if (disc < 0.0) continue;
+        if (RRT_F64_STATS == 2 || RRT_F64_STATS == 3 || RRT_F64_STATS == 5) cnt.d1++;
         const double sq = __builtin_sqrt(disc);
         double root = div_a64(h - sq, a, ra);
         if (!(0.001 < root)) root = div_a64(h + sq, a, ra);
         if (0.001 < root && root < t.closest) {
+            if (RRT_F64_STATS == 3) cnt.d2++;
             t.closest = root;
             t.closest32 = (float)root;
             t.hit_prim = i;
@@ -431,7 +533,10 @@ __device__ __forceinline__ void leaves64(const Rec *__restrict__ prims, Leaves l
 }
 
 struct Path64 {
-    D3 o, d, T;
+    D3 o, d;
+#if !RRT_F64_B2F
+    D3 T;
+#endif
     RngState rng;
     uint32_t k;  // bounce index (camera ray = 0)
 };
@@ -472,19 +577,25 @@ __device__ __forceinline__ void camera_ray64(uint32_t x, uint32_t y, Path64 &ps)
     if (C.flags & 0x1u) (void)rnd64(ps.rng);  // RRT_FLAG_RAY_TIME: the time draw (the_next_week/camera.rs:160)
     ps.o = origin;
     ps.d = sub(sample, origin);
+#if !RRT_F64_B2F
     ps.T = d3(1.0, 1.0, 1.0);
+#endif
     ps.k = 0;
 }
 
 // After the closest-hit query: sky / background, or emission / scatter / RR (camera.rs:182-209).
-// Returns true when the path has ended; its radiance T * Le (if any) goes into `sum`.
+// Returns true when the path has ended; `Le` then holds the radiance at its end (sky, background,
+// emission; 0 when absorbed, killed by Russian roulette or — in the caller — cut at max_depth),
+// which the caller carries back to the camera ray (fold_back64). A scatter stores its attenuation at
+// bounce k of the lane's history.
 // kClass: kF64Full (every book-1 material kind), kF64Untextured (no image texture: the f64 acos /
 // atan2 / texel path compiled out), kF64Diffuse (Lambertian and emissive only: metal and dielectric
 // compiled out), chosen per scene by launch_render_pass_f64 like the f32 kernel's classes.
 constexpr int kF64Full = 0, kF64Untextured = 1, kF64Diffuse = 2;
 template <int kClass, typename Rec>
 __device__ __forceinline__ bool shade64(const KParams &P, const Rec *prims, const GMaterial *mtl, const double *inv_r,
-                                        Path64 &ps, double t, int prim, D3 &sum) {
+                                        Path64 &ps, double t, int prim, D3 &Le, uint32_t slot) {
+    Le = d3(0.0, 0.0, 0.0);
     if (prim < 0) {
         D3 bg;
         if (P.bg_mode == 1u) {
@@ -494,7 +605,11 @@ __device__ __forceinline__ bool shade64(const KParams &P, const Rec *prims, cons
             const double a = 0.5 * (ud.y + 1.0);
             bg = d3((1.0 - a) * 1.0 + a * 0.5, (1.0 - a) * 1.0 + a * 0.7, (1.0 - a) * 1.0 + a * 1.0);
         }
-        sum = add(sum, mul(ps.T, bg));
+#if RRT_F64_B2F
+        Le = bg;
+#else
+        Le = mul(ps.T, bg);
+#endif
         return true;
     }
     const Rec cr = prims[prim];
@@ -510,10 +625,15 @@ __device__ __forceinline__ bool shade64(const KParams &P, const Rec *prims, cons
     const int kind = m.b.x;
     const D3 albedo = f2d(m.a.x, m.a.y, m.a.z);
     if (kind == 4) {  // DiffuseLight: emitted, scatter None
-        sum = add(sum, mul(ps.T, albedo));
+#if RRT_F64_B2F
+        Le = albedo;
+#else
+        Le = mul(ps.T, albedo);
+#endif
         return true;
     }
     D3 att, dir;
+    Att32 rec{m.a.x, m.a.y, m.a.z};  // the attenuation's history record
     if (kClass != kF64Diffuse && kind == 1) {  // Metal (material.rs:53-64): unit(reflect) + fuzz * random_unit_vector
         const D3 refl = unit_vector(reflect(ps.d, nrm));
         dir = add(refl, muls(random_unit_vector(ps.rng), (double)m.a.w));
@@ -541,22 +661,33 @@ __device__ __forceinline__ bool shade64(const KParams &P, const Rec *prims, cons
         if (cannot || reflectance_r0(c, r0) > rnd64(ps.rng)) dir = reflect(ud, nrm);
         else dir = refract(ud, nrm, ri);
         att = d3(1.0, 1.0, 1.0);
+        rec = Att32{1.0f, 1.0f, 1.0f};
     } else {  // Lambertian, plain or image-textured (material.rs:28-40; the_next_week/material.rs:41-53)
         dir = add(nrm, random_unit_vector(ps.rng));
         if (__builtin_fabs(dir.x) < 1e-8 && __builtin_fabs(dir.y) < 1e-8 && __builtin_fabs(dir.z) < 1e-8) dir = nrm;
-        att = (kClass != kF64Untextured && kind == 3) ? texel64(P, m.b.z, outward) : albedo;
+        att = albedo;
+        if (kClass != kF64Untextured && kind == 3) {
+            const uint32_t b = texel_bytes64(P, m.b.z, outward);
+            att = texel_value64(b);
+            if (b == 0x1000000u) rec = Att32{0.0f, 1.0f, 1.0f};
+            else rec = Att32{-(float)(b & 0xffu), -(float)((b >> 8) & 0xffu), -(float)(b >> 16)};
+        }
     }
     if (ps.k >= 5u) {  // camera.rs:189-200
-        double pr = att.x;
-        if (att.y > pr) pr = att.y;
-        if (att.z > pr) pr = att.z;
-        if (pr < 0.05) pr = 0.05;
-        if (pr > 0.95) pr = 0.95;
+        const double pr = rr_probability64(att);
         if (rnd64(ps.rng) > pr) return true;
+#if !RRT_F64_B2F
         ps.T = muls(mul(ps.T, att), 1.0 / pr);
     } else {
         ps.T = mul(ps.T, att);
+#endif
     }
+#if RRT_F64_B2F
+    reinterpret_cast<Att32 *>(P.hist)[(size_t)ps.k * P.hist_lanes + slot] = rec;
+#else
+    (void)rec;
+    (void)slot;
+#endif
     ps.o = p;
     ps.d = dir;
     ps.k++;
@@ -580,6 +711,7 @@ __device__ __forceinline__ void render64_body(const KParams &P) {
     const Rec *prims = reinterpret_cast<const Rec *>(P.prim_cr);
     const GMaterial *mtl = P.prim_mtl;
     const double *inv_r = P.prim_inv_r64;
+    const float4 *recs32 = P.prim_cr;  // the pre-test's f32 records (center, r)
     if constexpr (kLds) {  // stage nodes + spheres (+ 1/r) once per block
         uint4 *dst = lds_dyn + (P.stack_depth * kBlk * sizeof(uint16_t) + 15u) / 16u;
         // Node112: each 80-B GNode re-laid as 112 B whose axis a holds both children's (lo, hi), then
@@ -616,10 +748,20 @@ __device__ __forceinline__ void render64_body(const KParams &P) {
         double *dr = reinterpret_cast<double *>(dst + nn + np);
         if (P.inv_r_in_lds)
             for (uint32_t i = threadIdx.x; i < P.n_prims; i += kBlk) dr[i] = P.prim_inv_r64[i];
+        // the f32 records of the pre-test, after the 1/r table (widened layout only; otherwise the
+        // staged records are the f32 ones)
+        float4 *d32 = reinterpret_cast<float4 *>(dst + nn + np + (P.inv_r_in_lds ? (P.n_prims + 1u) / 2u : 0u));
+        if (kMode == kF64LdsWide && P.rec32_in_lds)
+            for (uint32_t i = threadIdx.x; i < P.n_prims; i += kBlk) d32[i] = P.prim_cr[i];
         __syncthreads();
         nodes = reinterpret_cast<const Node *>(dst);
         prims = reinterpret_cast<const Rec *>(dst + nn);
         if (P.inv_r_in_lds) inv_r = dr;
+        if constexpr (kMode == kF64LdsWide) {
+            if (P.rec32_in_lds) recs32 = d32;
+        } else {
+            recs32 = reinterpret_cast<const float4 *>(prims);
+        }
     }
     LdsStack<uint16_t, kBlk> stack;
     stack.init(lds_stack, threadIdx.x);
@@ -630,13 +772,18 @@ __device__ __forceinline__ void render64_body(const KParams &P) {
     uint32_t has = 0, need_ray = 0;
     bool q_open = true;
     uint32_t xy = 0, s = 0, s_hi = 0;
+    uint32_t px = 0;         // the unit's tile-local pixel index
+    uint32_t tail = 0;       // the unit is a tail chunk: its samples' radiances go to seq64 one by one
+    const uint32_t slot = blockIdx.x * (uint32_t)kBlk + threadIdx.x;  // the lane's history slot
     uint64_t pkey = 0;
     D3 sum = d3(0.0, 0.0, 0.0);
     Path64 ps;
     Trav64 tr;
     tr.node = -1;
+    [[maybe_unused]] uint64_t ph0 = 0, ph1 = 0, ph2 = 0, tp = 0;
     uint32_t pool_base = (blockIdx.x & (kQueues - 1u)) * 64u, pool_left = 0;  // queue claims: rrt_kernel.hip
     for (;;) {
+        if constexpr (RRT_F64_STATS == 1) tp = __builtin_amdgcn_s_memtime();
         __builtin_amdgcn_s_setprio(kPrioRefill);
         const uint64_t idle = __ballot(!has);
         if (idle != 0 && pool_left == 0 && q_open) {
@@ -677,6 +824,8 @@ __device__ __forceinline__ void render64_body(const KParams &P) {
                     xy = x | (y << 16);
                     s = Q.sample_begin + chunk_first(Q, chunk);
                     s_hi = min(s + (chunk < Q.n_big ? Q.chunk : Q.chunk_small), Q.sample_end);
+                    px = ly * Q.width + x;
+                    tail = Q.seq && chunk >= Q.n_big ? 1u : 0u;
                     sum = d3(0.0, 0.0, 0.0);
                     pkey = pixel_key(Q, x, y);
                     ps.rng = path_rng_k(pkey, s);
@@ -708,15 +857,29 @@ __device__ __forceinline__ void render64_body(const KParams &P) {
         const uint32_t live = (uint32_t)__popcll(__ballot(has));
         const uint32_t min_active = (live * P.trav_frac) >> 8;
         const uint32_t leaf_min = (live * P.leaf_frac) >> 8;
+        if constexpr (RRT_F64_STATS == 1) {
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            ph0 += t - tp;
+            tp = t;
+        }
         RayK64 rk;
+        RaySphere32 r32;
         double a = 0.0;
         if (tr.node >= 0) {
             rk = ray_consts64(ps.o, ps.d);
+            if (RRT_F64_SPHERE32 && RRT_F64_S32_HOLD) r32 = sphere32_ray(ps.o.x, ps.o.y, ps.o.z, ps.d.x, ps.d.y, ps.d.z);
             a = dot(ps.d, ps.d);  // sphere.rs:27 r.direction().length_squared()
         }
         __builtin_amdgcn_s_setprio(kPrioNode);
         Leaves lv = 0;
         for (;;) {
+            if constexpr (RRT_F64_STATS == 4) {
+                const uint64_t sm = __ballot(tr.node >= 0 && lv == 0);
+                if (sm != 0) {
+                    ph0 += 1;
+                    ph1 += (uint64_t)__popcll(sm);
+                }
+            }
             if (tr.node >= 0 && lv == 0) {
                 Leaves l;
                 if (trav_node64<kCount>(nodes, stack, rk, tr, l, cnt)) lv = l;
@@ -727,40 +890,79 @@ __device__ __forceinline__ void render64_body(const KParams &P) {
             const bool batch = ((uint32_t)__popcll(pm) > leaf_min) | leave | (tm == pm);
             if ((pm != 0) & batch) {
                 __builtin_amdgcn_s_setprio(kPrioLeaf);
+                [[maybe_unused]] const uint32_t n_l = lv >> kLinkCountShift, s_l = cnt.d1;
                 if (lv != 0) {
-                    leaves64<kCount>(prims, lv, ps.o, ps.d, a, tr, cnt);
+                    leaves64<kCount>(prims, recs32, lv, ps.o, ps.d, a, r32, P.sphere32 != 0u, tr, cnt);
                     lv = 0;
                 }
+                if constexpr (RRT_F64_STATS == 2) {
+                    ph0 += wave_max_u32(n_l);
+                    ph1 += wave_max_u32(cnt.d1 - s_l);
+                    ph2 += 1;
+                }
+                if constexpr (RRT_F64_STATS == 4) ph2 += 64;
                 __builtin_amdgcn_s_setprio(kPrioNode);
             }
             if (leave) break;
         }
+        if constexpr (RRT_F64_STATS == 1) {
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            ph1 += t - tp;
+            tp = t;
+        }
         __builtin_amdgcn_s_setprio(kPrioShade);
+        D3 Le = d3(0.0, 0.0, 0.0);
         if (has && !need_ray && tr.node < 0) {
             need_ray = 1;
-            seg_done = shade64<kClass>(P, prims, mtl, inv_r, ps, tr.closest, tr.hit_prim, sum) ? 1u : 0u;
+            seg_done = shade64<kClass>(P, prims, mtl, inv_r, ps, tr.closest, tr.hit_prim, Le, slot) ? 1u : 0u;
         }
         w_paths += (uint32_t)__popcll(__ballot(seg_done));
-        if (seg_done) {  // pixel_color += ray_color(..): already in `sum`
+        if (seg_done) {  // pixel_color += ray_color(..) (camera.rs:72-76)
+#if RRT_F64_B2F
+            // the radiance at the path's end carried back through its scatters; a path that ended
+            // with none (absorbed, Russian roulette, max_depth) adds an exact 0
+            if (Le.x != 0.0 || Le.y != 0.0 || Le.z != 0.0)
+                Le = fold_back64<kClass == kF64Full>(reinterpret_cast<const Att32 *>(P.hist), P.hist_lanes, slot,
+                                                     ps.k, Le);
+#endif
+            const auto &Q = *kernarg_params();
+            if (tail) {  // a tail sample: its radiance, folded into the pixel's sum in order later
+                const size_t npx = (size_t)Q.tile_rows * Q.width;
+                double *o = Q.seq64 + 3u * ((size_t)(s - Q.sample_begin - Q.seq_first) * npx + px);
+                o[0] = Le.x;
+                o[1] = Le.y;
+                o[2] = Le.z;
+            } else {
+                sum = add(sum, Le);
+            }
             ++s;
             const uint32_t x = xy & 0xffffu, y = xy >> 16;
             if (s < s_hi) {
                 ps.rng = path_rng_k(pkey, s);
                 camera_ray64(x, y, ps);
             } else {  // unit complete: the chunk's f64 sum, in sample order
-                const auto &Q = *kernarg_params();
                 const uint32_t rel = s_hi - 1u - Q.sample_begin;
                 const uint32_t nbs = Q.n_big * Q.chunk;
                 const uint32_t chunk =
                     rel < nbs ? fast_div(rel, fdiv(Q.fd_chunk)) : Q.n_big + fast_div(rel - nbs, fdiv(Q.fd_chunk_small));
-                const uint32_t gb = fast_div(y, fdiv(Q.fd_band_rows));
-                const uint32_t ly = fast_div(gb, fdiv(Q.fd_n_ranks)) * Q.band_rows + (y - gb * Q.band_rows);
-                const size_t px = (size_t)ly * Q.width + x;
                 const D4 out{sum.x, sum.y, sum.z, (double)(s_hi - (Q.sample_begin + chunk_first(Q, chunk)))};
-                if (Q.n_chunks == 1) Q.accum64[px] = out;
-                else Q.partial64[(size_t)(chunk - Q.chunk_begin) * ((size_t)Q.tile_rows * Q.width) + px] = out;
+                if (Q.n_chunks == 1 || (Q.seq && !tail)) Q.accum64[px] = out;  // the whole pixel, or its prefix
+                else if (!tail) Q.partial64[(size_t)(chunk - Q.chunk_begin) * ((size_t)Q.tile_rows * Q.width) + px] = out;
                 has = 0;
             }
+        }
+        if constexpr (RRT_F64_STATS == 1) ph2 += __builtin_amdgcn_s_memtime() - tp;
+    }
+    if constexpr (RRT_F64_STATS == 3 && !kCount) {
+        ph0 = wave_sum_u32(cnt.d0);
+        ph1 = wave_sum_u32(cnt.d1);
+        ph2 = wave_sum_u32(cnt.d2);
+    }
+    if constexpr (RRT_F64_STATS != 0 && !kCount) {
+        if (lane == 0) {
+            atomicAdd(&P.counters[2], (unsigned long long)ph0);
+            atomicAdd(&P.counters[3], (unsigned long long)ph1);
+            atomicAdd(&P.counters[4], (unsigned long long)ph2);
         }
     }
     uint32_t nv = 0, bt = 0, st = 0;
@@ -810,6 +1012,23 @@ __global__ __launch_bounds__(256) void rrt_combine_chunks64(const D4 *__restrict
     accum[p] = D4{acc.x, acc.y, acc.z, count};
 }
 
+// Sequential-sum mode: the pass's tail-sample radiances added to each pixel's sum in sample order
+// (pixel_color += ray_color(..), camera.rs:72-76), continuing from the prefix chunk's sum (or the
+// previous pass's); w = the samples summed so far.
+__global__ __launch_bounds__(256) void rrt_fold_samples64(const double *__restrict__ seq, D4 *__restrict__ accum,
+                                                          uint32_t n_pixels, uint32_t n_samples, double count) {
+    const uint32_t p = blockIdx.x * 256u + threadIdx.x;
+    if (p >= n_pixels) return;
+    D4 acc = accum[p];
+    for (uint32_t j = 0; j < n_samples; ++j) {
+        const double *v = seq + 3u * ((size_t)j * n_pixels + p);
+        acc.x = acc.x + v[0];
+        acc.y = acc.y + v[1];
+        acc.z = acc.z + v[2];
+    }
+    accum[p] = D4{acc.x, acc.y, acc.z, count};
+}
+
 // f64 sums rounded to the ABI's f32 RGBA accum (round to nearest: the closest f32 to each sum).
 __global__ __launch_bounds__(256) void rrt_accum64_to_f32(const D4 *__restrict__ a64, float4 *__restrict__ a32,
                                                           uint32_t n_pixels) {
@@ -826,7 +1045,9 @@ size_t lds64_bytes(const KParams &p, int mode) {
     if (mode != kF64Global)
         lds += (size_t)p.n_nodes * 112u +
                (size_t)p.n_prims * ((mode == kF64LdsWide ? sizeof(Sphere64) : sizeof(float4)) +
-                                    (p.inv_r_in_lds ? sizeof(double) : 0u));
+                                    (p.inv_r_in_lds ? sizeof(double) : 0u) +
+                                    (mode == kF64LdsWide && p.rec32_in_lds ? sizeof(float4) : 0u)) +
+               (p.inv_r_in_lds ? 8u : 0u);  // the f32 records start 16-B aligned
     return lds;
 }
 
@@ -838,6 +1059,7 @@ size_t f64_lds_min_bytes(uint32_t n_nodes, uint32_t n_prims, uint32_t stack_dept
     p.n_prims = n_prims;
     p.stack_depth = stack_depth;
     p.inv_r_in_lds = 0u;
+    p.rec32_in_lds = 0u;
     return lds64_bytes(p, kF64Lds);
 }
 
@@ -852,7 +1074,11 @@ hipError_t launch64(const KParams &p, bool count, hipStream_t stream) {
     if (e != hipSuccess) return e;
     if (per_cu < 1) per_cu = 1;
     const uint32_t want = (p.n_units + kBlock64 - 1) / kBlock64;
-    const uint32_t blocks = std::max<uint32_t>(std::min<uint32_t>(want, (uint32_t)per_cu * p.n_cus), kQueues);
+    uint32_t blocks = std::max<uint32_t>(std::min<uint32_t>(want, (uint32_t)per_cu * p.n_cus), kQueues);
+    if (RRT_F64_B2F) {  // every lane needs a history slot
+        if (!p.hist || p.hist_lanes < kQueues * (uint32_t)kBlock64) return hipErrorInvalidValue;
+        blocks = std::min<uint32_t>(blocks, p.hist_lanes / (uint32_t)kBlock64);
+    }
     e = hipMemsetAsync(p.unit_counter, 0, kQueues * 32u * sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(kernel, dim3(blocks), dim3(kBlock64), lds, stream, p);
@@ -864,19 +1090,40 @@ hipError_t launch64(const KParams &p, bool count, hipStream_t stream) {
 #ifndef RRT_F64_WIDE_SPHERES
 #define RRT_F64_WIDE_SPHERES 1
 #endif
+// rrt_testing_f64_layout: a forced LDS layout (bit 0: widened Sphere64 records, bit 1: the 1/r table,
+// bit 2: the f32 pre-test records beside widened ones), or -1 for the automatic choice below
+std::atomic<int> g_f64_layout{-1};
+
 template <int kClass>
 hipError_t launch64_placed(const KParams &p, bool count, hipStream_t stream) {
     if (!p.scene_in_lds) return launch64<kF64Global, kClass>(p, count, stream);
+    if (const int lay = g_f64_layout.load(); lay >= 0) {
+        KParams q = p;
+        const bool wide = (lay & 1) != 0;
+        q.inv_r_in_lds = (lay & 2) ? 1u : 0u;
+        q.rec32_in_lds = wide && (lay & 4) ? 1u : 0u;
+        if (lds64_bytes(q, wide ? kF64LdsWide : kF64Lds) > 64u * 1024u) return hipErrorInvalidValue;
+        return wide ? launch64<kF64LdsWide, kClass>(q, count, stream) : launch64<kF64Lds, kClass>(q, count, stream);
+    }
     // the widened sphere records and the 1/r table join the staged scene while the block stays
     // within the 64 KB it may declare
     // (widened records before the 1/r table: a sphere test reads a record, a hit reads 1/r)
     KParams q = p;
-    if (RRT_F64_WIDE_SPHERES) {
-        for (const uint32_t inv_r : {1u, 0u}) {
-            q.inv_r_in_lds = inv_r;
-            if (lds64_bytes(q, kF64LdsWide) <= 64u * 1024u) return launch64<kF64LdsWide, kClass>(q, count, stream);
+    q.rec32_in_lds = 0u;
+#ifndef RRT_F64_PREFER_F32REC
+#define RRT_F64_PREFER_F32REC 0
+#endif
+    if (RRT_F64_WIDE_SPHERES && !(RRT_F64_PREFER_F32REC && p.sphere32)) {
+        // with the pre-test: the f32 records staged too, or read from global memory (L1 / L2)
+        for (const uint32_t rec32 : {p.sphere32 && RRT_F64_SPHERE32 ? 1u : 0u, 0u}) {
+            q.rec32_in_lds = rec32;
+            for (const uint32_t inv_r : {1u, 0u}) {
+                q.inv_r_in_lds = inv_r;
+                if (lds64_bytes(q, kF64LdsWide) <= 64u * 1024u) return launch64<kF64LdsWide, kClass>(q, count, stream);
+            }
         }
     }
+    q.rec32_in_lds = 0u;
     q.inv_r_in_lds = 1u;
     if (lds64_bytes(q, kF64Lds) > 64u * 1024u) q.inv_r_in_lds = 0u;
     return launch64<kF64Lds, kClass>(q, count, stream);
@@ -895,12 +1142,49 @@ hipError_t launch_render_pass_f64(const KParams &p, bool count, hipStream_t stre
     if (RRT_F64_CLASSES && !p.specular) e = launch64_placed<kF64Diffuse>(p, count, stream);
     else if (RRT_F64_CLASSES && !p.image_tex) e = launch64_placed<kF64Untextured>(p, count, stream);
     else e = launch64_placed<kF64Full>(p, count, stream);
-    if (e != hipSuccess || p.n_chunks <= 1) return e;
+    if (e != hipSuccess || p.n_chunks <= 1 || p.seq) return e;
     const uint32_t n_pixels = p.tile_rows * p.width;
     hipLaunchKernelGGL(rrt_combine_chunks64, dim3((n_pixels + 255) / 256), dim3(256), 0, stream, p.partial64,
                        p.accum64, n_pixels, p.pass_n, p.chunk_begin == 0 ? 1u : 0u,
                        (double)(p.sample_end - p.sample_begin));
     return hipGetLastError();
+}
+
+void set_f64_layout(int layout) { g_f64_layout.store(layout < 0 ? -1 : layout & 7); }
+
+// Passes of the sequential-sum schedule: the first holds the prefix chunk (chunk 0) and up to
+// pass_chunks tail chunks, each later one up to pass_chunks tail chunks; after a pass its tail samples
+// are folded into accum64 in order.
+hipError_t launch_render_f64_seq(const KParams &p, bool count, hipStream_t stream) {
+    const uint32_t n_tail = p.n_chunks > 0 ? p.n_chunks - 1u : 0u, m = std::max(1u, p.pass_chunks);
+    const uint32_t n_pixels = p.tile_rows * p.width;
+    const uint32_t S = p.sample_end - p.sample_begin;
+    uint32_t cb = 0;
+    while (cb < p.n_chunks) {
+        KParams q = p;
+        q.chunk_begin = cb;
+        q.pass_big = cb == 0 ? std::min(1u, p.n_big) : 0u;
+        q.pass_n = cb == 0 ? 1u + std::min(m, n_tail) : std::min(m, p.n_chunks - cb);
+        if (p.n_big == 0) q.pass_n = p.n_chunks;  // one chunk: the whole pixel
+        q.n_big_units = p.n_work_tiles * q.pass_big * 64u;
+        q.n_units = p.n_work_tiles * q.pass_n * 64u;
+        q.fd_pass_big = make_fastdiv(q.pass_big);
+        q.fd_pass_tail = make_fastdiv(q.pass_n - q.pass_big);
+        const uint32_t end = cb + q.pass_n;
+        const uint32_t tail0 = std::max(cb, p.n_big);  // the pass's first tail chunk
+        q.seq_first = tail0 < end ? chunk_first(p, tail0) : 0u;
+        hipError_t e = launch_render_pass_f64(q, count, stream);
+        if (e != hipSuccess) return e;
+        if (tail0 < end) {
+            const uint32_t done = std::min(S, chunk_first(p, end));
+            hipLaunchKernelGGL(rrt_fold_samples64, dim3((n_pixels + 255) / 256), dim3(256), 0, stream, p.seq64,
+                               p.accum64, n_pixels, done - q.seq_first, (double)done);
+            e = hipGetLastError();
+            if (e != hipSuccess) return e;
+        }
+        cb = end;
+    }
+    return hipSuccess;
 }
 
 hipError_t launch_accum64_to_f32(const D4 *d_accum64, float4 *d_accum, uint32_t n_pixels, hipStream_t stream) {

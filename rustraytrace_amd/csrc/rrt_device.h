@@ -109,7 +109,7 @@ __device__ __forceinline__ RngState path_rng_k(uint64_t key, uint32_t s) { retur
 
 // First sample (relative to sample_begin) of chunk c of a pixel (rrt_accum_chunk's schedule).
 template <class KP>
-__device__ __forceinline__ uint32_t chunk_first(const KP &P, uint32_t c) {
+__host__ __device__ __forceinline__ uint32_t chunk_first(const KP &P, uint32_t c) {
     return c < P.n_big ? c * P.chunk : P.n_big * P.chunk + (c - P.n_big) * P.chunk_small;
 }
 

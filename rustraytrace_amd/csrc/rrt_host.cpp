@@ -850,7 +850,11 @@ FlatBvh scene_bvh(const RrtSphere *spheres, uint32_t n_spheres, const ExtView &e
     FlatBvh fb = build_bvh(spheres, n_spheres, ex, width, max_leaf, f64 ? f64_node_cost_lds() : kNodeCost, order, fit);
     if (fb.stride == (uint32_t)sizeof(rrt::GNode)) return fb;
     fb = build_bvh(spheres, n_spheres, ex, width, std::min(max_leaf, max_leaf_global()), kNodeCost, order, fit);
-    if (f64 && fb.n_nodes > 65535u) fb = build_bvh(spheres, n_spheres, ex, width, max_leaf, kNodeCost, order, fit);
+    // the caller's leaf size when single-primitive leaves need more than the f64 kernel's 16-bit
+    // links, or a deeper stack than the kernels hold (coincident spheres: the SAH sweep splits ties
+    // 1 | n - 1, so a cluster of n turns into a chain n deep)
+    if ((f64 && fb.n_nodes > 65535u) || fb.stack_need > (uint32_t)rrt::kMaxStackDepth)
+        fb = build_bvh(spheres, n_spheres, ex, width, max_leaf, kNodeCost, order, fit);
     return fb;
 }
 
@@ -880,6 +884,10 @@ struct RrtScene {
     rrt::D4 *d_partial64 = nullptr;                 // its chunk partial sums
     size_t partial64_cap = 0;                       // D4 elements
     rrt::D4 *d_accum64 = nullptr;                   // its f64 sums behind the float entry points
+    double *d_seq64 = nullptr;                      // f64: tail-sample radiances of a pass
+    size_t seq64_cap = 0;                           // doubles
+    float *d_hist = nullptr;                        // f64: the lanes' attenuation histories
+    size_t hist_cap = 0;                            // bytes
     size_t accum64_cap = 0;                         // D4 elements
     uint32_t last_groups = 0, last_passes = 0;      // the last launch: 64-unit groups per pass, passes
     rrt::KParams base{};
@@ -909,6 +917,8 @@ void free_scene(RrtScene *s) {
     (void)hipFree(s->d_partial);
     (void)hipFree(s->d_partial64);
     (void)hipFree(s->d_accum64);
+    (void)hipFree(s->d_seq64);
+    (void)hipFree(s->d_hist);
     delete s;
 }
 
@@ -962,6 +972,19 @@ size_t partial_budget() {
     return mb << 20;
 }
 
+// The f64 path's tail-sample radiances (24 B per sample): 8 GiB unless RRT_PARTIAL_MB says
+// otherwise — C2's 64 tail samples of 2.07 M pixels (3.2 GB) in one pass of the 288-GB HBM.
+size_t seq_budget() {
+    if (std::getenv("RRT_PARTIAL_MB")) return partial_budget();
+    return (size_t)8192 << 20;
+}
+#ifndef RRT_F64_SEQ
+#define RRT_F64_SEQ 1
+#endif
+#ifndef RRT_F64_TAIL_DIV
+#define RRT_F64_TAIL_DIV 8
+#endif
+
 int fill_params(RrtScene *s, const RrtTile *t, float *d_accum, rrt::KParams &p) {
     p = s->base;
     p.accum = reinterpret_cast<float4 *>(d_accum);
@@ -981,11 +1004,27 @@ int fill_params(RrtScene *s, const RrtTile *t, float *d_accum, rrt::KParams &p) 
         const uint32_t k0 = p.chunk;
         while (p.chunk > std::max(1u, k0 / 4u) && S <= 2u * p.chunk) p.chunk /= 2u;
     }
-    if (const char *e = std::getenv("RRT_CHUNK_FORCE")) p.chunk = (uint32_t)std::max(1, std::atoi(e));  // A/B only
+#ifdef RRT_CHUNK_FORCE  // A/B builds only (tools/build_variants.sh): a fixed chunk outside the ABI's rule
+    p.chunk = std::max(1u, (uint32_t)RRT_CHUNK_FORCE);
+#endif
     p.chunk_small = std::max(1u, p.chunk / 8u);
     p.n_big = S > p.chunk ? (S - 1u) / p.chunk : 0u;
     const uint32_t tail = S - p.n_big * p.chunk;
     p.n_chunks = S ? p.n_big + (tail + p.chunk_small - 1u) / p.chunk_small : 0u;
+    p.seq = 0u;
+    if (s->f64 && RRT_F64_SEQ && S) {
+        // The f64 books path sums each pixel's samples in camera.rs:72-76's order: one prefix chunk
+        // of S - T samples (summed in the lane from 0), then T tail samples in chunks of K/8 whose
+        // radiances are kept one by one and folded in after the pass. T = S/8 in whole tail chunks:
+        // the tail chunks balance the queue's drain like the f32 schedule's, at 24 B per sample.
+        const uint32_t ts = p.chunk_small;
+        const uint32_t t_samples = S >= 2u * ts ? (S / RRT_F64_TAIL_DIV) / ts * ts : 0u;
+        p.seq = 1u;
+        p.n_big = 1u;
+        p.chunk = S - t_samples;
+        p.chunk_small = ts;
+        p.n_chunks = 1u + t_samples / ts;
+    }
     const uint64_t units = (uint64_t)p.n_work_tiles * p.n_chunks * 64u;
     if (units > 0xFFFFFFFFull) return fail(RRT_E_INVALID, "tile too large: more than 2^32 work units");
     p.n_units = (uint32_t)units;
@@ -1000,7 +1039,21 @@ int fill_params(RrtScene *s, const RrtTile *t, float *d_accum, rrt::KParams &p) 
     p.fd_pass_tail = rrt::make_fastdiv(p.n_chunks - p.n_big);
     p.unit_counter = s->d_unit_counter;
     p.pass_chunks = p.n_chunks;
-    if (p.n_chunks > 1) {  // partial sums [pass chunk][pixel], within the partial budget; grow on demand
+    if (p.seq && p.n_chunks > 1) {  // per-sample tail radiances [pass tail sample][pixel], within the budget
+        const size_t n_px = std::max<size_t>((size_t)p.tile_rows * p.width, 1);
+        const size_t per_chunk = n_px * p.chunk_small * 3u * sizeof(double);
+        const uint32_t n_tail = p.n_chunks - 1u;
+        p.pass_chunks = (uint32_t)std::min<size_t>(n_tail, std::max<size_t>(1, seq_budget() / per_chunk));
+        const size_t need = per_chunk * p.pass_chunks / sizeof(double);
+        if (need > s->seq64_cap) {
+            HIP_TRY(hipSetDevice(s->device), "hipSetDevice");
+            (void)hipFree(s->d_seq64);
+            s->d_seq64 = nullptr;
+            s->seq64_cap = 0;
+            HIP_TRY(hipMalloc((void **)&s->d_seq64, need * sizeof(double)), "hipMalloc tail sample radiances");
+            s->seq64_cap = need;
+        }
+    } else if (p.n_chunks > 1) {  // partial sums [pass chunk][pixel], within the partial budget; grow on demand
         const size_t n_px = std::max<size_t>((size_t)p.tile_rows * p.width, 1);
         const size_t elem = s->f64 ? sizeof(rrt::D4) : sizeof(rrt::F3);
         p.pass_chunks = (uint32_t)std::min<size_t>(p.n_chunks, std::max<size_t>(1, partial_budget() / (n_px * elem)));
@@ -1018,7 +1071,25 @@ int fill_params(RrtScene *s, const RrtTile *t, float *d_accum, rrt::KParams &p) 
     }
     p.partial = s->d_partial;
     p.partial64 = s->d_partial64;
+    p.seq64 = s->d_seq64;
     p.accum64 = nullptr;
+    if (s->f64) {  // the attenuation history: max_depth records of 12 B per lane slot
+        const uint64_t per_lane = (uint64_t)std::max(1u, p.max_depth) * 12u;
+        uint64_t lanes = (uint64_t)p.n_cus * 1024u;  // 4 waves per SIMD x 4 SIMDs x 64 (the f64 kernel's bound)
+        lanes = std::min<uint64_t>(lanes, (4ull << 30) / per_lane / 512u * 512u);
+        if (lanes < 8u * 512u) return fail(RRT_E_INVALID, "RRT_FLAG_F64: max_depth too large for the attenuation history");
+        const size_t need = (size_t)(lanes * per_lane);
+        if (need > s->hist_cap) {
+            HIP_TRY(hipSetDevice(s->device), "hipSetDevice");
+            (void)hipFree(s->d_hist);
+            s->d_hist = nullptr;
+            s->hist_cap = 0;
+            HIP_TRY(hipMalloc((void **)&s->d_hist, need), "hipMalloc attenuation history");
+            s->hist_cap = need;
+        }
+        p.hist = s->d_hist;
+        p.hist_lanes = (uint32_t)(s->hist_cap / per_lane);
+    }
     return RRT_OK;
 }
 
@@ -1341,6 +1412,15 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
     p.prim_mtl = s->d_prim_mtl;
     p.prim_inv_r64 = s->d_prim_inv_r64;
     p.prim_diel64 = s->d_prim_diel64;
+    // the f64 kernel's f32 sphere pre-test (rrt_sphere32.h) holds for centers and radii within 2^20
+    p.sphere32 = 0u;
+    if (f64) {
+        bool in = true;
+        for (uint32_t i = 0; i < n_prims && in; ++i)
+            for (int k = 0; k < 4; ++k) in = in && std::fabs((&prim_cr[i].x)[k]) <= 0x1.0p20f;
+        p.sphere32 = in ? 1u : 0u;
+        if (const char *e = std::getenv("RRT_F64_PRETEST")) p.sphere32 = p.sphere32 && std::atoi(e) != 0;
+    }
     p.prim_motion = s->d_prim_motion;
     p.perlin = s->d_perlin;
     p.n_perlin = n_perlin;
@@ -1652,6 +1732,11 @@ int32_t rrt_scene_count_work(RrtScene *scene, const RrtTile *tile, RrtCounters *
 // devices.
 static std::atomic<bool> g_device_wrap{false};
 extern "C" void rrt_testing_device_wrap(int32_t on) { g_device_wrap.store(on != 0); }
+
+// Test mode (rrt_testing_f64_layout, a test-only entry point): the f64 kernel stages a scene that fits
+// the block's LDS in the given layout instead of its automatic choice (every layout renders the same
+// bits; tests/test_gpu_books64.py reaches each fallback with it). -1 restores the automatic choice.
+extern "C" void rrt_testing_f64_layout(int32_t layout) { rrt::set_f64_layout(layout); }
 
 extern "C" int32_t rrt_testing_recip_check(uint64_t *mismatches) {
     if (!mismatches) return fail(RRT_E_INVALID, "null mismatches");

@@ -235,6 +235,22 @@ struct KParams {
     // per leaf-order primitive, a dielectric's (1 / eta, r0(1 / eta), r0(eta), 0) in f64, formed on
     // the host in the reference's operations (material.rs:75-102); zeros for other materials
     const double4 *prim_diel64;
+    // the f32 sphere pre-test (rrt_sphere32.h) is enabled: every sphere center and radius within
+    // 2^20 (its proven domain); rec32_in_lds: the widened-record layout also stages the f32 records
+    uint32_t sphere32;
+    uint32_t rec32_in_lds;
+    // The f64 books path's summation in camera.rs:72-76's order (seq = 1): each pixel's first
+    // S - T samples are one chunk summed from 0 in the lane (written to accum64 with w = S - T), the
+    // last T samples tail chunks whose per-sample radiances go to seq64 ([tail sample of the pass]
+    // [tile pixel] x 3 doubles; seq_first = the pass's first tail sample, relative to sample_begin),
+    // folded into accum64 in sample order after the pass (launch_render_f64_seq).
+    uint32_t seq;
+    uint32_t seq_first;
+    double *seq64;
+    // the f64 path's attenuation history ([bounce][lane slot] x 3 floats, rrt_books64.hip
+    // fold_back64): max_depth x hist_lanes records; the launch keeps blocks x threads <= hist_lanes
+    float *hist;
+    uint32_t hist_lanes;
 };
 
 // RRT_FLAG_F64 (include/rrt_hip.h): the f64 books-arithmetic kernel (rrt_books64.hip)
@@ -292,9 +308,14 @@ hipError_t launch_recip_check(unsigned long long *d_out, hipStream_t stream);
 // Implemented in rrt_books64.hip: one sample pass of the f64 books kernel (+ its chunk combine)
 // into p.accum64, and the f64 sums rounded to the f32 RGBA accum of the ABI.
 hipError_t launch_render_pass_f64(const KParams &p, bool count, hipStream_t stream);
+// The f64 render in sequential-sum mode (p.seq): the prefix + tail-chunk passes and the in-order
+// folds of the tail samples (rrt_books64.hip).
+hipError_t launch_render_f64_seq(const KParams &p, bool count, hipStream_t stream);
 // LDS of the f64 kernel's block with the scene staged in its smallest form (Node112 nodes, f32
 // sphere records, no 1/r table): the host stages an f64 scene only when this is <= 64 KB
 size_t f64_lds_min_bytes(uint32_t n_nodes, uint32_t n_prims, uint32_t stack_depth);
 hipError_t launch_accum64_to_f32(const D4 *d_accum64, float4 *d_accum, uint32_t n_pixels, hipStream_t stream);
+// Test support (rrt_testing_f64_layout): force the f64 kernel's LDS layout of a staged scene (-1: auto)
+void set_f64_layout(int layout);
 
 }  // namespace rrt

@@ -43,6 +43,11 @@ namespace {
 #ifndef RRT_PHASE_TIMING
 #define RRT_PHASE_TIMING 0
 #endif
+// Debug builds only: random_unit_vector takes its first candidate (wrong images; prices the
+// rejection loop's wave-iterations in an A/B)
+#ifndef RRT_DEBUG_NOREJECT
+#define RRT_DEBUG_NOREJECT 0
+#endif
 // Wave issue priority per loop phase (s_setprio levels 0-3; see the work loop's head).
 #ifndef RRT_PRIO_REFILL
 #define RRT_PRIO_REFILL 2
@@ -94,7 +99,7 @@ __device__ __forceinline__ float recip_rn(float s) {
     return e == e ? __builtin_fmaf(e, r, r) : r;
 }
 
-// sqrt(x) correctly rounded for x = 0 or x >= 2^-96 (and +inf, NaN): v_sqrt_f32 and the choice
+// sqrt(x) correctly rounded for x = +-0 or |x| >= 2^-96 (negative x: NaN, as IEEE; +-inf, NaN): v_sqrt_f32 and the choice
 // between its one-ulp neighbours by the sign of the fma remainders — the compiler's own correction
 // without the rescaling of small arguments (exhaustive on the device, rrt_testing_recip_check). The
 // kernel takes it where the argument is provably 0 or >= 2^-46: |p|^2 of the rejection loop, and
@@ -136,7 +141,7 @@ __device__ __forceinline__ V3 random_unit_vector(RngState &s, C &cnt) {
         py = rnd_pm1(s);
         pz = rnd_pm1(s);
         lensq = __builtin_fmaf(pz, pz, __builtin_fmaf(py, py, px * px));
-        if (0.0f < lensq && lensq <= 1.0f) break;
+        if (RRT_DEBUG_NOREJECT || (0.0f < lensq && lensq <= 1.0f)) break;  // (debug: first candidate)
     }
     const float inv = recip_rn(sqrt_rn_big(lensq));  // lensq >= 2^-46
     return v3(px * inv, py * inv, pz * inv);
@@ -1774,6 +1779,7 @@ hipError_t launch_render_pass(const KParams &p, bool count, hipStream_t stream) 
 
 // One launch (+ combine) per sample pass of at most p.pass_chunks chunks, in chunk order.
 hipError_t launch_render_kernel(const KParams &p, bool count, hipStream_t stream) {
+    if ((p.flags & kFlagF64) && p.seq) return launch_render_f64_seq(p, count, stream);
     if (p.n_chunks <= 1 || p.pass_chunks == 0 || p.pass_chunks >= p.n_chunks) {
         KParams q = p;
         q.chunk_begin = 0;
@@ -1826,7 +1832,8 @@ __global__ __launch_bounds__(256) void rrt_recip_check(unsigned long long *out) 
         const bool special = a == 0u || a >= 0x7f800000u;
         if ((normal || special) && !same(recip_rn(s), 1.0f / s)) ++bad0;
         if ((a < 0x7e800000u || a > 0x7f800000u) && !same(clamped_slope(s), clamp_inv(1.0f / s))) ++bad1;
-        if ((u == 0u || (u >= 0x0f800000u && u < 0x80000000u)) && !same(sqrt_rn_big(s), __builtin_sqrtf(s))) ++bad2;
+        // +-0 and every |s| >= 2^-96 of either sign (negatives: NaN like the IEEE root; -0: -0), +-inf, NaN
+        if ((a == 0u || a >= 0x0f800000u) && !same(sqrt_rn_big(s), __builtin_sqrtf(s))) ++bad2;
     }
     if (bad0) atomicAdd(&out[0], (unsigned long long)bad0);
     if (bad1) atomicAdd(&out[1], (unsigned long long)bad1);

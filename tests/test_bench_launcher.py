@@ -54,3 +54,33 @@ def test_forwarder_passes_one_line_and_exit_status(capsys):
     assert out.strip() == json.dumps({"metric": "m", "value": 1}) and "rank chatter" in err
     assert bench.run_launcher([sys.executable, "-c", "import sys; sys.exit(3)"]) == 3
     assert bench.run_launcher([sys.executable, "-c", "print('no line')"]) == 1
+
+
+def test_device_shortfall_decision():
+    assert bench.device_shortfall("nccl", 0, 1) is None
+    assert bench.device_shortfall("nccl", 7, 8) is None
+    assert "needs GPU 1" in bench.device_shortfall("nccl", 1, 1)
+    assert bench.device_shortfall("nccl", 0, 0) is not None
+    assert bench.device_shortfall("gloo", 5, 1) is None  # rehearsal ranks share the GPUs
+
+
+def test_short_box_fails_fast_under_an_external_launcher():
+    # one rank of an N-GPU job on a box with too few devices (here: none) exits non-zero with the
+    # message, before any rendezvous
+    env = dict(os.environ, WORLD_SIZE="2", RANK="1", LOCAL_RANK="1", MASTER_ADDR="127.0.0.1", MASTER_PORT="29533",
+               CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], env=env, capture_output=True,
+                       text=True, timeout=240)
+    assert r.returncode == 2, (r.returncode, r.stderr[-2000:])
+    assert "needs GPU 1" in r.stderr and r.stdout.strip() == ""
+
+
+def test_short_box_fails_fast_through_the_self_launch():
+    # bench.py --gpus 2 starting its own ranks on a box with no visible device: every rank stops
+    # before the rendezvous and the parent returns non-zero (no hang)
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode != 0 and "needs GPU" in r.stderr, (r.returncode, r.stderr[-2000:])

@@ -4,11 +4,17 @@ seed (per-channel float tolerance <= 1e-4 before u8 quantisation; bit-exact PPM 
 
 The kernel runs the books path's arithmetic (vec3.rs, sphere.rs:24-51, material.rs, camera.rs:
 152-209 in f64, unfused, the reference's operation order) on the same per-path random stream, so
-every path takes the same decisions as BOOKS: the closest-hit query counts are equal, and the only
-difference left is the throughput product's association (BOOKS multiplies back to front through
-its recursion, the kernel front to back) — a few f64 ulps per pixel sum. Bars, with the tolerance
-written here: every channel |gpu - books| / S <= 1e-4 (the north star's; measured max ~1e-15), the
-query counts equal, and the bytes of color.rs's f64 quantiser equal for every pixel.
+every path takes the same decisions as BOOKS and the closest-hit query counts are equal. It also
+forms each path's radiance back to front like BOOKS' recursion (the attenuation history,
+rrt_books64.hip fold_back64) and sums each pixel's samples in sample order like camera.rs:72-76
+(`pixel_color += ray_color(..)`: a prefix chunk summed in the lane, the tail samples folded in after
+the pass). So its f64 sums equal BOOKS' (the oracle's default for BOOKS: sequential sums) bit for
+bit, and the bars written here are: every sum bit-identical (which implies the north star's
+per-channel |gpu - books| / S <= 1e-4 and equal PPM bytes, both still checked and printed), the
+query counts equal. The comparison against BOOKS summed in the f32 kernel's chunk schedule (the
+round-4 order) is printed for reference, within 1e-4. Full-size rows also report how many channels
+sit within 1e-12 (relative) of a quantisation step of color.rs: the bytes a last-ulp difference in
+the sum could have moved, which the bit-identical sums rule out.
 """
 import numpy as np
 import pytest
@@ -42,7 +48,18 @@ def _gpu_f64(scene, rows=None):
     return out, out32, rays
 
 
-def _check(scene, gpu, books, label):
+def _step_exposure(books, S):
+    """Channels of the f64 sums whose color.rs value 256 clamp(sqrt(v / S), 0, .999) lies within
+    1e-12 (relative) of an integer step: the ones a last-ulp change of the sum could move a byte."""
+    v = np.sqrt(np.maximum(books[..., :3] / S, 0.0))
+    x = 256.0 * np.minimum(v, 0.999)
+    near = np.abs(x - np.round(x)) <= 1e-12 * np.maximum(x, 1e-300)
+    return int((near & (x > 0)).sum())
+
+
+def _check(scene, gpu, books, label, bar="bits"):
+    """bar: "bits" (every sum identical; implies the rest), "bytes" (within 1e-4 and every PPM byte
+    equal: the north star's bars), "tol" (within 1e-4 only)."""
     S = scene.spp
     assert np.array_equal(gpu[..., 3], books[..., 3])  # w = sample count
     err = np.abs(gpu[..., :3] - books[..., :3]) / S
@@ -51,9 +68,14 @@ def _check(scene, gpu, books, label):
     q_gpu = rrt.quantize_accum_books_f64(scene.width, gpu.shape[0], np.ascontiguousarray(gpu), S)
     q_books = rrt.quantize_accum_books_f64(scene.width, books.shape[0], np.ascontiguousarray(books), S)
     u8_equal = float((q_gpu == q_books).mean())
-    print(f"{label}: max |diff|/S {err.max():.3e} max rel {rel:.3e} within 1e-4 {within:.6f} u8 equal {u8_equal:.6f}")
+    nbits = int((gpu[..., :3] != books[..., :3]).sum())
+    print(f"{label}: max |diff|/S {err.max():.3e} max rel {rel:.3e} within 1e-4 {within:.6f} u8 equal {u8_equal:.6f}"
+          f" bit-differing channels {nbits} of {books[..., :3].size}")
     assert within == 1.0, f"{label}: {1 - within:.2e} of channels outside {TOL}"
-    assert u8_equal == 1.0, f"{label}: {int((q_gpu != q_books).sum())} PPM bytes differ"
+    if bar in ("bits", "bytes"):
+        assert u8_equal == 1.0, f"{label}: {int((q_gpu != q_books).sum())} PPM bytes differ"
+    if bar == "bits":
+        assert nbits == 0, f"{label}: {nbits} channels differ in their bits"
     return rel
 
 
@@ -61,10 +83,11 @@ def _check(scene, gpu, books, label):
 def test_f64_kernel_matches_books_path(cfg):
     scene = rrt.config_scene(cfg, image_width=64, samples_per_pixel=256)
     gpu, gpu32, gpu_rays = _gpu_f64(scene)
-    books, books_rays, _ = oracle.render(scene, oracle.BOOKS, threads=16)
+    books, books_rays, _ = oracle.render(scene, oracle.BOOKS, threads=16)  # camera.rs:72-76's order
     assert gpu_rays == books_rays, f"{cfg}: {gpu_rays} closest-hit queries vs BOOKS {books_rays}"
-    rel = _check(scene, gpu, books, cfg)
-    assert rel < 1e-12  # a few f64 ulps of throughput association, nothing else
+    _check(scene, gpu, books, cfg)
+    chunked, _, _ = oracle.render(scene, oracle.BOOKS, threads=16, chunk=oracle.DEFAULT_CHUNK)
+    _check(scene, gpu, chunked, f"{cfg} vs BOOKS in the f32 chunk schedule", bar="tol")
     assert np.array_equal(gpu32, gpu.astype(np.float32))
     # the PPM the books path prints (camera.rs:87-94) and the one from the GPU's f64 sums
     q = rrt.quantize_accum_books_f64(scene.width, scene.height, gpu, scene.spp)
@@ -89,6 +112,8 @@ def test_f64_full_size_rows_match_books(cfg, rows):
     y0, y1 = rows
     books, _, _ = oracle.render(scene, oracle.BOOKS, rows=rows, threads=16)
     _check(scene, gpu[y0:y1], books, f"{cfg} rows {y0}-{y1}")
+    print(f"{cfg} rows {y0}-{y1}: {_step_exposure(books, scene.spp)} of {books[..., :3].size} channels within "
+          f"1e-12 (relative) of a color.rs quantisation step")
     assert np.all(gpu[..., 3] == scene.spp)
     assert np.isfinite(gpu).all()
 
@@ -132,9 +157,46 @@ def test_f64_full_class_matches_books_path():
     gpu, gpu32, gpu_rays = _gpu_f64(scene)
     books, books_rays, _ = oracle.render(scene, oracle.BOOKS, threads=16)
     assert gpu_rays == books_rays, f"{gpu_rays} closest-hit queries vs BOOKS {books_rays}"
-    rel = _check(scene, gpu, books, "textured + specular")
-    assert rel < 1e-12
+    _check(scene, gpu, books, "textured + specular")
     assert np.array_equal(gpu32, gpu.astype(np.float32))
+
+
+# rrt_testing_f64_layout: bit 0 widened Sphere64 records, bit 1 the 1/r table, bit 2 the f32
+# pre-test records beside widened ones
+LAYOUTS = [0, 1, 2, 3, 5, 7]
+
+
+@pytest.mark.parametrize("which", ["C2", "textured_specular"])
+def test_f64_every_lds_layout_renders_the_same_bits(which, monkeypatch):
+    """Each LDS layout the f64 kernel may stage a scene in (launch64_placed's fallbacks for scenes near
+    the block's 64 KB) renders the automatic layout's bits, and those match BOOKS; with the f32
+    sphere pre-test switched off (RRT_F64_PRETEST=0) too."""
+    from rustraytrace_amd import _lib
+
+    lib = _lib.load()
+    scene = (rrt.config_scene("C2", image_width=64, samples_per_pixel=64) if which == "C2"
+             else _textured_specular_scene(image_width=48, samples_per_pixel=64))
+    ref, _, ref_rays = _gpu_f64(scene)
+    books, books_rays, _ = oracle.render(scene, oracle.BOOKS, threads=16)
+    assert ref_rays == books_rays
+    _check(scene, ref, books, f"{which} automatic layout")
+    ran = []
+    try:
+        for lay in LAYOUTS:
+            lib.rrt_testing_f64_layout(lay)
+            try:
+                out, _, rays = _gpu_f64(scene)
+            except rrt.RrtError:
+                continue  # the forced layout exceeds the block's 64 KB for this scene
+            assert rays == ref_rays and np.array_equal(out, ref), f"layout {lay} differs"
+            ran.append(lay)
+    finally:
+        lib.rrt_testing_f64_layout(-1)
+    print(f"{which}: layouts run {ran}")
+    assert set(ran) >= ({0, 1, 2, 3} if which == "C2" else set(LAYOUTS))
+    monkeypatch.setenv("RRT_F64_PRETEST", "0")
+    out, _, rays = _gpu_f64(scene)
+    assert rays == ref_rays and np.array_equal(out, ref), "pre-test off differs"
 
 
 @pytest.mark.parametrize("size,rows", [((64, 256), None), ((None, None), (536, 544))])
@@ -154,4 +216,4 @@ def test_f64_textured_matches_books_with_libm_trig(size, rows):
         gpu = gpu[rows[0]:rows[1]]
     diff = np.abs(gpu[..., :3] - books[..., :3]) / scene.spp
     print(f"C4 vs libm-trig BOOKS: {int((diff > 1e-12).sum())} of {diff.size} channels differ beyond 1e-12")
-    _check(scene, gpu, books, "C4 vs BOOKS (libm acos / atan2)")
+    _check(scene, gpu, books, "C4 vs BOOKS (libm acos / atan2)", bar="bytes")
