@@ -40,6 +40,9 @@ METRIC = "Mrays/sec + wall-clock for 1920×1080×512spp RTOW final scene"
 # (MI355X_MICROARCH.md constants table; cdna_hip_programming.md "CU = 4 x SIMD-32"), so
 # 256 CU x 4 SIMD x 32 lanes x 2 FLOP x 2.4 GHz = 157.3 TFLOP/s; v_pk_fma_f32 has the same peak.
 PEAK_F32_VALU_TFLOPS = 157.3
+# f64 VALU peak: AMD's MI355X spec sheet, 78.6 TFLOP/s vector FP64 — half the FP32 rate (a wave64
+# v_fma_f64 issues in 4 cycles on SIMD-32); MI355X_MICROARCH.md lists FP32 only
+PEAK_F64_VALU_TFLOPS = 78.6
 PEAK_HBM_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E ~8 TB/s
 FLOP_PER_SPHERE_TEST = 23  # sphere.rs:26-31
 FLOP_PER_BOX_TEST = 12  # aabb.rs:56-82 with hoisted reciprocal
@@ -250,7 +253,7 @@ def one_gpu_frame(config="C3", kw=None, device=0):
             "mrays_s": round(rays / wall / 1e6, 2)}
 
 
-def f64_books_frame(config, frames=2):
+def f64_books_frame(config, frames=2, issue_json=None):
     """The same workload through the f64 books-arithmetic kernel (RRT_FLAG_F64, rrt_books64.hip):
     the reference CPU path's own arithmetic on the GPU, which tests/test_gpu_books64.py checks
     against the f64 books restatement (every channel within 1e-4, identical PPM bytes). One warmup
@@ -279,12 +282,52 @@ def f64_books_frame(config, frames=2):
     wall = (time.perf_counter() - t) / frames
     ms = float(np.mean([ev[i].elapsed_time(ev[i + 1]) for i in range(frames)]))
     rays = ds.counters()["rays"] // frames
+    work = ds.count_work(tile)  # the instrumented twin: the books path's sphere and box tests per frame
     ds.close()
+    flops = FLOP_PER_SPHERE_TEST * work["sphere_tests"] + FLOP_PER_BOX_TEST * work["box_tests"]
+    achieved = flops / (ms / 1e3) / 1e12
+    roofline = {
+        "bound": "valu",
+        "achieved": round(achieved, 3),
+        "peak": PEAK_F64_VALU_TFLOPS,
+        "unit": "TFLOP/s",
+        "frac": round(achieved / PEAK_F64_VALU_TFLOPS, 4),
+        "traffic": None,
+        "algorithmic_flop_per_launch": flops,
+        "sphere_tests_per_launch": work["sphere_tests"],
+        "box_tests_per_launch": work["box_tests"],
+        "note": "f64 VALU issue bound: the books path's 23 FLOP per sphere test + 12 FLOP per box test (SURVEY 8d), "
+                "all f64 in the reference, over the HIP-event time of the frame (render passes + in-order folds); "
+                "peak = MI355X FP64 vector 78.6 TFLOP/s (AMD spec: half the FP32 rate). The kernel runs the box test "
+                "and a sphere pre-test in f32 with proven bounds (rrt_box32.h, rrt_sphere32.h), so part of the work "
+                "priced here at f64 issues at the f32 rate",
+    }
+    rec = None
+    path = issue_json or os.path.join(ROOT, "profiles", f"issue_{config}_f64.json")
+    if os.path.exists(path):
+        try:
+            with open(path) as f:
+                rec = json.load(f)
+        except (OSError, ValueError):
+            rec = None
+    if rec and rec.get("f64") and rec.get("config") == config and rec.get("width") == scene.width \
+            and rec.get("spp") == scene.spp:
+        import hashlib
+
+        with open(rrt._lib.LIB_PATH, "rb") as f:
+            same = hashlib.sha256(f.read()).hexdigest() == rec.get("lib_sha256")
+        roofline.update({k: rec[k] for k in ("valu_busy", "lanes_per_valu", "valu_insts_per_ray") if k in rec})
+        roofline["issue_source"] = (f"{os.path.relpath(path, ROOT)}: rocprofv3 --pmc over one f64 {config} launch, "
+                                    f"{'this' if same else 'an earlier'} librrt_hip.so build "
+                                    f"({rec.get('lib_sha256', '')[:12]}); valu_busy counts 2 cycles per VALU "
+                                    f"wave-instruction (an f64 FMA takes 4)")
     return {"workload": f"{config} {scene.width}x{scene.height}x{scene.spp}spp, f64 books arithmetic (RRT_FLAG_F64)",
             "dtype": "f64", "value": round(rays / wall / 1e6, 2), "unit": "Mrays/s", "ms_per_frame": round(wall * 1e3, 3),
             "kernel_ms": round(ms, 3), "rays_per_frame": rays, "frames": frames,
-            "parity": "tests/test_gpu_books64.py: closest-hit counts equal to the f64 books restatement, every "
-                      "channel within 1e-4 (max |diff|/S ~1e-16), every PPM byte equal"}
+            "parity": "tests/test_gpu_books64.py: every f64 pixel sum bit-identical to the books restatement "
+                      "(closest hits, back-to-front throughput and camera.rs:72-76's sequential sums), so every "
+                      "channel within 1e-4 and every PPM byte equal",
+            "roofline": roofline}
 
 
 def reference_gpu_slot(config, budget_s=1.5):

@@ -335,14 +335,37 @@ __device__ __forceinline__ double rr_probability64(D3 att) {
     if (pr > 0.95) pr = 0.95;
     return pr;
 }
+// Debug builds only (RRT_F64_B2F_MODE): 1 = the records stored but the radiance carried front to
+// back (prices the stores), 2 = the fold without its loads (prices the loads); wrong images.
+#ifndef RRT_F64_B2F_MODE
+#define RRT_F64_B2F_MODE 0
+#endif
+// Back to front in groups of RRT_F64_FOLD_GROUP records: a group's loads issue together, then its
+// products in order.
+#ifndef RRT_F64_FOLD_GROUP
+#define RRT_F64_FOLD_GROUP 4
+#endif
 template <bool kTex>
 __device__ __forceinline__ D3 fold_back64(const Att32 *__restrict__ hist, uint32_t lanes, uint32_t slot, uint32_t n,
                                           D3 L) {
-    for (uint32_t k = n; k-- > 0;) {
-        const Att32 a = hist[(size_t)k * lanes + slot];
-        const D3 att = kTex ? d3(att_decode(a.x), att_decode(a.y), att_decode(a.z)) : f2d(a.x, a.y, a.z);
-        L = mul(att, L);
-        if (k >= 5u) L = muls(L, 1.0 / rr_probability64(att));  // Div<f64>: (1/p) * v (vec3.rs:142-148)
+    constexpr uint32_t G = RRT_F64_FOLD_GROUP;
+    uint32_t k = n;
+    while (k > 0u) {
+        const uint32_t m = k < G ? k : G;
+        Att32 a[G];
+#pragma unroll
+        for (uint32_t j = 0; j < G; ++j)
+            if (j < m) a[j] = RRT_F64_B2F_MODE == 2 ? Att32{0.5f, 0.5f, 0.5f} : hist[(size_t)(k - 1u - j) * lanes + slot];
+#pragma unroll
+        for (uint32_t j = 0; j < G; ++j) {
+            if (j < m) {
+                const D3 att = kTex ? d3(att_decode(a[j].x), att_decode(a[j].y), att_decode(a[j].z))
+                                    : f2d(a[j].x, a[j].y, a[j].z);
+                L = mul(att, L);
+                if (k - 1u - j >= 5u) L = muls(L, 1.0 / rr_probability64(att));  // Div<f64>: (1/p) * v (vec3.rs:142-148)
+            }
+        }
+        k -= m;
     }
     return L;
 }
@@ -480,9 +503,11 @@ __device__ __forceinline__ double radius_sq_of(const Sphere64 &c) { return RRT_F
 // discriminant may be >= 0, and the f64 test runs over the marked ones only, in index order (the
 // unmarked ones would `continue` in it). The wave runs the f64 body max-over-lanes of the marked
 // counts instead of the range lengths (C2: 1.17 against 2.21 iterations per leaf batch, measured by
-// RRT_F64_STATS=2). RRT_F64_SPHERE32=0: every sphere runs the f64 test.
+// RRT_F64_STATS=2). Off by default (RRT_F64_SPHERE32=1 builds it): same-box it did not pay — C2
+// -0..-3.5 %, C5 -2.4 % — the f64 sphere tests are not where the f64 kernel's time goes (C2: 54 % of
+// the tests reach disc >= 0 and the traversal loop, node steps included, is half the wave cycles).
 #ifndef RRT_F64_SPHERE32
-#define RRT_F64_SPHERE32 1
+#define RRT_F64_SPHERE32 0
 #endif
 #ifndef RRT_F64_S32_HOLD
 #define RRT_F64_S32_HOLD 0
@@ -534,7 +559,7 @@ __device__ __forceinline__ void leaves64(const Rec *__restrict__ prims, const fl
 
 struct Path64 {
     D3 o, d;
-#if !RRT_F64_B2F
+#if !RRT_F64_B2F || RRT_F64_B2F_MODE == 1
     D3 T;
 #endif
     RngState rng;
@@ -577,7 +602,7 @@ __device__ __forceinline__ void camera_ray64(uint32_t x, uint32_t y, Path64 &ps)
     if (C.flags & 0x1u) (void)rnd64(ps.rng);  // RRT_FLAG_RAY_TIME: the time draw (the_next_week/camera.rs:160)
     ps.o = origin;
     ps.d = sub(sample, origin);
-#if !RRT_F64_B2F
+#if !RRT_F64_B2F || RRT_F64_B2F_MODE == 1
     ps.T = d3(1.0, 1.0, 1.0);
 #endif
     ps.k = 0;
@@ -592,9 +617,19 @@ __device__ __forceinline__ void camera_ray64(uint32_t x, uint32_t y, Path64 &ps)
 // atan2 / texel path compiled out), kF64Diffuse (Lambertian and emissive only: metal and dielectric
 // compiled out), chosen per scene by launch_render_pass_f64 like the f32 kernel's classes.
 constexpr int kF64Full = 0, kF64Untextured = 1, kF64Diffuse = 2;
+// RRT_F64_DEFER = n > 0: a Lambertian scatter's rejection loop (random_unit_vector) draws at most n
+// candidates per pass of the work loop; a lane whose candidates all fail stays at its hit (ps.o = the
+// hit point, ps.d = the normal, `prec` = the attenuation record, `pend` = 1), takes no closest-hit
+// query, and draws on in the next pass. The same draws in the same order (candidates, then Russian
+// roulette's), so the same path: only the wave's schedule changes. The wave no longer runs the
+// loop until its unluckiest lane accepts (~5.6 wave-iterations for ~1.9 candidates per lane).
+#ifndef RRT_F64_DEFER
+#define RRT_F64_DEFER 0
+#endif
 template <int kClass, typename Rec>
 __device__ __forceinline__ bool shade64(const KParams &P, const Rec *prims, const GMaterial *mtl, const double *inv_r,
-                                        Path64 &ps, double t, int prim, D3 &Le, uint32_t slot) {
+                                        Path64 &ps, double t, int prim, D3 &Le, uint32_t slot, uint32_t &pend,
+                                        Att32 &prec) {
     Le = d3(0.0, 0.0, 0.0);
     if (prim < 0) {
         D3 bg;
@@ -605,7 +640,7 @@ __device__ __forceinline__ bool shade64(const KParams &P, const Rec *prims, cons
             const double a = 0.5 * (ud.y + 1.0);
             bg = d3((1.0 - a) * 1.0 + a * 0.5, (1.0 - a) * 1.0 + a * 0.7, (1.0 - a) * 1.0 + a * 1.0);
         }
-#if RRT_F64_B2F
+#if RRT_F64_B2F && RRT_F64_B2F_MODE != 1
         Le = bg;
 #else
         Le = mul(ps.T, bg);
@@ -625,7 +660,7 @@ __device__ __forceinline__ bool shade64(const KParams &P, const Rec *prims, cons
     const int kind = m.b.x;
     const D3 albedo = f2d(m.a.x, m.a.y, m.a.z);
     if (kind == 4) {  // DiffuseLight: emitted, scatter None
-#if RRT_F64_B2F
+#if RRT_F64_B2F && RRT_F64_B2F_MODE != 1
         Le = albedo;
 #else
         Le = mul(ps.T, albedo);
@@ -663,8 +698,6 @@ __device__ __forceinline__ bool shade64(const KParams &P, const Rec *prims, cons
         att = d3(1.0, 1.0, 1.0);
         rec = Att32{1.0f, 1.0f, 1.0f};
     } else {  // Lambertian, plain or image-textured (material.rs:28-40; the_next_week/material.rs:41-53)
-        dir = add(nrm, random_unit_vector(ps.rng));
-        if (__builtin_fabs(dir.x) < 1e-8 && __builtin_fabs(dir.y) < 1e-8 && __builtin_fabs(dir.z) < 1e-8) dir = nrm;
         att = albedo;
         if (kClass != kF64Untextured && kind == 3) {
             const uint32_t b = texel_bytes64(P, m.b.z, outward);
@@ -672,11 +705,20 @@ __device__ __forceinline__ bool shade64(const KParams &P, const Rec *prims, cons
             if (b == 0x1000000u) rec = Att32{0.0f, 1.0f, 1.0f};
             else rec = Att32{-(float)(b & 0xffu), -(float)((b >> 8) & 0xffu), -(float)(b >> 16)};
         }
+        if (RRT_F64_DEFER) {  // the scatter direction is drawn by the work loop (lambert_draw64)
+            ps.o = p;
+            ps.d = nrm;
+            prec = rec;
+            pend = 1;
+            return false;
+        }
+        dir = add(nrm, random_unit_vector(ps.rng));
+        if (__builtin_fabs(dir.x) < 1e-8 && __builtin_fabs(dir.y) < 1e-8 && __builtin_fabs(dir.z) < 1e-8) dir = nrm;
     }
     if (ps.k >= 5u) {  // camera.rs:189-200
         const double pr = rr_probability64(att);
         if (rnd64(ps.rng) > pr) return true;
-#if !RRT_F64_B2F
+#if !RRT_F64_B2F || RRT_F64_B2F_MODE == 1
         ps.T = muls(mul(ps.T, att), 1.0 / pr);
     } else {
         ps.T = mul(ps.T, att);
@@ -692,6 +734,40 @@ __device__ __forceinline__ bool shade64(const KParams &P, const Rec *prims, cons
     ps.d = dir;
     ps.k++;
     return false;
+}
+
+// A pending Lambertian scatter (RRT_F64_DEFER): up to RRT_F64_DEFER candidates of random_unit_vector
+// (vec3.rs:181-189, decided on integers); on acceptance the scatter completes as in shade64 —
+// direction nrm + unit, near_zero (material.rs:33-35), Russian roulette (camera.rs:189-200) and the
+// history record. Returns 1 when the path ended (Russian roulette), 0 otherwise; pend = 0 once done.
+template <int kClass>
+__device__ __forceinline__ uint32_t lambert_draw64(const KParams &P, Path64 &ps, uint32_t slot, uint32_t &pend,
+                                                   const Att32 &prec) {
+    int32_t a = 0, b = 0, c = 0;
+    bool ok = false;
+    for (int it = 0; it < (RRT_F64_DEFER > 0 ? RRT_F64_DEFER : 1) && !ok; ++it) {
+        a = draw_centred(ps.rng);
+        b = draw_centred(ps.rng);
+        c = draw_centred(ps.rng);
+        const uint64_t S = sq_i24(a) + sq_i24(b) + sq_i24(c);
+        ok = S - 1u < (1ull << 46);  // 0 < S <= 2^46
+    }
+    if (!ok) return 0u;
+    pend = 0;
+    const double x = centred_to_pm1(a), y = centred_to_pm1(b), z = centred_to_pm1(c);
+    const double lensq = x * x + y * y + z * z;
+    const D3 nrm = ps.d;
+    D3 dir = add(nrm, muls(d3(x, y, z), 1.0 / __builtin_sqrt(lensq)));
+    if (__builtin_fabs(dir.x) < 1e-8 && __builtin_fabs(dir.y) < 1e-8 && __builtin_fabs(dir.z) < 1e-8) dir = nrm;
+    if (ps.k >= 5u) {
+        const D3 att = kClass != kF64Untextured ? d3(att_decode(prec.x), att_decode(prec.y), att_decode(prec.z))
+                                                : f2d(prec.x, prec.y, prec.z);
+        if (rnd64(ps.rng) > rr_probability64(att)) return 1u;
+    }
+    reinterpret_cast<Att32 *>(P.hist)[(size_t)ps.k * P.hist_lanes + slot] = prec;
+    ps.d = dir;
+    ps.k++;
+    return 0u;
 }
 
 // The persistent work loop of rrt_kernel.hip's render_body (same queue, units, chunk order,
@@ -774,6 +850,8 @@ __device__ __forceinline__ void render64_body(const KParams &P) {
     uint32_t xy = 0, s = 0, s_hi = 0;
     uint32_t px = 0;         // the unit's tile-local pixel index
     uint32_t tail = 0;       // the unit is a tail chunk: its samples' radiances go to seq64 one by one
+    uint32_t pend = 0;       // RRT_F64_DEFER: a Lambertian scatter waits for an accepted candidate
+    Att32 prec{0.0f, 0.0f, 0.0f};
     const uint32_t slot = blockIdx.x * (uint32_t)kBlk + threadIdx.x;  // the lane's history slot
     uint64_t pkey = 0;
     D3 sum = d3(0.0, 0.0, 0.0);
@@ -912,18 +990,22 @@ __device__ __forceinline__ void render64_body(const KParams &P) {
         }
         __builtin_amdgcn_s_setprio(kPrioShade);
         D3 Le = d3(0.0, 0.0, 0.0);
-        if (has && !need_ray && tr.node < 0) {
+        if (has && !need_ray && tr.node < 0 && !pend) {
             need_ray = 1;
-            seg_done = shade64<kClass>(P, prims, mtl, inv_r, ps, tr.closest, tr.hit_prim, Le, slot) ? 1u : 0u;
+            seg_done = shade64<kClass>(P, prims, mtl, inv_r, ps, tr.closest, tr.hit_prim, Le, slot, pend, prec) ? 1u : 0u;
+        }
+        if (RRT_F64_DEFER && pend) {
+            seg_done = lambert_draw64<kClass>(P, ps, slot, pend, prec);
+            need_ray = pend ? 0u : 1u;
         }
         w_paths += (uint32_t)__popcll(__ballot(seg_done));
         if (seg_done) {  // pixel_color += ray_color(..) (camera.rs:72-76)
-#if RRT_F64_B2F
+#if RRT_F64_B2F && RRT_F64_B2F_MODE != 1
             // the radiance at the path's end carried back through its scatters; a path that ended
             // with none (absorbed, Russian roulette, max_depth) adds an exact 0
             if (Le.x != 0.0 || Le.y != 0.0 || Le.z != 0.0)
-                Le = fold_back64<kClass == kF64Full>(reinterpret_cast<const Att32 *>(P.hist), P.hist_lanes, slot,
-                                                     ps.k, Le);
+                Le = fold_back64<kClass != kF64Untextured>(reinterpret_cast<const Att32 *>(P.hist), P.hist_lanes,
+                                                           slot, ps.k, Le);
 #endif
             const auto &Q = *kernarg_params();
             if (tail) {  // a tail sample: its radiance, folded into the pixel's sum in order later
@@ -953,7 +1035,7 @@ __device__ __forceinline__ void render64_body(const KParams &P) {
         }
         if constexpr (RRT_F64_STATS == 1) ph2 += __builtin_amdgcn_s_memtime() - tp;
     }
-    if constexpr (RRT_F64_STATS == 3 && !kCount) {
+    if constexpr ((RRT_F64_STATS == 3 || RRT_F64_STATS == 5) && !kCount) {
         ph0 = wave_sum_u32(cnt.d0);
         ph1 = wave_sum_u32(cnt.d1);
         ph2 = wave_sum_u32(cnt.d2);

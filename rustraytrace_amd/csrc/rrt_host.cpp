@@ -982,7 +982,7 @@ size_t seq_budget() {
 #define RRT_F64_SEQ 1
 #endif
 #ifndef RRT_F64_TAIL_DIV
-#define RRT_F64_TAIL_DIV 8
+#define RRT_F64_TAIL_DIV 4
 #endif
 
 int fill_params(RrtScene *s, const RrtTile *t, float *d_accum, rrt::KParams &p) {
@@ -1007,7 +1007,10 @@ int fill_params(RrtScene *s, const RrtTile *t, float *d_accum, rrt::KParams &p) 
 #ifdef RRT_CHUNK_FORCE  // A/B builds only (tools/build_variants.sh): a fixed chunk outside the ABI's rule
     p.chunk = std::max(1u, (uint32_t)RRT_CHUNK_FORCE);
 #endif
-    p.chunk_small = std::max(1u, p.chunk / 8u);
+#ifndef RRT_TAIL_DIV
+#define RRT_TAIL_DIV 8
+#endif
+    p.chunk_small = std::max(1u, p.chunk / RRT_TAIL_DIV);
     p.n_big = S > p.chunk ? (S - 1u) / p.chunk : 0u;
     const uint32_t tail = S - p.n_big * p.chunk;
     p.n_chunks = S ? p.n_big + (tail + p.chunk_small - 1u) / p.chunk_small : 0u;
@@ -1015,8 +1018,10 @@ int fill_params(RrtScene *s, const RrtTile *t, float *d_accum, rrt::KParams &p) 
     if (s->f64 && RRT_F64_SEQ && S) {
         // The f64 books path sums each pixel's samples in camera.rs:72-76's order: one prefix chunk
         // of S - T samples (summed in the lane from 0), then T tail samples in chunks of K/8 whose
-        // radiances are kept one by one and folded in after the pass. T = S/8 in whole tail chunks:
-        // the tail chunks balance the queue's drain like the f32 schedule's, at 24 B per sample.
+        // radiances are kept one by one and folded in after the pass. T = S/4 in whole tail chunks,
+        // the f32 schedule's share of small units (C2: 128 samples in 8 chunks of 16): it balances the
+        // queue's drain as well as the chunked schedule did (same-box C2 18.75 vs 18.73 Grays/s), at
+        // 24 B per tail sample; T = S/8 left the drain uncovered (-5 %).
         const uint32_t ts = p.chunk_small;
         const uint32_t t_samples = S >= 2u * ts ? (S / RRT_F64_TAIL_DIV) / ts * ts : 0u;
         p.seq = 1u;

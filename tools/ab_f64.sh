@@ -8,7 +8,7 @@ for n in ${VARIANTS:-$(ls variants)}; do
   d=variants/$n
   RRT_LIB_PATH=$d/librrt_hip.so timeout -k 10 300 python bench.py --config ${CONFIG:-C2} --steps 1 --warmup 1 --no-cpu-baseline --no-breakdown --no-extra > gpurun_out/abf_$n.log 2>&1
   rc=$?
-  echo "r$r $n rc=$rc $(python -c "import json;d=json.loads(open('gpurun_out/abf_$n.log').read().splitlines()[-1]);f=d['f64_books'];print(d['value'],'f32 Mrays/s |',f['value'],'f64 Mrays/s',f['ms_per_frame'],'ms')" 2>/dev/null)"
+  echo "r$r ${CONFIG:-C2} $n rc=$rc $(python -c "import json;d=json.loads(open('gpurun_out/abf_$n.log').read().splitlines()[-1]);f=d['f64_books'];print(d['value'],'f32 Mrays/s |',f['value'],'f64 Mrays/s',f['ms_per_frame'],'ms')" 2>/dev/null)" | tee -a gpurun_out/ab_f64_summary.log
   if [ $rc -ne 0 ]; then tail -5 gpurun_out/abf_$n.log; exit $rc; fi
 done
 done
