@@ -302,6 +302,12 @@ def f64_books_frame(config, frames=2, issue_json=None):
                 "and a sphere pre-test in f32 with proven bounds (rrt_box32.h, rrt_sphere32.h), so part of the work "
                 "priced here at f64 issues at the f32 rate",
     }
+    traffic, traffic_src = load_traffic(os.path.join(ROOT, "profiles", f"traffic_{config}_f64.json"), config,
+                                        scene.width, scene.spp, rrt._lib.LIB_PATH)
+    if traffic:  # HBM bytes of the render launch (PMC): the attenuation history and the tail radiances
+        roofline.update({"traffic": traffic, "traffic_source": traffic_src,
+                         "hbm_GBps": round(traffic / (ms / 1e3) / 1e9, 2),
+                         "hbm_frac": round(traffic / (ms / 1e3) / 1e9 / PEAK_HBM_GBPS, 5)})
     rec = None
     path = issue_json or os.path.join(ROOT, "profiles", f"issue_{config}_f64.json")
     if os.path.exists(path):

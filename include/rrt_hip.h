@@ -37,8 +37,10 @@ extern "C" {
  * rrt_quantize_accum_books_f64; 8: RrtTile bands dealt in serpentine order (was b % n_ranks);
  * 9: rrt_accum_chunk() = 256 and the frame's chunk halved while S <= 2K down to a quarter (frames
  * over 512 samples sum in chunks of 256; was 128), rrt_testing_device_wrap, rrt_testing_recip_check
- * (test-only entry points, no drop-in counterpart). */
-#define RRT_ABI_VERSION 9u
+ * (test-only entry points, no drop-in counterpart); 10: tail chunks of K/4 samples (was K/8), the
+ * f64 books path's sums in camera.rs:72-76's sample order with the throughput formed back to front
+ * (bit-identical to the books path), rrt_testing_f64_layout. */
+#define RRT_ABI_VERSION 10u
 
 /* ---- scene ABI (== src/gpu/mod.rs:13-42) ------------------------------------------ */
 
@@ -264,13 +266,15 @@ uint32_t rrt_hip_abi_version(void);
  * (counted from the tile's sample_begin) of each chunk's in-order sample sum, chunks added in
  * order: ((c0 + c1) + c2) + ... With K = rrt_accum_chunk() halved while S <= 2K, down to
  * rrt_accum_chunk() / 4 (ABI v9: 256 for S > 512, 128 for 256 < S <= 512, 64 below; big chunks at
- * high spp, small ones at low spp), and k = max(1, K / 8): the first
+ * high spp, small ones at low spp), and k = max(1, K / 4) (ABI v10; K / 8 before): the first
  * nb = (S - 1) / K chunks hold K samples each (nb = 0 when S <= K), the remaining S - nb*K
  * samples form chunks of k (the last one possibly shorter) — small units at the end of the
  * work queue keep the persistent grid's tail short. Needed to reproduce it bit for bit.
  * The chunk partial sums live in a device buffer of at most RRT_PARTIAL_MB MiB (env, default
  * 2048); a render with more chunks than fit runs as consecutive sample passes of whole chunks,
- * each continuing the same fold, so the bits do not depend on the budget. */
+ * each continuing the same fold, so the bits do not depend on the budget.
+ * The f64 books path (RRT_FLAG_F64) sums each pixel's samples in sample order instead, as
+ * camera.rs:72-76 does: ((s0 + s1) + s2) + ... from 0. */
 uint32_t rrt_accum_chunk(void);
 
 /* ---- device-resident API (bench / multi-rank hosts) --------------------------------- */

@@ -97,6 +97,33 @@ __device__ __forceinline__ double rnd64(RngState &s) { return (double)(rng_next(
 // (half-rate): same draws, same decisions, same accepted point, which is converted once.
 __device__ __forceinline__ int32_t draw_centred(RngState &s) { return (int32_t)(rng_next(s) >> 8) - 8388608; }
 __device__ __forceinline__ uint64_t sq_i24(int32_t a) { return (uint64_t)((int64_t)a * (int64_t)a); }
+// The same decisions from f32 arithmetic where it is provably decisive (RRT_F64_REJ32): the f32
+// sum of squares of the exact coordinates a, b, c (|a| <= 2^23: exact in f32) is within 3u S
+// (u = 2^-24: one rounding per term) of the integer S, so it decides `S <= 2^46` (`S < 2^46` for the
+// disk) outside the band 2^46 (1 +- 2^-21) and `S > 0` exactly (it is 0 only for a = b = c = 0).
+// A wave with a lane in the band (~7e-7 of the candidates) decides those lanes on the integers.
+#ifndef RRT_F64_REJ32
+#define RRT_F64_REJ32 1
+#endif
+constexpr float kRej32Lo = 0x1.fffffp45f;   // 2^46 (1 - 2^-21)
+constexpr float kRej32Hi = 0x1.000008p46f;  // 2^46 (1 + 2^-21)
+// 1: 0 < S <= 2^46 (or S < 2^46 with kDisk), 0: not
+template <bool kDisk>
+__device__ __forceinline__ bool in_ball(int32_t a, int32_t b, int32_t c) {
+    if (!RRT_F64_REJ32) {
+        const uint64_t S = sq_i24(a) + sq_i24(b) + sq_i24(c);
+        return kDisk ? S < (1ull << 46) : S - 1u < (1ull << 46);
+    }
+    const float af = (float)a, bf = (float)b, cf = (float)c;
+    const float s32 = __builtin_fmaf(cf, cf, __builtin_fmaf(bf, bf, af * af));
+    bool in = (kDisk || s32 > 0.0f) && s32 <= kRej32Lo;
+    const bool band = s32 > kRej32Lo && s32 <= kRej32Hi;
+    if (__ballot(band) != 0 && band) {
+        const uint64_t S = sq_i24(a) + sq_i24(b) + sq_i24(c);
+        in = kDisk ? S < (1ull << 46) : S - 1u < (1ull << 46);
+    }
+    return in;
+}
 __device__ __forceinline__ double centred_to_pm1(int32_t a) { return (double)a * 0x1.0p-23; }  // exact
 
 // vec3.rs:181-189 random_unit_vector (Vec3::random_range(-1, 1): x, y, z drawn in order)
@@ -106,8 +133,7 @@ __device__ __forceinline__ D3 random_unit_vector(RngState &s) {
         a = draw_centred(s);
         b = draw_centred(s);
         c = draw_centred(s);
-        const uint64_t S = sq_i24(a) + sq_i24(b) + sq_i24(c);
-        if (RRT_DEBUG_NOREJECT || S - 1u < (1ull << 46)) break;  // 0 < S <= 2^46
+        if (RRT_DEBUG_NOREJECT || in_ball<false>(a, b, c)) break;  // 0 < S <= 2^46
     }
     const double x = centred_to_pm1(a), y = centred_to_pm1(b), z = centred_to_pm1(c);
     const double lensq = x * x + y * y + z * z;
@@ -335,6 +361,29 @@ __device__ __forceinline__ double rr_probability64(D3 att) {
     if (pr > 0.95) pr = 0.95;
     return pr;
 }
+// The first RRT_F64_LDS_HIST records of a lane's history live in an LDS ring beside the traversal
+// stack ([bounce][thread], 12 B), the rest in global memory ([bounce][lane slot]): most paths are
+// short (C2: 2.6 rays per path), so their records never leave the CU.
+#ifndef RRT_F64_LDS_HIST
+#define RRT_F64_LDS_HIST 0
+#endif
+struct Hist64 {
+    Att32 *ring;     // LDS: RRT_F64_LDS_HIST x block threads
+    Att32 *global;   // P.hist
+    uint32_t lanes;  // P.hist_lanes
+    uint32_t slot;   // the lane's global slot
+    uint32_t tid;    // threadIdx.x
+    uint32_t blk;    // block threads
+    __device__ __forceinline__ void store(uint32_t k, const Att32 &r) const {
+        if (RRT_F64_LDS_HIST > 0 && k < (uint32_t)RRT_F64_LDS_HIST) ring[k * blk + tid] = r;
+        else global[(size_t)k * lanes + slot] = r;
+    }
+    __device__ __forceinline__ Att32 load(uint32_t k) const {
+        if (RRT_F64_LDS_HIST > 0 && k < (uint32_t)RRT_F64_LDS_HIST) return ring[k * blk + tid];
+        return global[(size_t)k * lanes + slot];
+    }
+};
+
 // Debug builds only (RRT_F64_B2F_MODE): 1 = the records stored but the radiance carried front to
 // back (prices the stores), 2 = the fold without its loads (prices the loads); wrong images.
 #ifndef RRT_F64_B2F_MODE
@@ -346,8 +395,7 @@ __device__ __forceinline__ double rr_probability64(D3 att) {
 #define RRT_F64_FOLD_GROUP 4
 #endif
 template <bool kTex>
-__device__ __forceinline__ D3 fold_back64(const Att32 *__restrict__ hist, uint32_t lanes, uint32_t slot, uint32_t n,
-                                          D3 L) {
+__device__ __forceinline__ D3 fold_back64(const Hist64 &hist, uint32_t n, D3 L) {
     constexpr uint32_t G = RRT_F64_FOLD_GROUP;
     uint32_t k = n;
     while (k > 0u) {
@@ -355,7 +403,7 @@ __device__ __forceinline__ D3 fold_back64(const Att32 *__restrict__ hist, uint32
         Att32 a[G];
 #pragma unroll
         for (uint32_t j = 0; j < G; ++j)
-            if (j < m) a[j] = RRT_F64_B2F_MODE == 2 ? Att32{0.5f, 0.5f, 0.5f} : hist[(size_t)(k - 1u - j) * lanes + slot];
+            if (j < m) a[j] = RRT_F64_B2F_MODE == 2 ? Att32{0.5f, 0.5f, 0.5f} : hist.load(k - 1u - j);
 #pragma unroll
         for (uint32_t j = 0; j < G; ++j) {
             if (j < m) {
@@ -592,7 +640,7 @@ __device__ __forceinline__ void camera_ray64(uint32_t x, uint32_t y, Path64 &ps)
         for (;;) {  // vec3.rs:172-179 random_in_unit_disk, decided on integers (random_unit_vector)
             a = draw_centred(ps.rng);
             b = draw_centred(ps.rng);
-            if (sq_i24(a) + sq_i24(b) < (1ull << 46)) break;
+            if (in_ball<true>(a, b, 0)) break;  // S < 2^46
         }
         const double px = centred_to_pm1(a), py = centred_to_pm1(b);
         const D3 du = d3(C.cam64[4][0], C.cam64[4][1], C.cam64[4][2]);
@@ -628,7 +676,7 @@ constexpr int kF64Full = 0, kF64Untextured = 1, kF64Diffuse = 2;
 #endif
 template <int kClass, typename Rec>
 __device__ __forceinline__ bool shade64(const KParams &P, const Rec *prims, const GMaterial *mtl, const double *inv_r,
-                                        Path64 &ps, double t, int prim, D3 &Le, uint32_t slot, uint32_t &pend,
+                                        Path64 &ps, double t, int prim, D3 &Le, const Hist64 &hist, uint32_t &pend,
                                         Att32 &prec) {
     Le = d3(0.0, 0.0, 0.0);
     if (prim < 0) {
@@ -725,10 +773,10 @@ __device__ __forceinline__ bool shade64(const KParams &P, const Rec *prims, cons
 #endif
     }
 #if RRT_F64_B2F
-    reinterpret_cast<Att32 *>(P.hist)[(size_t)ps.k * P.hist_lanes + slot] = rec;
+    hist.store(ps.k, rec);
 #else
     (void)rec;
-    (void)slot;
+    (void)hist;
 #endif
     ps.o = p;
     ps.d = dir;
@@ -741,7 +789,7 @@ __device__ __forceinline__ bool shade64(const KParams &P, const Rec *prims, cons
 // direction nrm + unit, near_zero (material.rs:33-35), Russian roulette (camera.rs:189-200) and the
 // history record. Returns 1 when the path ended (Russian roulette), 0 otherwise; pend = 0 once done.
 template <int kClass>
-__device__ __forceinline__ uint32_t lambert_draw64(const KParams &P, Path64 &ps, uint32_t slot, uint32_t &pend,
+__device__ __forceinline__ uint32_t lambert_draw64(const KParams &P, Path64 &ps, const Hist64 &hist, uint32_t &pend,
                                                    const Att32 &prec) {
     int32_t a = 0, b = 0, c = 0;
     bool ok = false;
@@ -749,8 +797,7 @@ __device__ __forceinline__ uint32_t lambert_draw64(const KParams &P, Path64 &ps,
         a = draw_centred(ps.rng);
         b = draw_centred(ps.rng);
         c = draw_centred(ps.rng);
-        const uint64_t S = sq_i24(a) + sq_i24(b) + sq_i24(c);
-        ok = S - 1u < (1ull << 46);  // 0 < S <= 2^46
+        ok = in_ball<false>(a, b, c);  // 0 < S <= 2^46
     }
     if (!ok) return 0u;
     pend = 0;
@@ -764,7 +811,7 @@ __device__ __forceinline__ uint32_t lambert_draw64(const KParams &P, Path64 &ps,
                                                 : f2d(prec.x, prec.y, prec.z);
         if (rnd64(ps.rng) > rr_probability64(att)) return 1u;
     }
-    reinterpret_cast<Att32 *>(P.hist)[(size_t)ps.k * P.hist_lanes + slot] = prec;
+    hist.store(ps.k, prec);
     ps.d = dir;
     ps.k++;
     return 0u;
@@ -788,8 +835,10 @@ __device__ __forceinline__ void render64_body(const KParams &P) {
     const GMaterial *mtl = P.prim_mtl;
     const double *inv_r = P.prim_inv_r64;
     const float4 *recs32 = P.prim_cr;  // the pre-test's f32 records (center, r)
+    const uint32_t stack16 = (P.stack_depth * kBlk * sizeof(uint16_t) + 15u) / 16u;
+    constexpr uint32_t kRing16 = (uint32_t)RRT_F64_LDS_HIST * kBlk * 12u / 16u;  // kBlk is a multiple of 64
     if constexpr (kLds) {  // stage nodes + spheres (+ 1/r) once per block
-        uint4 *dst = lds_dyn + (P.stack_depth * kBlk * sizeof(uint16_t) + 15u) / 16u;
+        uint4 *dst = lds_dyn + stack16 + kRing16;
         // Node112: each 80-B GNode re-laid as 112 B whose axis a holds both children's (lo, hi), then
         // both (hi, lo), and the links at 96 — one ds_read_b128 per axis at the ray's sign offset
         // reads both children's (entry, exit) pairs (4 LDS cycles, against 8 for two ds_read2_b32):
@@ -850,9 +899,12 @@ __device__ __forceinline__ void render64_body(const KParams &P) {
     uint32_t xy = 0, s = 0, s_hi = 0;
     uint32_t px = 0;         // the unit's tile-local pixel index
     uint32_t tail = 0;       // the unit is a tail chunk: its samples' radiances go to seq64 one by one
+    uint32_t tcidx = 0;      // a tail unit's chunk index within the pass
+    uint32_t tmask = 0;      // a tail unit's samples with nonzero radiance (bit = sample - its first)
     uint32_t pend = 0;       // RRT_F64_DEFER: a Lambertian scatter waits for an accepted candidate
     Att32 prec{0.0f, 0.0f, 0.0f};
-    const uint32_t slot = blockIdx.x * (uint32_t)kBlk + threadIdx.x;  // the lane's history slot
+    const Hist64 hist{reinterpret_cast<Att32 *>(lds_dyn + stack16), reinterpret_cast<Att32 *>(P.hist), P.hist_lanes,
+                      blockIdx.x * (uint32_t)kBlk + threadIdx.x, threadIdx.x, (uint32_t)kBlk};
     uint64_t pkey = 0;
     D3 sum = d3(0.0, 0.0, 0.0);
     Path64 ps;
@@ -904,6 +956,8 @@ __device__ __forceinline__ void render64_body(const KParams &P) {
                     s_hi = min(s + (chunk < Q.n_big ? Q.chunk : Q.chunk_small), Q.sample_end);
                     px = ly * Q.width + x;
                     tail = Q.seq && chunk >= Q.n_big ? 1u : 0u;
+                    tcidx = tail ? fast_div(s - Q.sample_begin - Q.seq_first, fdiv(Q.fd_chunk_small)) : 0u;
+                    tmask = 0u;
                     sum = d3(0.0, 0.0, 0.0);
                     pkey = pixel_key(Q, x, y);
                     ps.rng = path_rng_k(pkey, s);
@@ -992,10 +1046,10 @@ __device__ __forceinline__ void render64_body(const KParams &P) {
         D3 Le = d3(0.0, 0.0, 0.0);
         if (has && !need_ray && tr.node < 0 && !pend) {
             need_ray = 1;
-            seg_done = shade64<kClass>(P, prims, mtl, inv_r, ps, tr.closest, tr.hit_prim, Le, slot, pend, prec) ? 1u : 0u;
+            seg_done = shade64<kClass>(P, prims, mtl, inv_r, ps, tr.closest, tr.hit_prim, Le, hist, pend, prec) ? 1u : 0u;
         }
         if (RRT_F64_DEFER && pend) {
-            seg_done = lambert_draw64<kClass>(P, ps, slot, pend, prec);
+            seg_done = lambert_draw64<kClass>(P, ps, hist, pend, prec);
             need_ray = pend ? 0u : 1u;
         }
         w_paths += (uint32_t)__popcll(__ballot(seg_done));
@@ -1004,16 +1058,21 @@ __device__ __forceinline__ void render64_body(const KParams &P) {
             // the radiance at the path's end carried back through its scatters; a path that ended
             // with none (absorbed, Russian roulette, max_depth) adds an exact 0
             if (Le.x != 0.0 || Le.y != 0.0 || Le.z != 0.0)
-                Le = fold_back64<kClass != kF64Untextured>(reinterpret_cast<const Att32 *>(P.hist), P.hist_lanes,
-                                                           slot, ps.k, Le);
+                Le = fold_back64<kClass != kF64Untextured>(hist, ps.k, Le);
 #endif
             const auto &Q = *kernarg_params();
             if (tail) {  // a tail sample: its radiance, folded into the pixel's sum in order later
-                const size_t npx = (size_t)Q.tile_rows * Q.width;
-                double *o = Q.seq64 + 3u * ((size_t)(s - Q.sample_begin - Q.seq_first) * npx + px);
-                o[0] = Le.x;
-                o[1] = Le.y;
-                o[2] = Le.z;
+                // only nonzero radiances are kept (an exact 0 leaves BOOKS' sum unchanged), packed in
+                // sample order, with the unit's mask of which samples they are
+                if (Le.x != 0.0 || Le.y != 0.0 || Le.z != 0.0) {
+                    const size_t npx = (size_t)Q.tile_rows * Q.width;
+                    const uint32_t j = (uint32_t)__popc(tmask);
+                    double *o = Q.seq64 + 3u * (((size_t)tcidx * Q.chunk_small + j) * npx + px);
+                    o[0] = Le.x;
+                    o[1] = Le.y;
+                    o[2] = Le.z;
+                    tmask |= 1u << (s - Q.sample_begin - Q.seq_first - tcidx * Q.chunk_small);
+                }
             } else {
                 sum = add(sum, Le);
             }
@@ -1030,6 +1089,7 @@ __device__ __forceinline__ void render64_body(const KParams &P) {
                 const D4 out{sum.x, sum.y, sum.z, (double)(s_hi - (Q.sample_begin + chunk_first(Q, chunk)))};
                 if (Q.n_chunks == 1 || (Q.seq && !tail)) Q.accum64[px] = out;  // the whole pixel, or its prefix
                 else if (!tail) Q.partial64[(size_t)(chunk - Q.chunk_begin) * ((size_t)Q.tile_rows * Q.width) + px] = out;
+                else Q.seqmask[(size_t)tcidx * ((size_t)Q.tile_rows * Q.width) + px] = tmask;
                 has = 0;
             }
         }
@@ -1071,10 +1131,17 @@ __device__ __forceinline__ void render64_body(const KParams &P) {
 #define RRT_F64_WAVES 4  // waves/SIMD bound of the untextured and diffuse classes (<= 128 VGPRs, no spills)
 #endif
 constexpr int kBlock64 = RRT_F64_BLOCK;  // threads per block of the f64 kernel
+// The full class (texture + specular) needs more than 128 VGPRs (3 waves/SIMD): 512-thread blocks,
+// since a block of 1024 needs 4 waves per SIMD.
+__host__ __device__ constexpr int blk64(int cls) { return cls == 0 ? 512 : kBlock64; }
+// LDS one block may declare: 160 KiB on gfx950 (MI355X_MICROARCH.md occupancy section) when the
+// block is the CU's only one (1024 threads at 4 waves/SIMD), else the 64 KiB that keeps two
+// 512-thread blocks per CU
+__host__ __device__ constexpr size_t lds_budget64(int blk) { return blk >= 1024 ? 160u * 1024u : 64u * 1024u; }
 
 template <int kMode, bool kCount, int kClass>
-__global__ __launch_bounds__(kBlock64, kClass == kF64Full ? 1 : RRT_F64_WAVES) void rrt_render64(KParams P) {
-    render64_body<kMode, kCount, kBlock64, kClass>(P);
+__global__ __launch_bounds__(blk64(kClass), kClass == kF64Full ? 1 : RRT_F64_WAVES) void rrt_render64(KParams P) {
+    render64_body<kMode, kCount, blk64(kClass), kClass>(P);
 }
 
 // The pass's f64 chunk sums into accum64, continuing the left fold over chunks in order (as
@@ -1097,16 +1164,23 @@ __global__ __launch_bounds__(256) void rrt_combine_chunks64(const D4 *__restrict
 // Sequential-sum mode: the pass's tail-sample radiances added to each pixel's sum in sample order
 // (pixel_color += ray_color(..), camera.rs:72-76), continuing from the prefix chunk's sum (or the
 // previous pass's); w = the samples summed so far.
-__global__ __launch_bounds__(256) void rrt_fold_samples64(const double *__restrict__ seq, D4 *__restrict__ accum,
-                                                          uint32_t n_pixels, uint32_t n_samples, double count) {
+// The tail units kept each chunk's nonzero radiances packed in sample order plus a mask; the zero
+// ones add nothing (s + 0 = s for the nonnegative sums), so the fold skips them.
+__global__ __launch_bounds__(256) void rrt_fold_samples64(const double *__restrict__ seq,
+                                                          const uint32_t *__restrict__ masks, D4 *__restrict__ accum,
+                                                          uint32_t n_pixels, uint32_t n_chunks, uint32_t chunk_small,
+                                                          double count) {
     const uint32_t p = blockIdx.x * 256u + threadIdx.x;
     if (p >= n_pixels) return;
     D4 acc = accum[p];
-    for (uint32_t j = 0; j < n_samples; ++j) {
-        const double *v = seq + 3u * ((size_t)j * n_pixels + p);
-        acc.x = acc.x + v[0];
-        acc.y = acc.y + v[1];
-        acc.z = acc.z + v[2];
+    for (uint32_t c = 0; c < n_chunks; ++c) {
+        const uint32_t n = (uint32_t)__popc(masks[(size_t)c * n_pixels + p]);
+        for (uint32_t j = 0; j < n; ++j) {
+            const double *v = seq + 3u * (((size_t)c * chunk_small + j) * n_pixels + p);
+            acc.x = acc.x + v[0];
+            acc.y = acc.y + v[1];
+            acc.z = acc.z + v[2];
+        }
     }
     accum[p] = D4{acc.x, acc.y, acc.z, count};
 }
@@ -1122,8 +1196,9 @@ __global__ __launch_bounds__(256) void rrt_accum64_to_f32(const D4 *__restrict__
 
 // LDS of the f64 kernel's block in each mode (stack, then the staged scene; the 1/r table when
 // p.inv_r_in_lds)
-size_t lds64_bytes(const KParams &p, int mode) {
-    size_t lds = ((size_t)p.stack_depth * kBlock64 * sizeof(uint16_t) + 15u) / 16u * 16u;
+size_t lds64_bytes(const KParams &p, int mode, int blk = kBlock64) {
+    size_t lds = ((size_t)p.stack_depth * blk * sizeof(uint16_t) + 15u) / 16u * 16u;
+    lds += (size_t)RRT_F64_LDS_HIST * blk * 12u;  // the history ring
     if (mode != kF64Global)
         lds += (size_t)p.n_nodes * 112u +
                (size_t)p.n_prims * ((mode == kF64LdsWide ? sizeof(Sphere64) : sizeof(float4)) +
@@ -1142,28 +1217,38 @@ size_t f64_lds_min_bytes(uint32_t n_nodes, uint32_t n_prims, uint32_t stack_dept
     p.stack_depth = stack_depth;
     p.inv_r_in_lds = 0u;
     p.rec32_in_lds = 0u;
-    return lds64_bytes(p, kF64Lds);
+    // the host's staging rule (rrt_host.cpp scene_bvh): the 512-thread block's layout without the
+    // history ring within 64 KB, whatever block the classes launch
+    return lds64_bytes(p, kF64Lds, 512) - (size_t)RRT_F64_LDS_HIST * 512u * 12u;
 }
 
 namespace {
 
 template <int kMode, int kClass>
 hipError_t launch64(const KParams &p, bool count, hipStream_t stream) {
-    const size_t lds = lds64_bytes(p, kMode);
+    constexpr int B = blk64(kClass);
+    const size_t lds = lds64_bytes(p, kMode, B);
+    if (lds > lds_budget64(B)) return hipErrorInvalidValue;
     auto kernel = count ? rrt_render64<kMode, true, kClass> : rrt_render64<kMode, false, kClass>;
+    hipError_t e;
+    if (lds > 64u * 1024u) {  // beyond the default dynamic-LDS limit (gfx950 allows 160 KiB per block)
+        e = hipFuncSetAttribute(reinterpret_cast<const void *>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds);
+        if (e != hipSuccess) return e;
+    }
     int per_cu = 0;
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock64, lds);
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, B, lds);
     if (e != hipSuccess) return e;
     if (per_cu < 1) per_cu = 1;
-    const uint32_t want = (p.n_units + kBlock64 - 1) / kBlock64;
+    const uint32_t want = (p.n_units + B - 1) / B;
     uint32_t blocks = std::max<uint32_t>(std::min<uint32_t>(want, (uint32_t)per_cu * p.n_cus), kQueues);
     if (RRT_F64_B2F) {  // every lane needs a history slot
-        if (!p.hist || p.hist_lanes < kQueues * (uint32_t)kBlock64) return hipErrorInvalidValue;
-        blocks = std::min<uint32_t>(blocks, p.hist_lanes / (uint32_t)kBlock64);
+        if (!p.hist || p.hist_lanes < kQueues * (uint32_t)B) return hipErrorInvalidValue;
+        blocks = std::min<uint32_t>(blocks, p.hist_lanes / (uint32_t)B);
     }
     e = hipMemsetAsync(p.unit_counter, 0, kQueues * 32u * sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(kernel, dim3(blocks), dim3(kBlock64), lds, stream, p);
+    hipLaunchKernelGGL(kernel, dim3(blocks), dim3(B), lds, stream, p);
     return hipGetLastError();
 }
 
@@ -1184,7 +1269,8 @@ hipError_t launch64_placed(const KParams &p, bool count, hipStream_t stream) {
         const bool wide = (lay & 1) != 0;
         q.inv_r_in_lds = (lay & 2) ? 1u : 0u;
         q.rec32_in_lds = wide && (lay & 4) ? 1u : 0u;
-        if (lds64_bytes(q, wide ? kF64LdsWide : kF64Lds) > 64u * 1024u) return hipErrorInvalidValue;
+        if (lds64_bytes(q, wide ? kF64LdsWide : kF64Lds, blk64(kClass)) > lds_budget64(blk64(kClass)))
+            return hipErrorInvalidValue;
         return wide ? launch64<kF64LdsWide, kClass>(q, count, stream) : launch64<kF64Lds, kClass>(q, count, stream);
     }
     // the widened sphere records and the 1/r table join the staged scene while the block stays
@@ -1201,13 +1287,14 @@ hipError_t launch64_placed(const KParams &p, bool count, hipStream_t stream) {
             q.rec32_in_lds = rec32;
             for (const uint32_t inv_r : {1u, 0u}) {
                 q.inv_r_in_lds = inv_r;
-                if (lds64_bytes(q, kF64LdsWide) <= 64u * 1024u) return launch64<kF64LdsWide, kClass>(q, count, stream);
+                if (lds64_bytes(q, kF64LdsWide, blk64(kClass)) <= lds_budget64(blk64(kClass)))
+                    return launch64<kF64LdsWide, kClass>(q, count, stream);
             }
         }
     }
     q.rec32_in_lds = 0u;
     q.inv_r_in_lds = 1u;
-    if (lds64_bytes(q, kF64Lds) > 64u * 1024u) q.inv_r_in_lds = 0u;
+    if (lds64_bytes(q, kF64Lds, blk64(kClass)) > lds_budget64(blk64(kClass))) q.inv_r_in_lds = 0u;
     return launch64<kF64Lds, kClass>(q, count, stream);
 }
 
@@ -1260,7 +1347,7 @@ hipError_t launch_render_f64_seq(const KParams &p, bool count, hipStream_t strea
         if (tail0 < end) {
             const uint32_t done = std::min(S, chunk_first(p, end));
             hipLaunchKernelGGL(rrt_fold_samples64, dim3((n_pixels + 255) / 256), dim3(256), 0, stream, p.seq64,
-                               p.accum64, n_pixels, done - q.seq_first, (double)done);
+                               p.seqmask, p.accum64, n_pixels, end - tail0, p.chunk_small, (double)done);
             e = hipGetLastError();
             if (e != hipSuccess) return e;
         }

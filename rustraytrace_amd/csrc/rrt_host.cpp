@@ -984,6 +984,9 @@ size_t seq_budget() {
 #ifndef RRT_F64_TAIL_DIV
 #define RRT_F64_TAIL_DIV 4
 #endif
+#ifndef RRT_F64_TS_DIV  // the f64 tail units: K/8 samples
+#define RRT_F64_TS_DIV 8
+#endif
 
 int fill_params(RrtScene *s, const RrtTile *t, float *d_accum, rrt::KParams &p) {
     p = s->base;
@@ -1007,8 +1010,10 @@ int fill_params(RrtScene *s, const RrtTile *t, float *d_accum, rrt::KParams &p) 
 #ifdef RRT_CHUNK_FORCE  // A/B builds only (tools/build_variants.sh): a fixed chunk outside the ABI's rule
     p.chunk = std::max(1u, (uint32_t)RRT_CHUNK_FORCE);
 #endif
+// tail chunks of K/4 (ABI v10; K/8 before): a quarter of C2's chunk partials fewer (7 instead of 11
+// per pixel, ~100 MB less HBM written and read per launch), same-box C2 +0.3 %, C4 +0.6 %, C5 -0.4 %
 #ifndef RRT_TAIL_DIV
-#define RRT_TAIL_DIV 8
+#define RRT_TAIL_DIV 4
 #endif
     p.chunk_small = std::max(1u, p.chunk / RRT_TAIL_DIV);
     p.n_big = S > p.chunk ? (S - 1u) / p.chunk : 0u;
@@ -1022,7 +1027,7 @@ int fill_params(RrtScene *s, const RrtTile *t, float *d_accum, rrt::KParams &p) 
         // the f32 schedule's share of small units (C2: 128 samples in 8 chunks of 16): it balances the
         // queue's drain as well as the chunked schedule did (same-box C2 18.75 vs 18.73 Grays/s), at
         // 24 B per tail sample; T = S/8 left the drain uncovered (-5 %).
-        const uint32_t ts = p.chunk_small;
+        const uint32_t ts = std::min(std::max(1u, p.chunk / RRT_F64_TS_DIV), 32u);  // a tail unit's mask is 32 bits
         const uint32_t t_samples = S >= 2u * ts ? (S / RRT_F64_TAIL_DIV) / ts * ts : 0u;
         p.seq = 1u;
         p.n_big = 1u;
@@ -1046,10 +1051,10 @@ int fill_params(RrtScene *s, const RrtTile *t, float *d_accum, rrt::KParams &p) 
     p.pass_chunks = p.n_chunks;
     if (p.seq && p.n_chunks > 1) {  // per-sample tail radiances [pass tail sample][pixel], within the budget
         const size_t n_px = std::max<size_t>((size_t)p.tile_rows * p.width, 1);
-        const size_t per_chunk = n_px * p.chunk_small * 3u * sizeof(double);
+        const size_t per_chunk = n_px * p.chunk_small * 3u * sizeof(double) + n_px * sizeof(uint32_t);
         const uint32_t n_tail = p.n_chunks - 1u;
         p.pass_chunks = (uint32_t)std::min<size_t>(n_tail, std::max<size_t>(1, seq_budget() / per_chunk));
-        const size_t need = per_chunk * p.pass_chunks / sizeof(double);
+        const size_t need = (per_chunk * p.pass_chunks + sizeof(double) - 1) / sizeof(double);
         if (need > s->seq64_cap) {
             HIP_TRY(hipSetDevice(s->device), "hipSetDevice");
             (void)hipFree(s->d_seq64);
@@ -1077,6 +1082,11 @@ int fill_params(RrtScene *s, const RrtTile *t, float *d_accum, rrt::KParams &p) 
     p.partial = s->d_partial;
     p.partial64 = s->d_partial64;
     p.seq64 = s->d_seq64;
+    p.seqmask = nullptr;
+    if (p.seq && p.n_chunks > 1) {  // the masks follow the pass's packed radiances
+        const size_t n_px = std::max<size_t>((size_t)p.tile_rows * p.width, 1);
+        p.seqmask = reinterpret_cast<uint32_t *>(s->d_seq64 + (size_t)p.pass_chunks * n_px * p.chunk_small * 3u);
+    }
     p.accum64 = nullptr;
     if (s->f64) {  // the attenuation history: max_depth records of 12 B per lane slot
         const uint64_t per_lane = (uint64_t)std::max(1u, p.max_depth) * 12u;

@@ -246,7 +246,8 @@ struct KParams {
     // folded into accum64 in sample order after the pass (launch_render_f64_seq).
     uint32_t seq;
     uint32_t seq_first;
-    double *seq64;
+    double *seq64;       // [tail chunk of the pass][j < chunk_small][tile pixel] x 3: nonzero radiances packed
+    uint32_t *seqmask;   // [tail chunk of the pass][tile pixel]: which of the chunk's samples they are
     // the f64 path's attenuation history ([bounce][lane slot] x 3 floats, rrt_books64.hip
     // fold_back64): max_depth x hist_lanes records; the launch keeps blocks x threads <= hist_lanes
     float *hist;

@@ -64,3 +64,43 @@ def test_draws_on_the_sphere_decide_as_f64():
     # exact boundary points: S = 2^46 is accepted by the sphere test (<= 1) and rejected by the disk (< 1)
     assert int_unit(0, 2 ** 23, 2 ** 23) and ref_unit(0, 2 ** 23, 2 ** 23)
     assert not int_disk(0, 2 ** 23) and not ref_disk(0, 2 ** 23)
+
+
+# The kernel's f32 pre-decision (rrt_books64.hip in_ball, RRT_F64_REJ32): the f32 sum of squares
+# fma(c, c, fma(b, b, a*a)) of the exact centred coordinates decides outside the band
+# 2^46 (1 +- 2^-21); inside it the integers decide. Emulated exactly: a*a rounded to f32, each fma
+# as the exact f64 sum (<= 49 significant bits) rounded once to f32.
+LO, HI = np.float32(2.0 ** 46 * (1 - 2.0 ** -21)), np.float32(2.0 ** 46 * (1 + 2.0 ** -21))
+
+
+def f32_decision(a, b, c, disk):
+    a, b, c = (np.asarray(v, np.int64) - 2 ** 23 for v in (a, b, c))
+    p = (a.astype(np.float64) ** 2).astype(np.float32)
+    p = (b.astype(np.float64) ** 2 + p.astype(np.float64)).astype(np.float32)
+    s32 = (c.astype(np.float64) ** 2 + p.astype(np.float64)).astype(np.float32)
+    accept = (s32 <= LO) & ((s32 > 0) | disk)
+    band = (s32 > LO) & (s32 <= HI)
+    return accept, band
+
+
+def test_f32_pre_decision_matches_the_integers():
+    rng = np.random.default_rng(11)
+    n = 400_000
+    a, b, c = (rng.integers(0, 2 ** 24, n) for _ in range(3))
+    # and candidates on and around the sphere / circle: S within +-2^30 of 2^46
+    t = rng.normal(size=(n, 3))
+    t /= np.linalg.norm(t, axis=1, keepdims=True)
+    r = 2.0 ** 23 * (1 + rng.uniform(-2.0 ** -17, 2.0 ** -17, n))
+    near = np.clip(np.round(t * r[:, None]) + 2 ** 23, 0, 2 ** 24 - 1).astype(np.int64)
+    for disk in (False, True):
+        for A, B, C in ((a, b, c), (near[:, 0], near[:, 1], near[:, 2] if not disk else np.full(n, 2 ** 23))):
+            acc, band = f32_decision(A, B, C, disk)
+            S = sum((np.asarray(v, np.int64) - 2 ** 23) ** 2 for v in (A, B, C))
+            exact = (S < 2 ** 46) if disk else ((S > 0) & (S <= 2 ** 46))
+            decided = ~band
+            assert np.array_equal(acc[decided], exact[decided])
+            assert band.mean() < 0.05  # the band is rare even among candidates placed at the boundary
+    acc, band = f32_decision(a, b, c, False)
+    assert band.mean() < 1e-5  # random candidates: ~7e-7 in the band
+    assert f32_decision([2 ** 23], [2 ** 23], [2 ** 23], False)[0][0] == False  # S = 0 rejected (1e-160 < |p|^2)
+    assert f32_decision([2 ** 23], [2 ** 23], [2 ** 23], True)[0][0] == True    # the disk takes S = 0

@@ -6,7 +6,9 @@ FETCH_SIZE / WRITE_SIZE are in KiB and count the L2's memory-side requests. gfx9
 FETCH_SIZE reads half the bytes of a wide 16-B/lane streaming read; this kernel's reads are
 L2-resident scene gathers and its only streaming traffic is the accum write, so the raw
 values are reported alongside the corrected upper bound (2 x FETCH_SIZE + WRITE_SIZE).
-    python tools/pmc_traffic.py <fetch_dir> <write_dir> <config> <width> <spp> <out_json>
+    python tools/pmc_traffic.py <fetch_dir> <write_dir> <config> <width> <spp> <out_json> [f64]
+The f64 books kernel's launch (trailing argument `f64`): rrt_render64, with its in-order tail fold
+(rrt_fold_samples64) reported as the combine step.
 """
 import csv
 import glob
@@ -35,14 +37,17 @@ def counter(d, name, kernel="rrt_render"):
     return sum(vals) / len(vals), len(vals)
 
 
-def main(fetch_dir, write_dir, config, width, spp, out):
+def main(fetch_dir, write_dir, config, width, spp, out, f64=""):
+    f64 = f64 == "f64"
     fetch_kib, n1 = counter(fetch_dir, "FETCH_SIZE")
     write_kib, n2 = counter(write_dir, "WRITE_SIZE")
-    cf_kib, nc = counter(fetch_dir, "FETCH_SIZE", "rrt_combine_chunks")
-    cw_kib, _ = counter(write_dir, "WRITE_SIZE", "rrt_combine_chunks")
+    combine = "rrt_fold_samples64" if f64 else "rrt_combine_chunks"
+    cf_kib, nc = counter(fetch_dir, "FETCH_SIZE", combine)
+    cw_kib, _ = counter(write_dir, "WRITE_SIZE", combine)
     so = os.path.join(ROOT, "rustraytrace_amd", "librrt_hip.so")
     rec = {
         "config": config,
+        "f64": f64,
         "width": int(width),
         "spp": int(spp),
         "dispatches": [n1, n2],
