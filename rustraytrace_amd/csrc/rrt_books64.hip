@@ -77,8 +77,26 @@ __device__ __forceinline__ D3 mul(D3 a, D3 b) { return d3(a.x * b.x, a.y * b.y, 
 __device__ __forceinline__ D3 muls(D3 a, double s) { return d3(a.x * s, a.y * s, a.z * s); }
 // vec3.rs:156-158 dot = u0*v0 + u1*v1 + u2*v2 (left to right, unfused)
 __device__ __forceinline__ double dot(D3 a, D3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+// 1 / x, the IEEE quotient, in 6 instructions instead of the expansion's 11 for x in [2^-64, 2^64]:
+// there the expansion's v_div_scale steps are identities (numerator 1, quotient in [2^-64, 2^64]) and
+// its v_div_fixup passes the v_div_fmas result through, so what remains is its own reciprocal
+// (v_rcp_f64 + two Newton steps) and final step fma(fma(-x, r, 1), r, r) — the same operations the
+// f64 root divisions use (recip_a64 / div_a64, below). Outside the range: the IEEE division. Off by
+// default: same-box within noise (C2 +-0.5 %, C4 -1 %, `profiles/r5_f64_ab_batch5.log`).
+#ifndef RRT_F64_FASTRCP
+#define RRT_F64_FASTRCP 0
+#endif
+__device__ __forceinline__ double recip64(double x) {
+    if (!RRT_F64_FASTRCP || !(x >= 0x1.0p-64 && x <= 0x1.0p64)) return 1.0 / x;
+    double r = __builtin_amdgcn_rcp(x);
+    double e = __builtin_fma(-x, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    e = __builtin_fma(-x, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    return __builtin_fma(__builtin_fma(-x, r, 1.0), r, r);
+}
 // vec3.rs:168-170 unit_vector = v / |v|, Div<f64> = (1/rhs) * v (vec3.rs:142-148)
-__device__ __forceinline__ D3 unit_vector(D3 v) { return muls(v, 1.0 / __builtin_sqrt(dot(v, v))); }
+__device__ __forceinline__ D3 unit_vector(D3 v) { return muls(v, recip64(__builtin_sqrt(dot(v, v)))); }
 __device__ __forceinline__ D3 f2d(float x, float y, float z) { return d3((double)x, (double)y, (double)z); }
 // f64::min: a NaN operand yields the other
 __device__ __forceinline__ double rmin(double a, double b) { return a < b ? a : b; }
@@ -102,8 +120,11 @@ __device__ __forceinline__ uint64_t sq_i24(int32_t a) { return (uint64_t)((int64
 // (u = 2^-24: one rounding per term) of the integer S, so it decides `S <= 2^46` (`S < 2^46` for the
 // disk) outside the band 2^46 (1 +- 2^-21) and `S > 0` exactly (it is 0 only for a = b = c = 0).
 // A wave with a lane in the band (~7e-7 of the candidates) decides those lanes on the integers.
+// Off by default: same-box C2 -5 %, C4 -5 %, C5 -4 % (`profiles/r5_f64_ab_batch5.log`) — the
+// band's ballot and branch in every iteration cost the scalar unit more than the integer
+// multiplies they replace (round 4 measured the same of an f32 test with an f64 fallback).
 #ifndef RRT_F64_REJ32
-#define RRT_F64_REJ32 1
+#define RRT_F64_REJ32 0
 #endif
 constexpr float kRej32Lo = 0x1.fffffp45f;   // 2^46 (1 - 2^-21)
 constexpr float kRej32Hi = 0x1.000008p46f;  // 2^46 (1 + 2^-21)
@@ -137,7 +158,7 @@ __device__ __forceinline__ D3 random_unit_vector(RngState &s) {
     }
     const double x = centred_to_pm1(a), y = centred_to_pm1(b), z = centred_to_pm1(c);
     const double lensq = x * x + y * y + z * z;
-    return muls(d3(x, y, z), 1.0 / __builtin_sqrt(lensq));
+    return muls(d3(x, y, z), recip64(__builtin_sqrt(lensq)));
 }
 
 // vec3.rs:201-203 reflect = v - (2 * dot(v, n)) * n
@@ -410,7 +431,7 @@ __device__ __forceinline__ D3 fold_back64(const Hist64 &hist, uint32_t n, D3 L) 
                 const D3 att = kTex ? d3(att_decode(a[j].x), att_decode(a[j].y), att_decode(a[j].z))
                                     : f2d(a[j].x, a[j].y, a[j].z);
                 L = mul(att, L);
-                if (k - 1u - j >= 5u) L = muls(L, 1.0 / rr_probability64(att));  // Div<f64>: (1/p) * v (vec3.rs:142-148)
+                if (k - 1u - j >= 5u) L = muls(L, recip64(rr_probability64(att)));  // Div<f64>: (1/p) * v (vec3.rs:142-148)
             }
         }
         k -= m;
@@ -767,7 +788,7 @@ __device__ __forceinline__ bool shade64(const KParams &P, const Rec *prims, cons
         const double pr = rr_probability64(att);
         if (rnd64(ps.rng) > pr) return true;
 #if !RRT_F64_B2F || RRT_F64_B2F_MODE == 1
-        ps.T = muls(mul(ps.T, att), 1.0 / pr);
+        ps.T = muls(mul(ps.T, att), recip64(pr));
     } else {
         ps.T = mul(ps.T, att);
 #endif
@@ -804,7 +825,7 @@ __device__ __forceinline__ uint32_t lambert_draw64(const KParams &P, Path64 &ps,
     const double x = centred_to_pm1(a), y = centred_to_pm1(b), z = centred_to_pm1(c);
     const double lensq = x * x + y * y + z * z;
     const D3 nrm = ps.d;
-    D3 dir = add(nrm, muls(d3(x, y, z), 1.0 / __builtin_sqrt(lensq)));
+    D3 dir = add(nrm, muls(d3(x, y, z), recip64(__builtin_sqrt(lensq))));
     if (__builtin_fabs(dir.x) < 1e-8 && __builtin_fabs(dir.y) < 1e-8 && __builtin_fabs(dir.z) < 1e-8) dir = nrm;
     if (ps.k >= 5u) {
         const D3 att = kClass != kF64Untextured ? d3(att_decode(prec.x), att_decode(prec.y), att_decode(prec.z))
