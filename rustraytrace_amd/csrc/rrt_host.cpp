@@ -984,6 +984,11 @@ size_t seq_budget() {
 #ifndef RRT_F64_TAIL_DIV
 #define RRT_F64_TAIL_DIV 4
 #endif
+// frames of more than 512 samples (C4, C3): T = S/2, prefix units of S/2 samples. Same-box against
+// S/4: C4 +4 %; the same rule at 512 samples and below: C2 -4.5 %, C5 -5 % (r5_f64_ab_batch6.log)
+#ifndef RRT_F64_TAIL_DIV_HI
+#define RRT_F64_TAIL_DIV_HI 2
+#endif
 #ifndef RRT_F64_TS_DIV  // the f64 tail units: K/8 samples
 #define RRT_F64_TS_DIV 8
 #endif
@@ -1023,12 +1028,13 @@ int fill_params(RrtScene *s, const RrtTile *t, float *d_accum, rrt::KParams &p) 
     if (s->f64 && RRT_F64_SEQ && S) {
         // The f64 books path sums each pixel's samples in camera.rs:72-76's order: one prefix chunk
         // of S - T samples (summed in the lane from 0), then T tail samples in chunks of K/8 whose
-        // radiances are kept one by one and folded in after the pass. T = S/4 in whole tail chunks,
-        // the f32 schedule's share of small units (C2: 128 samples in 8 chunks of 16): it balances the
-        // queue's drain as well as the chunked schedule did (same-box C2 18.75 vs 18.73 Grays/s), at
-        // 24 B per tail sample; T = S/8 left the drain uncovered (-5 %).
+        // radiances are kept one by one and folded in after the pass. T = S/4 in whole tail chunks
+        // (C2: 128 samples in 8 chunks of 16): it balances the queue's drain as well as the chunked
+        // schedule did (same-box C2 18.75 vs 18.73 Grays/s); T = S/8 left the drain uncovered (-5 %).
+        // T = S/2 above 512 samples.
         const uint32_t ts = std::min(std::max(1u, p.chunk / RRT_F64_TS_DIV), 32u);  // a tail unit's mask is 32 bits
-        const uint32_t t_samples = S >= 2u * ts ? (S / RRT_F64_TAIL_DIV) / ts * ts : 0u;
+        const uint32_t tdiv = S > 512u ? RRT_F64_TAIL_DIV_HI : RRT_F64_TAIL_DIV;
+        const uint32_t t_samples = S >= 2u * ts ? (S / tdiv) / ts * ts : 0u;
         p.seq = 1u;
         p.n_big = 1u;
         p.chunk = S - t_samples;
