@@ -373,6 +373,55 @@ struct Att32 {
 __device__ __forceinline__ double att_decode(float f) {
     return (__float_as_uint(f) >> 31) ? texel_channel64((uint32_t)(-f)) : (double)f;
 }
+// RRT_F64_REC4 = 1: a 4-B record instead — the primitive index (its material's albedo), kRecOne for a
+// dielectric's (1, 1, 1), or kRecTexel | the texel's bytes (kRecTexel | 0x1000000: the no-data
+// texture's (0, 1, 1)); the fold reads the albedo back from the material record.
+#ifndef RRT_F64_REC4
+#define RRT_F64_REC4 0
+#endif
+[[maybe_unused]] constexpr uint32_t kRecOne = 0xFFFFFFFEu, kRecTexel = 0x80000000u;
+#if RRT_F64_REC4
+using HRec = uint32_t;
+#else
+using HRec = Att32;
+#endif
+__device__ __forceinline__ HRec rec_albedo(int prim, const GMaterial &m) {
+#if RRT_F64_REC4
+    (void)m;
+    return (uint32_t)prim;
+#else
+    (void)prim;
+    return Att32{m.a.x, m.a.y, m.a.z};
+#endif
+}
+__device__ __forceinline__ HRec rec_one() {
+#if RRT_F64_REC4
+    return kRecOne;
+#else
+    return Att32{1.0f, 1.0f, 1.0f};
+#endif
+}
+__device__ __forceinline__ HRec rec_texel(uint32_t b) {
+#if RRT_F64_REC4
+    return kRecTexel | b;
+#else
+    if (b == 0x1000000u) return Att32{0.0f, 1.0f, 1.0f};
+    return Att32{-(float)(b & 0xffu), -(float)((b >> 8) & 0xffu), -(float)(b >> 16)};
+#endif
+}
+// the attenuation a record stands for (kTex: the class has image textures)
+template <bool kTex>
+__device__ __forceinline__ D3 rec_att(const HRec &r, const GMaterial *__restrict__ mtl) {
+#if RRT_F64_REC4
+    if (r == kRecOne) return d3(1.0, 1.0, 1.0);
+    if (kTex && (r & kRecTexel)) return texel_value64(r & 0x1ffffffu);
+    const float4 a = mtl[r].a;
+    return f2d(a.x, a.y, a.z);
+#else
+    (void)mtl;
+    return kTex ? d3(att_decode(r.x), att_decode(r.y), att_decode(r.z)) : f2d(r.x, r.y, r.z);
+#endif
+}
 // camera.rs:191-195: max of the attenuation's components, clamped to [0.05, 0.95]
 __device__ __forceinline__ double rr_probability64(D3 att) {
     double pr = att.x;
@@ -389,17 +438,17 @@ __device__ __forceinline__ double rr_probability64(D3 att) {
 #define RRT_F64_LDS_HIST 0
 #endif
 struct Hist64 {
-    Att32 *ring;     // LDS: RRT_F64_LDS_HIST x block threads
-    Att32 *global;   // P.hist
+    HRec *ring;      // LDS: RRT_F64_LDS_HIST x block threads
+    HRec *global;    // P.hist
     uint32_t lanes;  // P.hist_lanes
     uint32_t slot;   // the lane's global slot
     uint32_t tid;    // threadIdx.x
     uint32_t blk;    // block threads
-    __device__ __forceinline__ void store(uint32_t k, const Att32 &r) const {
+    __device__ __forceinline__ void store(uint32_t k, const HRec &r) const {
         if (RRT_F64_LDS_HIST > 0 && k < (uint32_t)RRT_F64_LDS_HIST) ring[k * blk + tid] = r;
         else global[(size_t)k * lanes + slot] = r;
     }
-    __device__ __forceinline__ Att32 load(uint32_t k) const {
+    __device__ __forceinline__ HRec load(uint32_t k) const {
         if (RRT_F64_LDS_HIST > 0 && k < (uint32_t)RRT_F64_LDS_HIST) return ring[k * blk + tid];
         return global[(size_t)k * lanes + slot];
     }
@@ -416,20 +465,23 @@ struct Hist64 {
 #define RRT_F64_FOLD_GROUP 4
 #endif
 template <bool kTex>
-__device__ __forceinline__ D3 fold_back64(const Hist64 &hist, uint32_t n, D3 L) {
+__device__ __forceinline__ D3 fold_back64(const Hist64 &hist, const GMaterial *__restrict__ mtl, uint32_t n, D3 L) {
     constexpr uint32_t G = RRT_F64_FOLD_GROUP;
     uint32_t k = n;
     while (k > 0u) {
         const uint32_t m = k < G ? k : G;
-        Att32 a[G];
+        HRec a[G];
 #pragma unroll
         for (uint32_t j = 0; j < G; ++j)
-            if (j < m) a[j] = RRT_F64_B2F_MODE == 2 ? Att32{0.5f, 0.5f, 0.5f} : hist.load(k - 1u - j);
+            if (j < m) a[j] = RRT_F64_B2F_MODE == 2 ? rec_one() : hist.load(k - 1u - j);
+        D3 at[G];
+#pragma unroll
+        for (uint32_t j = 0; j < G; ++j)
+            if (j < m) at[j] = rec_att<kTex>(a[j], mtl);
 #pragma unroll
         for (uint32_t j = 0; j < G; ++j) {
             if (j < m) {
-                const D3 att = kTex ? d3(att_decode(a[j].x), att_decode(a[j].y), att_decode(a[j].z))
-                                    : f2d(a[j].x, a[j].y, a[j].z);
+                const D3 att = at[j];
                 L = mul(att, L);
                 if (k - 1u - j >= 5u) L = muls(L, recip64(rr_probability64(att)));  // Div<f64>: (1/p) * v (vec3.rs:142-148)
             }
@@ -698,7 +750,7 @@ constexpr int kF64Full = 0, kF64Untextured = 1, kF64Diffuse = 2;
 template <int kClass, typename Rec>
 __device__ __forceinline__ bool shade64(const KParams &P, const Rec *prims, const GMaterial *mtl, const double *inv_r,
                                         Path64 &ps, double t, int prim, D3 &Le, const Hist64 &hist, uint32_t &pend,
-                                        Att32 &prec) {
+                                        HRec &prec) {
     Le = d3(0.0, 0.0, 0.0);
     if (prim < 0) {
         D3 bg;
@@ -737,7 +789,7 @@ __device__ __forceinline__ bool shade64(const KParams &P, const Rec *prims, cons
         return true;
     }
     D3 att, dir;
-    Att32 rec{m.a.x, m.a.y, m.a.z};  // the attenuation's history record
+    HRec rec = rec_albedo(prim, m);  // the attenuation's history record
     if (kClass != kF64Diffuse && kind == 1) {  // Metal (material.rs:53-64): unit(reflect) + fuzz * random_unit_vector
         const D3 refl = unit_vector(reflect(ps.d, nrm));
         dir = add(refl, muls(random_unit_vector(ps.rng), (double)m.a.w));
@@ -765,14 +817,13 @@ __device__ __forceinline__ bool shade64(const KParams &P, const Rec *prims, cons
         if (cannot || reflectance_r0(c, r0) > rnd64(ps.rng)) dir = reflect(ud, nrm);
         else dir = refract(ud, nrm, ri);
         att = d3(1.0, 1.0, 1.0);
-        rec = Att32{1.0f, 1.0f, 1.0f};
+        rec = rec_one();
     } else {  // Lambertian, plain or image-textured (material.rs:28-40; the_next_week/material.rs:41-53)
         att = albedo;
         if (kClass != kF64Untextured && kind == 3) {
             const uint32_t b = texel_bytes64(P, m.b.z, outward);
             att = texel_value64(b);
-            if (b == 0x1000000u) rec = Att32{0.0f, 1.0f, 1.0f};
-            else rec = Att32{-(float)(b & 0xffu), -(float)((b >> 8) & 0xffu), -(float)(b >> 16)};
+            rec = rec_texel(b);
         }
         if (RRT_F64_DEFER) {  // the scatter direction is drawn by the work loop (lambert_draw64)
             ps.o = p;
@@ -811,7 +862,7 @@ __device__ __forceinline__ bool shade64(const KParams &P, const Rec *prims, cons
 // history record. Returns 1 when the path ended (Russian roulette), 0 otherwise; pend = 0 once done.
 template <int kClass>
 __device__ __forceinline__ uint32_t lambert_draw64(const KParams &P, Path64 &ps, const Hist64 &hist, uint32_t &pend,
-                                                   const Att32 &prec) {
+                                                   const HRec &prec, const GMaterial *mtl) {
     int32_t a = 0, b = 0, c = 0;
     bool ok = false;
     for (int it = 0; it < (RRT_F64_DEFER > 0 ? RRT_F64_DEFER : 1) && !ok; ++it) {
@@ -828,8 +879,7 @@ __device__ __forceinline__ uint32_t lambert_draw64(const KParams &P, Path64 &ps,
     D3 dir = add(nrm, muls(d3(x, y, z), recip64(__builtin_sqrt(lensq))));
     if (__builtin_fabs(dir.x) < 1e-8 && __builtin_fabs(dir.y) < 1e-8 && __builtin_fabs(dir.z) < 1e-8) dir = nrm;
     if (ps.k >= 5u) {
-        const D3 att = kClass != kF64Untextured ? d3(att_decode(prec.x), att_decode(prec.y), att_decode(prec.z))
-                                                : f2d(prec.x, prec.y, prec.z);
+        const D3 att = rec_att<kClass != kF64Untextured>(prec, mtl);
         if (rnd64(ps.rng) > rr_probability64(att)) return 1u;
     }
     hist.store(ps.k, prec);
@@ -857,7 +907,7 @@ __device__ __forceinline__ void render64_body(const KParams &P) {
     const double *inv_r = P.prim_inv_r64;
     const float4 *recs32 = P.prim_cr;  // the pre-test's f32 records (center, r)
     const uint32_t stack16 = (P.stack_depth * kBlk * sizeof(uint16_t) + 15u) / 16u;
-    constexpr uint32_t kRing16 = (uint32_t)RRT_F64_LDS_HIST * kBlk * 12u / 16u;  // kBlk is a multiple of 64
+    constexpr uint32_t kRing16 = (uint32_t)RRT_F64_LDS_HIST * kBlk * (uint32_t)sizeof(HRec) / 16u;  // kBlk: a multiple of 64
     if constexpr (kLds) {  // stage nodes + spheres (+ 1/r) once per block
         uint4 *dst = lds_dyn + stack16 + kRing16;
         // Node112: each 80-B GNode re-laid as 112 B whose axis a holds both children's (lo, hi), then
@@ -923,8 +973,8 @@ __device__ __forceinline__ void render64_body(const KParams &P) {
     uint32_t tcidx = 0;      // a tail unit's chunk index within the pass
     uint32_t tmask = 0;      // a tail unit's samples with nonzero radiance (bit = sample - its first)
     uint32_t pend = 0;       // RRT_F64_DEFER: a Lambertian scatter waits for an accepted candidate
-    Att32 prec{0.0f, 0.0f, 0.0f};
-    const Hist64 hist{reinterpret_cast<Att32 *>(lds_dyn + stack16), reinterpret_cast<Att32 *>(P.hist), P.hist_lanes,
+    HRec prec{};
+    const Hist64 hist{reinterpret_cast<HRec *>(lds_dyn + stack16), reinterpret_cast<HRec *>(P.hist), P.hist_lanes,
                       blockIdx.x * (uint32_t)kBlk + threadIdx.x, threadIdx.x, (uint32_t)kBlk};
     uint64_t pkey = 0;
     D3 sum = d3(0.0, 0.0, 0.0);
@@ -1070,7 +1120,7 @@ __device__ __forceinline__ void render64_body(const KParams &P) {
             seg_done = shade64<kClass>(P, prims, mtl, inv_r, ps, tr.closest, tr.hit_prim, Le, hist, pend, prec) ? 1u : 0u;
         }
         if (RRT_F64_DEFER && pend) {
-            seg_done = lambert_draw64<kClass>(P, ps, hist, pend, prec);
+            seg_done = lambert_draw64<kClass>(P, ps, hist, pend, prec, mtl);
             need_ray = pend ? 0u : 1u;
         }
         w_paths += (uint32_t)__popcll(__ballot(seg_done));
@@ -1079,7 +1129,7 @@ __device__ __forceinline__ void render64_body(const KParams &P) {
             // the radiance at the path's end carried back through its scatters; a path that ended
             // with none (absorbed, Russian roulette, max_depth) adds an exact 0
             if (Le.x != 0.0 || Le.y != 0.0 || Le.z != 0.0)
-                Le = fold_back64<kClass != kF64Untextured>(hist, ps.k, Le);
+                Le = fold_back64<kClass != kF64Untextured>(hist, mtl, ps.k, Le);
 #endif
             const auto &Q = *kernarg_params();
             if (tail) {  // a tail sample: its radiance, folded into the pixel's sum in order later
@@ -1158,7 +1208,12 @@ __host__ __device__ constexpr int blk64(int cls) { return cls == 0 ? 512 : kBloc
 // LDS one block may declare: 160 KiB on gfx950 (MI355X_MICROARCH.md occupancy section) when the
 // block is the CU's only one (1024 threads at 4 waves/SIMD), else the 64 KiB that keeps two
 // 512-thread blocks per CU
-__host__ __device__ constexpr size_t lds_budget64(int blk) { return blk >= 1024 ? 160u * 1024u : 64u * 1024u; }
+#ifndef RRT_F64_LDS512_KB
+#define RRT_F64_LDS512_KB 64
+#endif
+__host__ __device__ constexpr size_t lds_budget64(int blk) {
+    return blk >= 1024 ? 160u * 1024u : (size_t)RRT_F64_LDS512_KB * 1024u;
+}
 
 template <int kMode, bool kCount, int kClass>
 __global__ __launch_bounds__(blk64(kClass), kClass == kF64Full ? 1 : RRT_F64_WAVES) void rrt_render64(KParams P) {
@@ -1219,7 +1274,7 @@ __global__ __launch_bounds__(256) void rrt_accum64_to_f32(const D4 *__restrict__
 // p.inv_r_in_lds)
 size_t lds64_bytes(const KParams &p, int mode, int blk = kBlock64) {
     size_t lds = ((size_t)p.stack_depth * blk * sizeof(uint16_t) + 15u) / 16u * 16u;
-    lds += (size_t)RRT_F64_LDS_HIST * blk * 12u;  // the history ring
+    lds += (size_t)RRT_F64_LDS_HIST * blk * sizeof(HRec);  // the history ring
     if (mode != kF64Global)
         lds += (size_t)p.n_nodes * 112u +
                (size_t)p.n_prims * ((mode == kF64LdsWide ? sizeof(Sphere64) : sizeof(float4)) +
@@ -1240,7 +1295,7 @@ size_t f64_lds_min_bytes(uint32_t n_nodes, uint32_t n_prims, uint32_t stack_dept
     p.rec32_in_lds = 0u;
     // the host's staging rule (rrt_host.cpp scene_bvh): the 512-thread block's layout without the
     // history ring within 64 KB, whatever block the classes launch
-    return lds64_bytes(p, kF64Lds, 512) - (size_t)RRT_F64_LDS_HIST * 512u * 12u;
+    return lds64_bytes(p, kF64Lds, 512) - (size_t)RRT_F64_LDS_HIST * 512u * sizeof(HRec);
 }
 
 namespace {

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Debug-statistics pass: the f64 kernel's RRT_F64_STATS variants (variants/s1..s4) on C2 and C5,
+# Debug-statistics pass (round 5): the f64 kernel's RRT_F64_STATS variants (variants/s1..s4) on C2 and C5,
 # and the f32 kernel's RRT_PHASE_TIMING=8 variant (variants/p8: node steps whose stepping lanes all
 # visit one node) on C5 and final_scene (NW9). Each line: config, counters (slots 2..4 = the stats).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
