@@ -51,7 +51,7 @@ mod imp {
     /// The books path's f64 arithmetic (RRT_FLAG_F64): checked against `--backend cpu` output.
     pub const RRT_FLAG_F64: u32 = 0x8;
     /// ABI this shim was written against (RRT_ABI_VERSION).
-    pub const RRT_ABI_VERSION: u32 = 10;
+    pub const RRT_ABI_VERSION: u32 = 11;
 
     #[link(name = "rrt_hip")]
     extern "C" {

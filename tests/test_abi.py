@@ -61,7 +61,7 @@ int main(void) { return 0; }
 
 
 def test_abi_version():
-    assert _lib.load().rrt_hip_abi_version() == 10
+    assert _lib.load().rrt_hip_abi_version() == 11
 
 
 def test_tile_rows_match_python_partition():
