@@ -40,7 +40,7 @@ extern "C" {
  * (test-only entry points, no drop-in counterpart); 10: tail chunks of K/4 samples (was K/8), the
  * f64 books path's sums in camera.rs:72-76's sample order with the throughput formed back to front
  * (bit-identical to the books path), rrt_testing_f64_layout; 11: frames of at most
- * rrt_accum_chunk() samples keep tail chunks of K/8. */
+ * rrt_accum_chunk() / 4 samples (no big chunk) keep tail chunks of K/8. */
 #define RRT_ABI_VERSION 11u
 
 /* ---- scene ABI (== src/gpu/mod.rs:13-42) ------------------------------------------ */
@@ -267,8 +267,8 @@ uint32_t rrt_hip_abi_version(void);
  * (counted from the tile's sample_begin) of each chunk's in-order sample sum, chunks added in
  * order: ((c0 + c1) + c2) + ... With K = rrt_accum_chunk() halved while S <= 2K, down to
  * rrt_accum_chunk() / 4 (ABI v9: 256 for S > 512, 128 for 256 < S <= 512, 64 below; big chunks at
- * high spp, small ones at low spp), and k = max(1, K / 4) for S > rrt_accum_chunk(), max(1, K / 8)
- * for S <= rrt_accum_chunk() (ABI v11; K / 8 for every S before v10): the first
+ * high spp, small ones at low spp), and k = max(1, K / 4), or max(1, K / 8) for
+ * S <= rrt_accum_chunk() / 4 (ABI v11; K / 8 for every S before v10): the first
  * nb = (S - 1) / K chunks hold K samples each (nb = 0 when S <= K), the remaining S - nb*K
  * samples form chunks of k (the last one possibly shorter) — small units at the end of the
  * work queue keep the persistent grid's tail short. Needed to reproduce it bit for bit.

@@ -18,7 +18,7 @@ TWIN, BOOKS = 0, 1
 # Accum summation chunk of the HIP backend (include/rrt_hip.h rrt_accum_chunk): a frame of S
 # samples uses K = DEFAULT_CHUNK halved while S <= 2K, down to DEFAULT_CHUNK / 4 (256 for S > 512,
 # 128 for 256 < S <= 512, 64 below); (S-1)/K chunks of K samples, then chunks of max(1, K/4) for the
-# tail (max(1, K/8) when S <= DEFAULT_CHUNK); samples summed in order within a chunk, chunk sums added in order. The f32 kernel sums in
+# tail (max(1, K/8) when S <= DEFAULT_CHUNK / 4); samples summed in order within a chunk, chunk sums added in order. The f32 kernel sums in
 # that schedule; the f64 books kernel (RRT_FLAG_F64) sums every pixel's samples in sample order, the
 # reference's own order (camera.rs:72-76), which is BOOKS' default here (chunk 0 = one chunk).
 DEFAULT_CHUNK = 256

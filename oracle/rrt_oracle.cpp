@@ -1727,7 +1727,7 @@ int render(const RrtCamera *c, const RrtSphere *s, uint32_t n, const RrtMaterial
                 const uint64_t rays_before = tl.rays;
                 // accum order of the kernel (rrt_accum_chunk, include/rrt_hip.h): in-order sums
                 // over chunks from s0 — (S-1)/K chunks of K samples, then chunks of max(1, K/4)
-                // (max(1, K/8) when S <= K0) for the rest (chunk 0 = one chunk) — chunk sums added
+                // (max(1, K/8) when S <= K0/4) for the rest (chunk 0 = one chunk) — chunk sums added
                 // in order
                 Vec3<T> sum = mk(T(0), T(0), T(0));
                 const uint32_t S = s1 - s0;
@@ -1735,7 +1735,7 @@ int render(const RrtCamera *c, const RrtSphere *s, uint32_t n, const RrtMaterial
                 // include/rrt_hip.h; rrt_host.cpp)
                 uint32_t big = chunk ? chunk : (S ? S : 1);
                 while (chunk && big > std::max(1u, chunk / 4u) && S <= 2u * big) big /= 2u;
-                const uint32_t small = chunk ? std::max(1u, big / (S <= chunk ? 8u : 4u)) : big;
+                const uint32_t small = chunk ? std::max(1u, big / (S <= chunk / 4u ? 8u : 4u)) : big;
                 const uint32_t nb = (chunk && S > big) ? (S - 1u) / big : 0u;
                 for (uint32_t c0 = s0; c0 < s1;) {
                     const uint32_t step = (c0 - s0) < nb * big ? big : small;

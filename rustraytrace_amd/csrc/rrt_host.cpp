@@ -1013,18 +1013,18 @@ int fill_params(RrtScene *s, const RrtTile *t, float *d_accum, rrt::KParams &p) 
 #ifdef RRT_CHUNK_FORCE  // A/B builds only (tools/build_variants.sh): a fixed chunk outside the ABI's rule
     p.chunk = std::max(1u, (uint32_t)RRT_CHUNK_FORCE);
 #endif
-// tail chunks of K/4 above K0 samples (ABI v10; K/8 before): a quarter of C2's chunk partials fewer
-// (7 instead of 11 per pixel, ~100 MB less HBM written and read per launch), same-box C2 +0.3 %,
-// C4 +0.6 %. Frames of at most K0 samples keep K/8 (ABI v11): their units are few per lane, so the
-// queue's drain is what the tail chunks buy — same-box final_scene (64 spp) +6.4 % over K/4, C5
-// (256 spp) +0.2 % (profiles/r5_ab_tail_div.log)
+// tail chunks of K/4 (ABI v10; K/8 before): a quarter of C2's chunk partials fewer (7 instead of 11
+// per pixel, ~100 MB less HBM written and read per launch), same-box C2 +0.3 %, C4 +0.6 %, C5 ±0.2 %.
+// Frames of at most K0/4 samples, which are all tail (no big chunk), keep K/8 (ABI v11): their units
+// are few per lane, so the queue's drain is what the small chunks buy — same-box final_scene
+// (64 spp) +6.4 % over K/4 (profiles/r5_ab_tail_div.log)
 #ifndef RRT_TAIL_DIV
 #define RRT_TAIL_DIV 4
 #endif
 #ifndef RRT_TAIL_DIV_LO
 #define RRT_TAIL_DIV_LO 8
 #endif
-    p.chunk_small = std::max(1u, p.chunk / (S <= k0 ? RRT_TAIL_DIV_LO : RRT_TAIL_DIV));
+    p.chunk_small = std::max(1u, p.chunk / (S <= k0 / 4u ? RRT_TAIL_DIV_LO : RRT_TAIL_DIV));
     p.n_big = S > p.chunk ? (S - 1u) / p.chunk : 0u;
     const uint32_t tail = S - p.n_big * p.chunk;
     p.n_chunks = S ? p.n_big + (tail + p.chunk_small - 1u) / p.chunk_small : 0u;
@@ -1118,7 +1118,7 @@ int fill_params(RrtScene *s, const RrtTile *t, float *d_accum, rrt::KParams &p) 
     return RRT_OK;
 }
 
-// The largest big chunk K0 (tail chunks K/4, K/8 for frames of at most K0 samples; the frame's K: rrt_accum_chunk's rule, halved while
+// The largest big chunk K0 (tail chunks K/4, K/8 for frames of at most K0/4 samples; the frame's K: rrt_accum_chunk's rule, halved while
 // S <= 2K down to K0/4). 128 in round 2 (with 8 work queues the per-unit cost matters more than the
 // drain: C2 +1.2 %, C4 +10 %, C5 -0.5 % against 64); 256 since round 4 for frames over 512 samples:
 // C4 +2.4 %, C3 +0.8 % same-box, C2 and C5 keep 128 and 64 (K = 256 at C2's 512 spp: -0.3 %).

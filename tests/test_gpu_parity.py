@@ -136,12 +136,15 @@ def test_multi_gpu_one_shot_equals_single():
         rrt.render(scene, n_gpus=n + 1)
 
 
-@pytest.mark.parametrize("spp,s0", [(200, 0), (130, 7), (128, 0), (100, 3), (9, 0), (129, 0), (300, 0), (600, 0)])
+@pytest.mark.parametrize("spp,s0", [(200, 0), (130, 7), (128, 0), (100, 3), (9, 0), (129, 0), (300, 0), (600, 0),
+                                    (256, 0), (257, 0), (64, 0), (65, 0)])
 def test_chunked_accumulation_matches_oracle(spp, s0):
-    # rrt_accum_chunk() = 256; frames of S <= 256 samples use K = 64 (tail chunks of K/8 = 8), up
-    # to 512 K = 128 (tail chunks of K/4 = 32), larger ones K = 256 (tail chunks of 64): (128, 0):
-    # 64 + 8 x 8; (100, 3): 64 + 4 x 8 + 4; (9, 0): 8 + 1; (129, 0): 2 x 64 + 1; (200, 0): 3 x 64 + 8;
-    # (300, 0): 2 x 128 + 32 + 12; (600, 0): 2 x 256 + 64 + 24.
+    # rrt_accum_chunk() = 256; frames of S <= 256 samples use K = 64 (tail chunks of K/4 = 16, or
+    # K/8 = 8 when S <= 64: no big chunk), up to 512 K = 128 (tail chunks of 32), larger ones K = 256
+    # (tail chunks of 64): (128, 0): 64 + 4 x 16; (100, 3): 64 + 2 x 16 + 4; (9, 0): 8 + 1; (129, 0):
+    # 2 x 64 + 1; (200, 0): 3 x 64 + 8; (300, 0): 2 x 128 + 32 + 12; (600, 0): 2 x 256 + 64 + 24;
+    # (256, 0): 3 x 64 + 4 x 16; (257, 0): 2 x 128 + 1; the ABI v11 boundary: (64, 0): 8 x 8,
+    # (65, 0): 64 + 1.
     # > rrt_accum_chunk() samples: the persistent queue splits pixels into chunks whose sums are
     # combined in chunk order; the oracle reproduces that order (rows, partial last chunk, offset).
     assert rrt._lib.load().rrt_accum_chunk() == oracle.DEFAULT_CHUNK

@@ -449,10 +449,10 @@ def test_bvh2_node_layouts_hold_the_same_tree(monkeypatch):
 
 
 @pytest.mark.parametrize("S,chunk", [(20, 8), (512, 64), (64, 64), (65, 64), (7, 0), (300, 128), (256, 128),
-                                     (600, 256), (513, 256), (512, 256), (256, 256)])
+                                     (600, 256), (513, 256), (512, 256), (256, 256), (257, 256), (64, 256), (65, 256)])
 def test_accum_chunk_schedule(S, chunk):
     """The TWIN accum groups samples as rrt_accum_chunk documents (include/rrt_hip.h): (S-1)/K
-    chunks of K, then chunks of max(1, K/4), or max(1, K/8) when S <= chunk (ABI v11); in-order f32 sums per chunk, chunks added in order."""
+    chunks of K, then chunks of max(1, K/4), or max(1, K/8) when S <= chunk / 4 (ABI v11); in-order f32 sums per chunk, chunks added in order."""
     sc = rrt.config_scene("C1", image_width=8, samples_per_pixel=S, max_depth=4)
     got, _, _ = oracle.render(sc, oracle.TWIN, chunk=chunk)
     per = [oracle.render(sc, oracle.TWIN, samples=(s, s + 1))[0][..., :3].astype(np.float32)
@@ -460,7 +460,7 @@ def test_accum_chunk_schedule(S, chunk):
     K = chunk if chunk else S  # the frame's chunk: halved while S <= 2K, down to chunk / 4
     while chunk and K > max(1, chunk // 4) and S <= 2 * K:
         K //= 2
-    k = max(1, K // (8 if S <= chunk else 4)) if chunk else S
+    k = max(1, K // (8 if S <= chunk // 4 else 4)) if chunk else S
     nb = (S - 1) // K if chunk and S > K else 0
     bounds, c0 = [], 0
     while c0 < S:
