@@ -299,8 +299,8 @@ def f64_books_frame(config, frames=2, issue_json=None):
         "note": "f64 VALU issue bound: the books path's 23 FLOP per sphere test + 12 FLOP per box test (SURVEY 8d), "
                 "all f64 in the reference, over the HIP-event time of the frame (render passes + in-order folds); "
                 "peak = MI355X FP64 vector 78.6 TFLOP/s (AMD spec: half the FP32 rate). The kernel runs the box test "
-                "and a sphere pre-test in f32 with proven bounds (rrt_box32.h, rrt_sphere32.h), so part of the work "
-                "priced here at f64 issues at the f32 rate",
+                "in f32 with a proven bound (rrt_box32.h), so part of the work priced here at f64 issues at the f32 "
+                "rate (the f32 sphere pre-test of rrt_sphere32.h is built but off: RRT_F64_SPHERE32=0)",
     }
     traffic, traffic_src = load_traffic(os.path.join(ROOT, "profiles", f"traffic_{config}_f64.json"), config,
                                         scene.width, scene.spp, rrt._lib.LIB_PATH)
