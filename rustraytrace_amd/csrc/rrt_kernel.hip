@@ -48,6 +48,9 @@ namespace {
 #ifndef RRT_DEBUG_NOREJECT
 #define RRT_DEBUG_NOREJECT 0
 #endif
+#ifndef RRT_DEBUG_EXTRA_NODE_LOAD
+#define RRT_DEBUG_EXTRA_NODE_LOAD 0
+#endif
 // Wave issue priority per loop phase (s_setprio levels 0-3; see the work loop's head).
 #ifndef RRT_PRIO_REFILL
 #define RRT_PRIO_REFILL 2
@@ -638,10 +641,32 @@ __device__ __forceinline__ bool trav_node(const Node *__restrict__ nodes, Stack 
         // the min/max slab (per-lane dword gathers cost more there than the min/max)
         const uint4 *q = reinterpret_cast<const uint4 *>(nodes + t.node);
         const uint4 a = q[0], b = q[1];
+#if RRT_DEBUG_EXTRA_NODE_LOAD == 1  // debug builds only: one more 16-B load of the same node (prices node bytes)
+        {
+            const uint4 *q2 = q;
+            asm volatile("" : "+v"(q2));
+            const uint4 c = q2[0];
+            asm volatile("" ::"v"(c.x ^ c.y ^ c.z ^ c.w));
+        }
+#endif
+#if RRT_DEBUG_EXTRA_NODE_LOAD == 2  // debug: a second load that waits for the first and that the next node waits for
+        uint32_t dep_zero;  // (prices one more L2 round trip in the node-to-node chain)
+        {
+            uint32_t z = a.x;
+            asm volatile("v_and_b32 %0, 0, %0" : "+v"(z));
+            const uint4 c = q[z];
+            dep_zero = c.x;
+            asm volatile("v_and_b32 %0, 0, %0" : "+v"(dep_zero));
+        }
+#endif
         h0 = box_hit(lo16(a.x), hi16(a.x), lo16(a.y), hi16(a.y), lo16(a.z), hi16(a.z), rk.inv, rk.oi, 0.001f, t.closest, tn0);
         h1 = box_hit(lo16(a.w), hi16(a.w), lo16(b.x), hi16(b.x), lo16(b.y), hi16(b.y), rk.inv, rk.oi, 0.001f, t.closest, tn1);
         l0 = b.z;
         l1 = b.w;
+#if RRT_DEBUG_EXTRA_NODE_LOAD == 2
+        l0 += dep_zero;
+        l1 += dep_zero;
+#endif
     }
     // Leaf children (count in the link's top bits, 0 = internal) are postponed; the hit ones
     // form one range: sibling leaves are adjacent in primitive order, so l0's first primitive
