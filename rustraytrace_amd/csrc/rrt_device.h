@@ -31,9 +31,30 @@ struct RngState {
     uint32_t a, b, c, d;
 };
 __device__ __forceinline__ uint32_t rotl32(uint32_t x, int k) { return (x << k) | (x >> (32 - k)); }
+// x ^ y ^ z in one gfx950 V_BITOP3_B32 (truth table 0x96)
+__device__ __forceinline__ uint32_t xor3_32(uint32_t x, uint32_t y, uint32_t z) {
+    return __builtin_amdgcn_bitop3_b32(x, y, z, 0x96);
+}
+// xoshiro128+ (c ^= a; d ^= b; b ^= c; a ^= d; c ^= b << 9; d = rotl(d, 11); result a + d before
+// the step), its two chained xors per word folded into three-input xors: 7 VALU instructions per
+// draw instead of 8, the same state sequence (tests/test_rng_bitop3.py checks the algebra).
+// RRT_RNG_BITOP3=0: the two-input form.
+#ifndef RRT_RNG_BITOP3
+#define RRT_RNG_BITOP3 1
+#endif
 __device__ __forceinline__ uint32_t rng_next(RngState &s) {
     const uint32_t r = s.a + s.d;
     const uint32_t t = s.b << 9;
+    if (RRT_RNG_BITOP3) {
+        const uint32_t db = s.d ^ s.b;
+        const uint32_t b = xor3_32(s.b, s.c, s.a);
+        const uint32_t c = xor3_32(s.c, s.a, t);
+        s.a ^= db;
+        s.b = b;
+        s.c = c;
+        s.d = rotl32(db, 11);
+        return r;
+    }
     s.c ^= s.a;
     s.d ^= s.b;
     s.b ^= s.c;
