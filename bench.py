@@ -389,6 +389,7 @@ def wall_clock_breakdown(scene, accum, kernel_ms):
     average), D2H of the float accum, P3 formatting (render_io.rs), and the end-to-end drop-in
     call rrt_hip_render (scene + kernel + D2H) plus the P3 write (render_io::write_ppm_from_accum
     to /dev/null)."""
+    import numpy as np
     import torch
 
     import rustraytrace_amd as rrt
@@ -406,7 +407,11 @@ def wall_clock_breakdown(scene, accum, kernel_ms):
     torch.cuda.synchronize()
     host, d2h_ms = timed(lambda: accum.cpu())
     _, fmt_ms = timed(lambda: rrt.write_ppm_from_accum(scene.width, scene.height, host.numpy(), scene.spp, os.devnull))
-    e2e_accum, render_ms = timed(lambda: rrt.render(scene, n_gpus=1))
+    # the drop-in call three times: the first in the process pays the one-shot call's device
+    # allocations and the first touch of the caller's fresh 33-MB host array; the line reports it
+    # and the median of the two that follow
+    e2e_accum, render_first_ms = timed(lambda: rrt.render(scene, n_gpus=1))
+    render_ms = float(np.median([timed(lambda: rrt.render(scene, n_gpus=1))[1] for _ in range(2)]))
     # the same call as the Rust shim and the CLI make it (flags 0: progress lines on stderr, the
     # work-queue heads read every 100 ms, the end noticed within ~1 ms)
     _, progress_ms = timed(lambda: rrt.render(scene, n_gpus=1, quiet=False))
@@ -422,7 +427,9 @@ def wall_clock_breakdown(scene, accum, kernel_ms):
         "d2h_ms": round(d2h_ms, 3),
         "ppm_write_ms": round(fmt_ms, 3),
         "end_to_end_ms": round(render_ms + fmt2_ms, 3),
-        "end_to_end_note": "rrt_hip_render (BVH build, H2D, kernel, D2H, 1 GPU) + P3 write of the frame",
+        "end_to_end_first_call_ms": round(render_first_ms + fmt2_ms, 3),
+        "end_to_end_note": "rrt_hip_render (BVH build, H2D, kernel, D2H, 1 GPU) + P3 write of the frame; "
+                           "end_to_end_ms: median of the 2nd and 3rd calls in the process, first_call: the 1st",
         "render_with_progress_ms": round(progress_ms, 3),
         "progress_note": "rrt_hip_render without RRT_FLAG_QUIET (as the Rust shim and the CLI call it), no P3 write",
         "end_to_end_rgb8_p3_ms": round(rgb8_ms + p3_ms, 3),
