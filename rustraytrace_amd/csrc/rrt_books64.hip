@@ -113,7 +113,7 @@ __device__ __forceinline__ double rnd64(RngState &s) { return (double)(rng_next(
 // (tests/test_rejection_exact.py). The loops compute S in 64-bit integers from 24-bit signed
 // multiplies (full-rate VALU) instead of the reference's f64 conversions, products and sums
 // (half-rate): same draws, same decisions, same accepted point, which is converted once.
-__device__ __forceinline__ int32_t draw_centred(RngState &s) { return rng_next_centred(s); }  // (r >> 8) - 2^23
+__device__ __forceinline__ int32_t draw_centred(RngState &s) { return (int32_t)(rng_next(s) >> 8) - 8388608; }
 __device__ __forceinline__ uint64_t sq_i24(int32_t a) { return (uint64_t)((int64_t)a * (int64_t)a); }
 // The same decisions from f32 arithmetic where it is provably decisive (RRT_F64_REJ32): the f32
 // sum of squares of the exact coordinates a, b, c (|a| <= 2^23: exact in f32) is within 3u S

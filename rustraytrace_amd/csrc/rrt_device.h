@@ -13,9 +13,9 @@ __device__ __forceinline__ uint32_t wave_slot() {
 // ---- RNG: xoshiro128+ per path, keyed by (seed, pixel, sample) ------------------------------
 // Counter-based in effect: the i-th draw of a path is a pure function of
 // (seed, global pixel index, sample index, i); nothing depends on lane or launch shape.
-// xoshiro128+ (Blackman & Vigna) is all full-rate 32-bit VALU (add, shift, xor, alignbit,
-// gfx950's three-input bitop3): 7 instructions per draw against ~17 with three quarter-rate
-// multiplies for the 64-bit LCG of a PCG32 (+4.3 % on C2, same-box A/B). Only the top 24 bits of each output are used
+// xoshiro128+ (Blackman & Vigna) is all full-rate 32-bit VALU (add, shift, xor, alignbit):
+// 8 instructions per draw against ~17 with three quarter-rate multiplies for the 64-bit LCG
+// of a PCG32 (+4.3 % on C2, same-box A/B). Only the top 24 bits of each output are used
 // (random_double), the bits the authors recommend for floating-point generation.
 // f16 planes of a GNodeH (exact conversions; in an FMA operand they become v_fma_mix_f32)
 __device__ __forceinline__ float lo16(uint32_t v) { return (float)__builtin_bit_cast(_Float16, (uint16_t)(v & 0xffffu)); }
@@ -42,7 +42,8 @@ __device__ __forceinline__ uint32_t xor3_32(uint32_t x, uint32_t y, uint32_t z) 
 #ifndef RRT_RNG_BITOP3
 #define RRT_RNG_BITOP3 1
 #endif
-__device__ __forceinline__ void rng_advance(RngState &s) {
+__device__ __forceinline__ uint32_t rng_next(RngState &s) {
+    const uint32_t r = s.a + s.d;
     const uint32_t t = s.b << 9;
     if (RRT_RNG_BITOP3) {
         const uint32_t db = s.d ^ s.b;
@@ -52,7 +53,7 @@ __device__ __forceinline__ void rng_advance(RngState &s) {
         s.b = b;
         s.c = c;
         s.d = rotl32(db, 11);
-        return;
+        return r;
     }
     s.c ^= s.a;
     s.d ^= s.b;
@@ -60,20 +61,7 @@ __device__ __forceinline__ void rng_advance(RngState &s) {
     s.a ^= s.d;
     s.c ^= t;
     s.d = rotl32(s.d, 11);
-}
-__device__ __forceinline__ uint32_t rng_next(RngState &s) {
-    const uint32_t r = s.a + s.d;
-    rng_advance(s);
     return r;
-}
-// The next draw's 24-bit value centred, (r >> 8) - 2^23 in [-2^23, 2^23): r ^ 2^31 = r + 2^31
-// (mod 2^32), so it is (r + 2^31) >> 8 as a signed shift — a v_add3_u32 (the draw's own add) and a
-// v_ashrrev_i32, one instruction less than shift-and-subtract. u * 2^-23 - 1 (rnd_pm1) equals this
-// value times 2^-23 exactly, so the rejection loops test the candidate's scaled |p|^2 on it.
-__device__ __forceinline__ int32_t rng_next_centred(RngState &s) {
-    const uint32_t rc = s.a + s.d + 0x80000000u;
-    rng_advance(s);
-    return (int32_t)rc >> 8;
 }
 // state = (z, pixel key); the low bit of the last word is forced so the state is never zero
 __device__ __forceinline__ RngState rng_seed(uint64_t z, uint64_t key) {

@@ -135,23 +135,18 @@ __device__ __forceinline__ V3 unit(V3 v) {
 // (1e-160 underflows to 0 in f32: the one intentional f32 deviation).
 // The loop only draws and tests; the normalisation runs once after it, with the wave
 // converged (inside the loop it would run in every iteration in which any lane accepts).
-// The loop runs on the candidates scaled by 2^23 (the centred 24-bit draws, exact in f32): each
-// rounding of the |p|^2 chain then happens 2^46 times larger, with no underflow (a nonzero term is
-// >= 1), so its result is |p|^2 * 2^46 exactly and the test against 2^46 decides as the test
-// against 1 does — one instruction less per draw than rnd_pm1's shift-convert-fma.
 template <typename C>
 __device__ __forceinline__ V3 random_unit_vector(RngState &s, C &cnt) {
-    float fa, fb, fc, l;
+    float px, py, pz, lensq;
     for (;;) {
         if constexpr (RRT_PHASE_TIMING == 4) cnt.d2 += wave_slot();
-        fa = (float)rng_next_centred(s);
-        fb = (float)rng_next_centred(s);
-        fc = (float)rng_next_centred(s);
-        l = __builtin_fmaf(fc, fc, __builtin_fmaf(fb, fb, fa * fa));  // |p|^2 * 2^46
-        if (RRT_DEBUG_NOREJECT || (0.0f < l && l <= 0x1.0p46f)) break;  // (debug: first candidate)
+        px = rnd_pm1(s);
+        py = rnd_pm1(s);
+        pz = rnd_pm1(s);
+        lensq = __builtin_fmaf(pz, pz, __builtin_fmaf(py, py, px * px));
+        if (RRT_DEBUG_NOREJECT || (0.0f < lensq && lensq <= 1.0f)) break;  // (debug: first candidate)
     }
-    const float px = fa * 0x1.0p-23f, py = fb * 0x1.0p-23f, pz = fc * 0x1.0p-23f;  // rnd_pm1's values
-    const float inv = recip_rn(sqrt_rn_big(l * 0x1.0p-46f));  // |p|^2 >= 2^-46
+    const float inv = recip_rn(sqrt_rn_big(lensq));  // lensq >= 2^-46
     return v3(px * inv, py * inv, pz * inv);
 }
 
@@ -823,14 +818,13 @@ __device__ __forceinline__ void camera_ray(const KParams &P, uint32_t x, uint32_
                          C.p00[2] + C.du[2] * fi + C.dv[2] * fj);
     V3 origin = v3(C.center[0], C.center[1], C.center[2]);
     if (C.defocus_radius > 0.0f) {
-        float fa, fb;
-        for (;;) {  // vec3.rs:172-179 random_in_unit_disk, on the 2^23-scaled candidates (random_unit_vector)
+        float px, py;
+        for (;;) {  // vec3.rs:172-179 random_in_unit_disk
             if constexpr (RRT_PHASE_TIMING == 7) cnt.d2 += wave_slot();
-            fa = (float)rng_next_centred(ps.rng);
-            fb = (float)rng_next_centred(ps.rng);
-            if (__builtin_fmaf(fb, fb, fa * fa) < 0x1.0p46f) break;
+            px = rnd_pm1(ps.rng);
+            py = rnd_pm1(ps.rng);
+            if (__builtin_fmaf(py, py, px * px) < 1.0f) break;
         }
-        const float px = fa * 0x1.0p-23f, py = fb * 0x1.0p-23f;
         origin = v3(C.center[0] + C.disk_u[0] * px + C.disk_v[0] * py,
                     C.center[1] + C.disk_u[1] * px + C.disk_v[1] * py,
                     C.center[2] + C.disk_u[2] * px + C.disk_v[2] * py);
