@@ -1100,7 +1100,10 @@ int fill_params(RrtScene *s, const RrtTile *t, float *d_accum, rrt::KParams &p) 
     p.accum64 = nullptr;
     if (s->f64) {  // the attenuation history: max_depth records of 12 B per lane slot
         const uint64_t per_lane = (uint64_t)std::max(1u, p.max_depth) * 12u;
-        uint64_t lanes = (uint64_t)p.n_cus * 1024u;  // 4 waves per SIMD x 4 SIMDs x 64 (the f64 kernel's bound)
+#ifndef RRT_F64_HIST_LANES_PER_CU
+#define RRT_F64_HIST_LANES_PER_CU 1024  // 4 waves per SIMD x 4 SIMDs x 64 (the f64 kernel's bound)
+#endif
+        uint64_t lanes = (uint64_t)p.n_cus * RRT_F64_HIST_LANES_PER_CU;
         lanes = std::min<uint64_t>(lanes, (4ull << 30) / per_lane / 512u * 512u);
         if (lanes < 8u * 512u) return fail(RRT_E_INVALID, "RRT_FLAG_F64: max_depth too large for the attenuation history");
         const size_t need = (size_t)(lanes * per_lane);
