@@ -40,7 +40,7 @@ extern "C" {
  * (test-only entry points, no drop-in counterpart); 10: tail chunks of K/4 samples (was K/8), the
  * f64 books path's sums in camera.rs:72-76's sample order with the throughput formed back to front
  * (bit-identical to the books path), rrt_testing_f64_layout; 11: frames of at most
- * rrt_accum_chunk() / 4 samples (no big chunk) keep tail chunks of K/8. */
+ * rrt_accum_chunk() / 4 samples (no big chunk) keep tail chunks of K/8; rrt_testing_trig32_check. */
 #define RRT_ABI_VERSION 11u
 
 /* ---- scene ABI (== src/gpu/mod.rs:13-42) ------------------------------------------ */
@@ -572,6 +572,12 @@ void rrt_testing_f64_layout(int32_t layout);
  * patterns +-0 or |s| >= 2^-96 of either sign (negatives, infinities and NaN included) whose square
  * root differs from the IEEE one (tests/test_gpu_recip.py: all 0). */
 int32_t rrt_testing_recip_check(uint64_t *mismatches);
+
+/* Test support, not part of the drop-in (ABI v11): the largest absolute errors of the device's f32
+ * acosf over every f32 in [-1, 1] (out[0]) and atanf over every f32 in [0, 1] (out[1]) against its
+ * f64 acos / atan, and the bounds the f64 kernel's texel enclosures assume for them (out[2],
+ * out[3]; tests/test_gpu_trig32.py: each error at most half its bound). */
+int32_t rrt_testing_trig32_check(double *out);
 
 #ifdef __cplusplus
 }

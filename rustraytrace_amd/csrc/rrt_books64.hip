@@ -325,25 +325,101 @@ __device__ __forceinline__ double div_by_const64(double x, double c) {
 // theta = acos(-y), phi = atan2(-z, x) + pi, u = phi / (2 pi), v = theta / pi. The texel's bytes
 // r | g << 8 | b << 16 (value = (1/255) byte, rtw_image.rs:46-55), or 0x1000000 for a texture with no
 // data (the solid cyan (0, 1, 1) of texture.rs:91-93).
-__device__ __forceinline__ uint32_t texel_bytes64(const KParams &P, int tex, D3 outward) {
-    const double theta = rrt_acos64(-outward.y);
-    const double phi = rrt_atan2_64(-outward.z, outward.x) + kPiD;
+#ifndef RRT_DEBUG_F64_TEXEL_FIXED  // debug builds only: no acos / atan2 (prices them; wrong images)
+#define RRT_DEBUG_F64_TEXEL_FIXED 0
+#endif
+__device__ __forceinline__ int as_i32_rs(double x) {  // Rust `as i32`: saturating, NaN -> 0
+    if (!(x == x)) return 0;
+    if (x <= -2147483648.0) return (int)0x80000000;
+    if (x >= 2147483647.0) return 0x7fffffff;
+    return (int)x;
+}
+// The texel column of phi and the row of theta (Interval::clamp, 1 - v, the image scale, `as i32`,
+// rtw_image.rs:51-52, 70-78's clamp). Every step is monotone — a correctly rounded division or
+// product by a positive constant, a clamp, 1 - v, a truncation — so the column is non-decreasing in
+// phi and the row non-increasing in theta.
+__device__ __forceinline__ int texel_col64(double phi, int w) {
     double u = div_by_const64(phi, 2.0 * kPiD);
+    u = u < 0.0 ? 0.0 : (u > 1.0 ? 1.0 : u);
+    const int i = as_i32_rs(u * (double)w);
+    return i < 0 ? 0 : (i < w ? i : w - 1);
+}
+__device__ __forceinline__ int texel_row64(double theta, int h) {
     double v = div_by_const64(theta, kPiD);
-    const GTexture t = P.texs[tex];
-    if (t.height <= 0) return 0x1000000u;                      // texture.rs:91-93: (0, 1, 1)
-    u = u < 0.0 ? 0.0 : (u > 1.0 ? 1.0 : u);                   // Interval::clamp
     v = 1.0 - (v < 0.0 ? 0.0 : (v > 1.0 ? 1.0 : v));
-    auto as_i32 = [](double x) -> int {                        // Rust `as i32`: saturating, NaN -> 0
-        if (!(x == x)) return 0;
-        if (x <= -2147483648.0) return (int)0x80000000;
-        if (x >= 2147483647.0) return 0x7fffffff;
-        return (int)x;
-    };
-    int i = as_i32(u * (double)t.width);
-    int j = as_i32(v * (double)t.height);
-    i = i < 0 ? 0 : (i < t.width ? i : t.width - 1);           // rtw_image.rs:51-52, 70-78
-    j = j < 0 ? 0 : (j < t.height ? j : t.height - 1);
+    const int j = as_i32_rs(v * (double)h);
+    return j < 0 ? 0 : (j < h ? j : h - 1);
+}
+
+// The texel decided from f32 angles where that is provably the books path's texel: an enclosure
+// [lo, hi] of rrt_acos64(-y) (of rrt_atan2_64(-z, x)) from the device's f32 acosf (atanf) with
+// bounded error; the row (column) at both ends of it is the row (column) at the f64 angle when the
+// two agree, by the monotonicity above. Else, and for arguments outside the enclosures' domains, the
+// f64 fdlibm angle itself (one lookup in a few thousand on C4). The error bounds are at least twice
+// the largest error of acosf over every f32 in [-1, 1] and of atanf over every f32 in [0, 1] against
+// the device's f64 acos / atan (rrt_testing_trig32_check, tests/test_gpu_trig32.py); kLibm64Err
+// covers fdlibm's f64 error (< 1 ulp, < 2^-51 for these angles) many times over. RRT_F64_TEXEL_FAST=0:
+// the fdlibm angles always. Without image data no angle is needed (texture.rs:91-93).
+#ifndef RRT_F64_TEXEL_FAST
+#define RRT_F64_TEXEL_FAST 1
+#endif
+constexpr double kAcos32Err = 0x1.0p-20;
+constexpr double kAtan32Err = 0x1.0p-21;
+constexpr double kLibm64Err = 0x1.0p-40;
+__device__ __forceinline__ float next_up32(float x) {
+    const uint32_t b = __float_as_uint(x);
+    if ((b & 0x7fffffffu) == 0u) return __uint_as_float(1u);  // +-0 -> the smallest subnormal
+    return __uint_as_float((b >> 31) ? b - 1u : b + 1u);
+}
+__device__ __forceinline__ float next_down32(float x) { return -next_up32(-x); }
+// acos(y) for y in [yd, yu] (the f32 neighbours around fl32(y)) lies in [acos(yu), acos(yd)]
+__device__ __forceinline__ bool acos_enclosure64(double y, double &lo, double &hi) {
+    const float y32 = (float)y;
+    const float yd = next_down32(y32), yu = next_up32(y32);
+    if (!(yd >= -1.0f && yu <= 1.0f)) return false;  // |y| at or beyond 1 in f32, or NaN
+    lo = (double)acosf(yu) - (kAcos32Err + kLibm64Err);
+    hi = (double)acosf(yd) + (kAcos32Err + kLibm64Err);
+    return true;
+}
+// atan2(yy, xx) from atanf of the f32 ratio t = min / max of |yy|, |xx| (<= 1): the inputs' and the
+// quotient's roundings move t by at most 3 2^-24 t <= 2^-22 and atan is 1-Lipschitz; the octant
+// arithmetic in f64 adds < 2^-50. Zero, tiny, huge or NaN components take fdlibm.
+__device__ __forceinline__ bool atan2_enclosure64(double yy, double xx, double &lo, double &hi) {
+    const double ay = __builtin_fabs(yy), ax = __builtin_fabs(xx);
+    const double mn = ay < ax ? ay : ax, mx = ay < ax ? ax : ay;
+    if (!(mn >= 0x1.0p-60 && mx <= 0x1.0p60)) return false;
+    const float t = (float)mn / (float)mx;
+    const double base = (double)atanf(t);
+    const double e = kAtan32Err + 0x1.0p-22 + 0x1.0p-50 + kLibm64Err;
+    double a = ay > ax ? 0.5 * kPiD - base : base;  // the angle in [0, pi/2]
+    if (xx < 0.0) a = kPiD - a;
+    if (yy < 0.0) a = -a;
+    lo = a - e;
+    hi = a + e;
+    return true;
+}
+__device__ __forceinline__ uint32_t texel_bytes64(const KParams &P, int tex, D3 outward) {
+    const GTexture t = P.texs[tex];
+    if (t.height <= 0) return 0x1000000u;  // texture.rs:91-93: (0, 1, 1)
+    int i, j;
+    if (RRT_DEBUG_F64_TEXEL_FIXED) {
+        i = texel_col64(2.0 + outward.x * 0x1.0p-60, t.width);
+        j = texel_row64(1.0 + outward.y * 0x1.0p-60, t.height);
+    } else {
+        double lo = 0.0, hi = 0.0;
+        bool ok = RRT_F64_TEXEL_FAST && atan2_enclosure64(-outward.z, outward.x, lo, hi);
+        if (ok) {
+            i = texel_col64(lo + kPiD, t.width);  // phi = fl(atan2 + pi) is monotone in atan2
+            ok = i == texel_col64(hi + kPiD, t.width);
+        }
+        if (!ok) i = texel_col64(rrt_atan2_64(-outward.z, outward.x) + kPiD, t.width);
+        ok = RRT_F64_TEXEL_FAST && acos_enclosure64(-outward.y, lo, hi);
+        if (ok) {
+            j = texel_row64(lo, t.height);
+            ok = j == texel_row64(hi, t.height);
+        }
+        if (!ok) j = texel_row64(rrt_acos64(-outward.y), t.height);
+    }
     const uint8_t *px = P.tex_pool + t.offset + ((size_t)j * t.width + i) * 3;
     return (uint32_t)px[0] | ((uint32_t)px[1] << 8) | ((uint32_t)px[2] << 16);
 }
@@ -1272,6 +1348,31 @@ __global__ __launch_bounds__(256) void rrt_accum64_to_f32(const D4 *__restrict__
 
 // LDS of the f64 kernel's block in each mode (stack, then the staged scene; the 1/r table when
 // p.inv_r_in_lds)
+// Test support (rrt_testing_trig32_check): the largest |acosf(x) - acos(x)| over every f32 x in
+// [-1, 1] and |atanf(t) - atan(t)| over every f32 t in [0, 1], against the device's f64 functions,
+// as f64 bit patterns (non-negative doubles order as their bits) in out[0], out[1].
+__global__ __launch_bounds__(256) void rrt_trig32_check(unsigned long long *out) {
+    double e_acos = 0.0, e_atan = 0.0;
+    for (uint64_t k = blockIdx.x * 256ull + threadIdx.x; k <= 0x3f800000ull; k += (uint64_t)gridDim.x * 256ull) {
+        const float x = __uint_as_float((uint32_t)k);  // every f32 in [0, 1]
+        const double dx = (double)x;
+        double d = __builtin_fabs((double)acosf(x) - acos(dx));
+        e_acos = d > e_acos ? d : e_acos;
+        d = __builtin_fabs((double)acosf(-x) - acos(-dx));
+        e_acos = d > e_acos ? d : e_acos;
+        d = __builtin_fabs((double)atanf(x) - atan(dx));
+        e_atan = d > e_atan ? d : e_atan;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        e_acos = fmax(e_acos, __shfl_xor(e_acos, off, 64));
+        e_atan = fmax(e_atan, __shfl_xor(e_atan, off, 64));
+    }
+    if ((threadIdx.x & 63u) == 0u) {
+        atomicMax(&out[0], (unsigned long long)__double_as_longlong(e_acos));
+        atomicMax(&out[1], (unsigned long long)__double_as_longlong(e_atan));
+    }
+}
+
 size_t lds64_bytes(const KParams &p, int mode, int blk = kBlock64) {
     size_t lds = ((size_t)p.stack_depth * blk * sizeof(uint16_t) + 15u) / 16u * 16u;
     lds += (size_t)RRT_F64_LDS_HIST * blk * sizeof(HRec);  // the history ring
@@ -1400,6 +1501,13 @@ void set_f64_layout(int layout) { g_f64_layout.store(layout < 0 ? -1 : layout & 
 // Passes of the sequential-sum schedule: the first holds the prefix chunk (chunk 0) and up to
 // pass_chunks tail chunks, each later one up to pass_chunks tail chunks; after a pass its tail samples
 // are folded into accum64 in order.
+hipError_t launch_trig32_check(unsigned long long *d_out, double *bounds, hipStream_t stream) {
+    bounds[0] = kAcos32Err;
+    bounds[1] = kAtan32Err;
+    hipLaunchKernelGGL(rrt_trig32_check, dim3(4096), dim3(256), 0, stream, d_out);
+    return hipGetLastError();
+}
+
 hipError_t launch_render_f64_seq(const KParams &p, bool count, hipStream_t stream) {
     const uint32_t n_tail = p.n_chunks > 0 ? p.n_chunks - 1u : 0u, m = std::max(1u, p.pass_chunks);
     const uint32_t n_pixels = p.tile_rows * p.width;

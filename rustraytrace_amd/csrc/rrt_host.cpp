@@ -1779,6 +1779,23 @@ extern "C" int32_t rrt_testing_recip_check(uint64_t *mismatches) {
     for (int i = 0; i < 3; ++i) mismatches[i] = h[i];
     return RRT_OK;
 }
+extern "C" int32_t rrt_testing_trig32_check(double *out) {
+    if (!out) return fail(RRT_E_INVALID, "null out");
+    unsigned long long *d = nullptr;
+    HIP_TRY(hipMalloc((void **)&d, 2 * sizeof(unsigned long long)), "hipMalloc");
+    hipError_t e = hipMemset(d, 0, 2 * sizeof(unsigned long long));
+    double bounds[2] = {0.0, 0.0};
+    if (e == hipSuccess) e = rrt::launch_trig32_check(d, bounds, nullptr);
+    unsigned long long h[2] = {0, 0};
+    if (e == hipSuccess) e = hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess) return fail(RRT_E_HIP, std::string("rrt_testing_trig32_check: ") + hipGetErrorString(e));
+    std::memcpy(&out[0], &h[0], sizeof(double));
+    std::memcpy(&out[1], &h[1], sizeof(double));
+    out[2] = bounds[0];
+    out[3] = bounds[1];
+    return RRT_OK;
+}
 static bool device_wrap() { return g_device_wrap.load(); }
 
 // One-shot frame on n_gpus devices: float accum rows (accum_out), f64 accum rows (accum64_out, the

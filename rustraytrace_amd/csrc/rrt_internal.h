@@ -306,6 +306,10 @@ hipError_t launch_quantize(const float *d_accum, uint8_t *d_rgb8, uint32_t n_pix
 // quotient (and sqrt_rn_big against the IEEE sqrt) over every f32 bit pattern; d_out: 3 zeroed u64
 // mismatch counters
 hipError_t launch_recip_check(unsigned long long *d_out, hipStream_t stream);
+// Test support (rrt_testing_trig32_check, rrt_books64.hip): the largest errors of the device's acosf
+// over [-1, 1] and atanf over [0, 1] against its f64 acos / atan (d_out: 2 zeroed u64 holding f64
+// bits), and the error bounds the f64 kernel's texel enclosures assume (bounds[2])
+hipError_t launch_trig32_check(unsigned long long *d_out, double *bounds, hipStream_t stream);
 // Implemented in rrt_books64.hip: one sample pass of the f64 books kernel (+ its chunk combine)
 // into p.accum64, and the f64 sums rounded to the f32 RGBA accum of the ABI.
 hipError_t launch_render_pass_f64(const KParams &p, bool count, hipStream_t stream);
