@@ -96,6 +96,17 @@ def test_f64_kernel_matches_books_path(cfg):
                                                                                               scene.height, qb)
 
 
+def test_f64_earth_texels_whole_frame():
+    """C4's whole frame at 640x360x64 (14.7 M paths, the earth from pole to pole): the texels the
+    kernel decides from f32 enclosures of the fdlibm angles, and those it falls back to fdlibm for,
+    are the books path's — every sum bit for bit (rrt_books64.hip texel_bytes64)."""
+    scene = rrt.config_scene("C4", image_width=640, samples_per_pixel=64)
+    gpu, _, gpu_rays = _gpu_f64(scene)
+    books, books_rays, _ = oracle.render(scene, oracle.BOOKS, threads=16)
+    assert gpu_rays == books_rays
+    _check(scene, gpu, books, "C4 640x360x64")
+
+
 def test_f64_one_shot_render_and_ppm():
     scene = rrt.config_scene("C2", image_width=48, samples_per_pixel=64)
     accum = rrt.render_f64(scene)
