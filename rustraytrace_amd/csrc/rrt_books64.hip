@@ -352,14 +352,16 @@ __device__ __forceinline__ int texel_row64(double theta, int h) {
 }
 
 // The texel decided from f32 angles where that is provably the books path's texel: an enclosure
-// [lo, hi] of rrt_acos64(-y) (of rrt_atan2_64(-z, x)) from the device's f32 acosf (atanf) with
-// bounded error; the row (column) at both ends of it is the row (column) at the f64 angle when the
-// two agree, by the monotonicity above. Else, and for arguments outside the enclosures' domains, the
-// f64 fdlibm angle itself (one lookup in a few thousand on C4). The error bounds are at least twice
-// the largest error of acosf over every f32 in [-1, 1] and of atanf over every f32 in [0, 1] against
-// the device's f64 acos / atan (rrt_testing_trig32_check, tests/test_gpu_trig32.py); kLibm64Err
-// covers fdlibm's f64 error (< 1 ulp, < 2^-51 for these angles) many times over. RRT_F64_TEXEL_FAST=0:
-// the fdlibm angles always. Without image data no angle is needed (texture.rs:91-93).
+// c +- e of rrt_acos64(-y) (of rrt_atan2_64(-z, x) + pi) from the device's f32 acosf (atanf) with
+// bounded error, and the texel coordinate s = u w (v' h) of the f64 pipeline at c. The f64 angle's s
+// lies within e w / (2 pi) (e h / pi) of it, plus the pipeline's own roundings (< 2^-30 here), so
+// when no integer and no image edge lies that close to s, the f64 angle truncates to the same index
+// (and no clamp applies). Else, and for arguments outside the enclosures' domains, the f64 fdlibm
+// angle itself (a few lookups in ten thousand on C4). The error bounds are at least twice the largest
+// error of acosf over every f32 in [-1, 1] and of atanf over every f32 in [0, 1] against the device's
+// f64 acos / atan (rrt_testing_trig32_check, tests/test_gpu_trig32.py); kLibm64Err covers fdlibm's
+// f64 error (< 1 ulp, < 2^-51 for these angles) many times over. RRT_F64_TEXEL_FAST=0: the fdlibm
+// angles always. Without image data no angle is needed (texture.rs:91-93).
 #ifndef RRT_F64_TEXEL_FAST
 #define RRT_F64_TEXEL_FAST 1
 #endif
@@ -372,53 +374,71 @@ __device__ __forceinline__ float next_up32(float x) {
     return __uint_as_float((b >> 31) ? b - 1u : b + 1u);
 }
 __device__ __forceinline__ float next_down32(float x) { return -next_up32(-x); }
-// acos(y) for y in [yd, yu] (the f32 neighbours around fl32(y)) lies in [acos(yu), acos(yd)]
-__device__ __forceinline__ bool acos_enclosure64(double y, double &lo, double &hi) {
+// acos(y) for y in [yd, yu] (the f32 neighbours around fl32(y)) lies in [acos(yu), acos(yd)] (acos is
+// decreasing); the f32 ends' sum and difference are exact in f64
+__device__ __forceinline__ bool acos_enclosure64(double y, double &c, double &e) {
     const float y32 = (float)y;
     const float yd = next_down32(y32), yu = next_up32(y32);
     if (!(yd >= -1.0f && yu <= 1.0f)) return false;  // |y| at or beyond 1 in f32, or NaN
-    lo = (double)acosf(yu) - (kAcos32Err + kLibm64Err);
-    hi = (double)acosf(yd) + (kAcos32Err + kLibm64Err);
+    const double lo = (double)acosf(yu), hi = (double)acosf(yd);
+    c = 0.5 * (lo + hi);
+    e = 0.5 * (hi - lo) + (kAcos32Err + kLibm64Err + 0x1.0p-49);
     return true;
 }
-// atan2(yy, xx) from atanf of the f32 ratio t = min / max of |yy|, |xx| (<= 1): the inputs' and the
-// quotient's roundings move t by at most 3 2^-24 t <= 2^-22 and atan is 1-Lipschitz; the octant
-// arithmetic in f64 adds < 2^-50. Zero, tiny, huge or NaN components take fdlibm.
-__device__ __forceinline__ bool atan2_enclosure64(double yy, double xx, double &lo, double &hi) {
+// atan2(yy, xx) + pi from atanf of the f32 ratio t = min / max of |yy|, |xx| (<= 1): the inputs' and
+// the quotient's roundings move t by at most 3 2^-24 t <= 2^-22 and atan is 1-Lipschitz; the octant
+// arithmetic, pi's rounding and the + pi in f64 add < 2^-48 (the f64 path's own + pi included).
+// Zero, tiny, huge or NaN components take fdlibm.
+__device__ __forceinline__ bool phi_enclosure64(double yy, double xx, double &c, double &e) {
     const double ay = __builtin_fabs(yy), ax = __builtin_fabs(xx);
     const double mn = ay < ax ? ay : ax, mx = ay < ax ? ax : ay;
     if (!(mn >= 0x1.0p-60 && mx <= 0x1.0p60)) return false;
     const float t = (float)mn / (float)mx;
     const double base = (double)atanf(t);
-    const double e = kAtan32Err + 0x1.0p-22 + 0x1.0p-50 + kLibm64Err;
     double a = ay > ax ? 0.5 * kPiD - base : base;  // the angle in [0, pi/2]
     if (xx < 0.0) a = kPiD - a;
     if (yy < 0.0) a = -a;
-    lo = a - e;
-    hi = a + e;
+    c = a + kPiD;
+    e = kAtan32Err + 0x1.0p-22 + kLibm64Err + 0x1.0p-48;
+    return true;
+}
+// The column / row at the centre when the whole enclosure truncates to it: s_c = fl(fl(c / k) n) for
+// the image size n <= 2^20 and k = 2 pi (pi with the flip 1 - v); 1 / (2 pi) < 0.16, 1 / pi < 0.32.
+__device__ __forceinline__ bool texel_col_decided(double c, double e, int w, int &i) {
+    if (w > (1 << 20)) return false;
+    const double s = div_by_const64(c, 2.0 * kPiD) * (double)w;
+    const double hw = e * (double)w * 0.16 + 0x1.0p-30;
+    const double lo = s - hw, hi = s + hw;
+    if (!(lo > 0.0 && hi < (double)w)) return false;  // an image edge within reach (or NaN)
+    const double f = __builtin_floor(lo);
+    if (!(hi < f + 1.0)) return false;  // a column edge within reach
+    i = (int)f;
+    return true;
+}
+__device__ __forceinline__ bool texel_row_decided(double c, double e, int h, int &j) {
+    if (h > (1 << 20)) return false;
+    const double s = (1.0 - div_by_const64(c, kPiD)) * (double)h;
+    const double hw = e * (double)h * 0.32 + 0x1.0p-30;
+    const double lo = s - hw, hi = s + hw;
+    if (!(lo > 0.0 && hi < (double)h)) return false;
+    const double f = __builtin_floor(lo);
+    if (!(hi < f + 1.0)) return false;
+    j = (int)f;
     return true;
 }
 __device__ __forceinline__ uint32_t texel_bytes64(const KParams &P, int tex, D3 outward) {
     const GTexture t = P.texs[tex];
     if (t.height <= 0) return 0x1000000u;  // texture.rs:91-93: (0, 1, 1)
-    int i, j;
+    int i = 0, j = 0;
     if (RRT_DEBUG_F64_TEXEL_FIXED) {
         i = texel_col64(2.0 + outward.x * 0x1.0p-60, t.width);
         j = texel_row64(1.0 + outward.y * 0x1.0p-60, t.height);
     } else {
-        double lo = 0.0, hi = 0.0;
-        bool ok = RRT_F64_TEXEL_FAST && atan2_enclosure64(-outward.z, outward.x, lo, hi);
-        if (ok) {
-            i = texel_col64(lo + kPiD, t.width);  // phi = fl(atan2 + pi) is monotone in atan2
-            ok = i == texel_col64(hi + kPiD, t.width);
-        }
-        if (!ok) i = texel_col64(rrt_atan2_64(-outward.z, outward.x) + kPiD, t.width);
-        ok = RRT_F64_TEXEL_FAST && acos_enclosure64(-outward.y, lo, hi);
-        if (ok) {
-            j = texel_row64(lo, t.height);
-            ok = j == texel_row64(hi, t.height);
-        }
-        if (!ok) j = texel_row64(rrt_acos64(-outward.y), t.height);
+        double c = 0.0, e = 0.0;
+        if (!(RRT_F64_TEXEL_FAST && phi_enclosure64(-outward.z, outward.x, c, e) && texel_col_decided(c, e, t.width, i)))
+            i = texel_col64(rrt_atan2_64(-outward.z, outward.x) + kPiD, t.width);
+        if (!(RRT_F64_TEXEL_FAST && acos_enclosure64(-outward.y, c, e) && texel_row_decided(c, e, t.height, j)))
+            j = texel_row64(rrt_acos64(-outward.y), t.height);
     }
     const uint8_t *px = P.tex_pool + t.offset + ((size_t)j * t.width + i) * 3;
     return (uint32_t)px[0] | ((uint32_t)px[1] << 8) | ((uint32_t)px[2] << 16);
