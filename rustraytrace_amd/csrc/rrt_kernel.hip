@@ -1045,8 +1045,11 @@ __device__ __forceinline__ bool shade(const KParams &P, const PR &prims, const G
         dir = add(nrm, r);
         if (__builtin_fabsf(dir.x) < 1e-8f && __builtin_fabsf(dir.y) < 1e-8f && __builtin_fabsf(dir.z) < 1e-8f) dir = nrm;
         if (kBook2 != kBook1Untextured && kind == 3) {  // ImageTexture at the sphere's (u, v) (sphere.rs:46-52)
-            const float theta = rrt_acosf(-outward.y);
-            const float phi = rrt_atan2f(-outward.z, outward.x) + kPi;
+#ifndef RRT_DEBUG_TEXEL_FIXED  // debug builds only: no acos / atan2 (prices them; wrong images)
+#define RRT_DEBUG_TEXEL_FIXED 0
+#endif
+            const float theta = RRT_DEBUG_TEXEL_FIXED ? 1.0f + outward.y * 0x1.0p-30f : rrt_acosf(-outward.y);
+            const float phi = RRT_DEBUG_TEXEL_FIXED ? 2.0f + outward.x * 0x1.0p-30f : rrt_atan2f(-outward.z, outward.x) + kPi;
             att = texel(P, m.b.z, div_by_const(phi, 2.0f * kPi), div_by_const(theta, kPi));
         } else if (kBook2 > 0 && kind == 5) {  // CheckerTexture at p
             att = checker_even(m.a.w, p) ? v3(m.a.x, m.a.y, m.a.z)
