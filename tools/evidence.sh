@@ -35,7 +35,7 @@ if [[ $STEPS == *stats* ]]; then
   run kstats_C2_f64 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG}_C2_f64 -o run --output-format csv -- python3 tools/prof_render.py --f64 --config C2 --spp 512 --iters 3 --json gpurun_out/kstats_C2_f64.json
   cp gpurun_out/prof_${TAG}_C2_f64/run_kernel_stats.csv gpurun_out/profiles/${TAG}_C2_f64_kernel_stats.csv
 fi
-for spec in ${CONFIGS:-C2:512 C4:1024 C5:256 NW9:64:1080 C2f64:512}; do
+for spec in ${CONFIGS:-C2:512 C4:1024 C5:256 NW9:64:1080 C2f64:512 C4f64:1024 C5f64:256}; do
   c=${spec%%:*}; rest=${spec#*:}; s=${rest%%:*}; w=1920; wa=""; fa=""; cfg=$c; tf=""
   [ "$rest" != "$s" ] && { w=${rest#*:}; wa="--width $w"; }
   [[ $c == *f64 ]] && { cfg=${c%f64}; fa="--f64"; c=${cfg}_f64; tf=f64; }
