@@ -1235,9 +1235,18 @@ __device__ __forceinline__ void render64_body(const KParams &P) {
                     const size_t npx = (size_t)Q.tile_rows * Q.width;
                     const uint32_t j = (uint32_t)__popc(tmask);
                     double *o = Q.seq64 + 3u * (((size_t)tcidx * Q.chunk_small + j) * npx + px);
-                    o[0] = Le.x;
-                    o[1] = Le.y;
-                    o[2] = Le.z;
+#ifndef RRT_F64_SEQ_NT
+#define RRT_F64_SEQ_NT 1
+#endif
+                    if (RRT_F64_SEQ_NT) {  // streamed (read once, by the fold after the pass): kept
+                        __builtin_nontemporal_store(Le.x, o);  // from evicting the history's lines in L2
+                        __builtin_nontemporal_store(Le.y, o + 1);
+                        __builtin_nontemporal_store(Le.z, o + 2);
+                    } else {
+                        o[0] = Le.x;
+                        o[1] = Le.y;
+                        o[2] = Le.z;
+                    }
                     tmask |= 1u << (s - Q.sample_begin - Q.seq_first - tcidx * Q.chunk_small);
                 }
             } else {
