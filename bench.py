@@ -74,7 +74,10 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-breakdown", action="store_true", help="skip the wall-clock split (one extra frame)")
     ap.add_argument("--no-extra", action="store_true", help="skip the 1-GPU C3 frame and the C1 timings")
-    ap.add_argument("--no-f64", action="store_true", help="skip the f64 books-arithmetic frame (f64_books)")
+    ap.add_argument("--no-f64", action="store_true", help="skip the f64 books-arithmetic leg (f64_books)")
+    ap.add_argument("--f64", action="store_true",
+                    help="time the f64 books kernel (RRT_FLAG_F64, bit-identical to the books path) as the headline "
+                         "leg instead of the f32 kernel: value, dtype f64, the same band split and gather")
     ap.add_argument("--ref-slot", action="store_true",
                     help="also time the reference's own GPU kernel on a bounded sample (reference_gpu_slot; opt-in: "
                          "a third-party kernel, kept out of the default run)")
@@ -336,6 +339,112 @@ def f64_books_frame(config, frames=2, issue_json=None):
             "roofline": roofline}
 
 
+def f64_band_leg(scene, config, band, rank, world, device, backend, dist, steps, warmup, base=True):
+    """N > 1: the f64 books kernel (RRT_FLAG_F64, bit-identical to the books path: the north star's
+    correctness bar) over the same row-band split as the f32 leg, timed the same way: `warmup` frames,
+    then a barrier + synchronize, `steps` frames each followed by the RCCL gather of the f64 tiles to
+    rank 0, synchronize + barrier, the max over ranks of the wall-clock. Every pixel is keyed by its
+    global index and summed in sample order inside its rank, so the gathered f64 frame equals the
+    1-GPU f64 frame bit for bit (tests/test_gpu_multirank.py). Rank 0 also renders the same frame
+    alone after the timed steps (the f64 curve's 1-GPU base) unless `base` is False. Returns the
+    record on rank 0, None elsewhere."""
+    import numpy as np
+    import torch
+
+    import rustraytrace_amd as rrt
+    from rustraytrace_amd.distributed import band_rows, gather_rows
+
+    W, H, S = scene.width, scene.height, scene.spp
+    ds = rrt.DeviceScene(scene, device=device, f64=True)
+    tile = ds.tile(band_rows=band, rank=rank, n_ranks=world, sample_begin=0, sample_end=S)
+    rows = ds.tile_rows(tile)
+    accum = torch.empty((max(rows, 1), W, 4), dtype=torch.float64, device=f"cuda:{device}")
+    stream = torch.cuda.current_stream()
+    k0 = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
+    k1 = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
+    g1 = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
+
+    def step(i=None):
+        if i is not None:
+            k0[i].record(stream)
+        if rows:
+            ds.render_tile_f64_async(tile, accum.data_ptr(), stream.cuda_stream)
+        if i is not None:
+            k1[i].record(stream)
+        src = accum[:rows] if backend == "nccl" else accum[:rows].cpu()
+        gather_rows(src, H, band, dist)
+        if i is not None:
+            g1[i].record(stream)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    ds.reset_counters()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(i)
+    torch.cuda.synchronize()
+    dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kms = float(np.mean([a.elapsed_time(b) for a, b in zip(k0, k1)]))
+    gms = float(np.mean([a.elapsed_time(b) for a, b in zip(k1, g1)]))
+    rays = ds.counters()["rays"]
+    ds.close()
+    del accum
+    red_dev = f"cuda:{device}" if backend == "nccl" else "cpu"
+    every = [torch.zeros(3, dtype=torch.float64, device=red_dev) for _ in range(world)]
+    dist.all_gather(every, torch.tensor([elapsed, kms, rays], dtype=torch.float64, device=red_dev))
+    every = torch.stack(every).cpu().numpy()
+    elapsed, rays = float(every[:, 0].max()), int(every[:, 2].sum())
+    per_rank = [round(float(v), 3) for v in every[:, 1]]
+    one = None
+    if rank == 0 and base:
+        one = one_gpu_frame_f64(scene, device)
+    dist.barrier()
+    if rank != 0:
+        return None
+    value = round(rays / elapsed / 1e6, 2)
+    rec = {"workload": f"{config} {W}x{H}x{S}spp, f64 books arithmetic (RRT_FLAG_F64), {band}-row bands dealt in "
+                       f"serpentine order over {world} ranks, RCCL gather of the f64 tiles to rank 0 inside the "
+                       "timed step" + (" (gloo rehearsal: ranks share a GPU, host copies)" if backend == "gloo" else ""),
+           "dtype": "f64", "value": value, "unit": "Mrays/s", "steps": steps, "warmup": warmup,
+           "ms_per_step": round(elapsed / steps * 1e3, 3), "rays_per_step": rays // steps,
+           "kernel_ms_per_rank": per_rank, "kernel_ms_max_over_ranks": max(per_rank),
+           "rank_imbalance": round(max(per_rank) / float(np.mean(per_rank)) - 1.0, 5),
+           "gather_ms": round(gms, 3), "rows_per_rank": [len(band_rows(H, band, r, world)) for r in range(world)],
+           "parity": "tests/test_gpu_multirank.py: the gathered f64 frame equals the 1-GPU f64 frame bit for bit; "
+                     "tests/test_gpu_books64.py: the 1-GPU f64 frame equals the books restatement bit for bit"}
+    if one is not None:
+        rec["one_gpu_base"] = one
+        rec["scaling_efficiency"] = round(value / (world * one["mrays_s"]), 4)
+    return rec
+
+
+def one_gpu_frame_f64(scene, device=0):
+    """The f64 band leg's 1-GPU base: the same frame through the f64 kernel on one GPU, one frame
+    (no warmup frame), wall-clock around it."""
+    import torch
+
+    import rustraytrace_amd as rrt
+
+    ds = rrt.DeviceScene(scene, device=device, f64=True)
+    tile = ds.tile(BAND_ROWS, 0, 1, 0, scene.spp)
+    buf = torch.empty((scene.height, scene.width, 4), dtype=torch.float64, device=f"cuda:{device}")
+    stream = torch.cuda.current_stream()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    ds.render_tile_f64_async(tile, buf.data_ptr(), stream.cuda_stream)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t
+    rays = ds.counters()["rays"]
+    ds.close()
+    del buf
+    return {"workload": f"{scene.name} {scene.width}x{scene.height}x{scene.spp}spp f64, 1 GPU, one frame (no warmup "
+                        "frame)", "frame_s": round(wall, 4), "rays": rays, "mrays_s": round(rays / wall / 1e6, 2)}
+
+
 def reference_gpu_slot(config, budget_s=1.5):
     """The reference's own GPU kernel on this GPU (oracle/_ref/ref_slot.hsaco: CUDA_SOURCE of
     src/cuda/mod.rs:15-335 compiled unmodified for gfx950, launched as imp::render launches it;
@@ -533,7 +642,8 @@ def main():
         kw["samples_per_pixel"] = args.spp
     scene = rrt.named_scene(config, **kw)
     W, H, S = scene.width, scene.height, scene.spp
-    ds = rrt.DeviceScene(scene, device=device)
+    f64 = args.f64
+    ds = rrt.DeviceScene(scene, device=device, f64=f64)
     # bands of equal count per rank when the height allows it (C3: 10 rows at 2/4/8 ranks)
     band = balanced_band(H, world) if (bands and world > 1) else BAND_ROWS
     if bands:
@@ -542,7 +652,8 @@ def main():
     else:
         tile = ds.tile(band_rows=BAND_ROWS, rank=0, n_ranks=1, sample_begin=rank * S, sample_end=(rank + 1) * S)
         rows = H
-    accum = torch.empty((max(rows, 1), W, 4), dtype=torch.float32, device=f"cuda:{device}")
+    accum = torch.empty((max(rows, 1), W, 4), dtype=torch.float64 if f64 else torch.float32, device=f"cuda:{device}")
+    render = ds.render_tile_f64_async if f64 else ds.render_tile_async
     stream = torch.cuda.current_stream()
     image = [None]  # rank 0: the gathered frame of the last step
 
@@ -557,7 +668,7 @@ def main():
         if i is not None:
             k_start[i].record(stream)
         if rows:
-            ds.render_tile_async(tile, accum.data_ptr(), stream.cuda_stream)
+            render(tile, accum.data_ptr(), stream.cuda_stream)
         if i is not None:
             k_end[i].record(stream)
         if world > 1:
@@ -601,8 +712,14 @@ def main():
         if rank == 0 and bands and not args.no_extra:
             # the strong-scaling base on this node: the same frame on rank 0's GPU alone, after the
             # timed region (the other ranks wait at the barrier below)
-            one_gpu = one_gpu_frame(config, kw, device)
+            one_gpu = one_gpu_frame_f64(scene, device) if f64 else one_gpu_frame(config, kw, device)
         dist.barrier()
+    f64_leg = None
+    if world > 1 and bands and not f64 and not args.no_f64 and config in ("C1", "C2", "C3", "C4", "C5"):
+        # the path that meets the north star's bar, over the same split (after the f32 leg's timed
+        # steps; its own barrier-bracketed timing and max over ranks)
+        f64_leg = f64_band_leg(scene, config, band, rank, world, device, backend, dist,
+                               steps=max(1, min(args.steps, 3)), warmup=1, base=not args.no_extra)
 
     if rank == 0:
         work = ds.count_work(tile)  # instrumented twin kernel: same paths, per-launch work counts
@@ -613,7 +730,7 @@ def main():
         traffic_json = args.traffic_json or os.path.join(ROOT, "profiles", f"traffic_{config}.json")
         traffic, traffic_src = (None, None)
         issue = None
-        if rows == H:  # the PMC records are of a whole-frame launch
+        if rows == H and not f64:  # the PMC records are of a whole-frame f32 launch
             traffic, traffic_src = load_traffic(traffic_json, config, W, S, rrt._lib.LIB_PATH)
             issue = load_issue(args.issue_json or os.path.join(ROOT, "profiles", f"issue_{config}.json"), config, W, S,
                                rrt._lib.LIB_PATH)
@@ -626,12 +743,15 @@ def main():
                      f"sum of the partial accums on rank 0" if world > 1 else "whole frame on 1 GPU, no gather")
         if world > 1 and backend == "gloo":
             split += " (gloo rehearsal: ranks share a GPU, host copies)"
+        if f64:
+            split += "; f64 books kernel (RRT_FLAG_F64), f64 tiles"
+        peak = PEAK_F64_VALU_TFLOPS if f64 else PEAK_F32_VALU_TFLOPS
         roofline = {
             "bound": "valu",
             "achieved": round(achieved, 3),
-            "peak": PEAK_F32_VALU_TFLOPS,
+            "peak": peak,
             "unit": "TFLOP/s",
-            "frac": round(achieved / PEAK_F32_VALU_TFLOPS, 4),
+            "frac": round(achieved / peak, 4),
             "traffic": traffic,
             "traffic_source": traffic_src,
             "hbm_GBps": round(traffic / avg_kernel_s / 1e9, 2) if traffic else None,
@@ -646,6 +766,10 @@ def main():
                     "(SURVEY 8d's 78.6 assumed 16-lane SIMDs). lds_l2_scene_read_GBps_algorithmic = "
                     "(16 B/sphere test + 56 B/node visit) / kernel time: scene reads served by LDS/L2, not HBM",
         }
+        if f64:
+            roofline["note"] = ("f64 VALU issue bound: the books path's 23 FLOP per sphere test + 12 FLOP per box test "
+                                "(SURVEY 8d), all f64 in the reference, over the average HIP-event time of the frame; "
+                                "peak = MI355X FP64 vector 78.6 TFLOP/s (half the FP32 rate)")
         if scene.quads is not None or scene.media is not None:
             roofline["note"] += (" Book-2 scene: the kernel's primitive-test count (spheres, quads, medium boundaries) "
                                  "is priced at the sphere test's 23 FLOP / 16 B.")
@@ -662,7 +786,7 @@ def main():
             "higher_is_better": True,
             "scaling": "strong" if bands else "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "f64" if f64 else "f32",
             "data": "synthetic",
             "config": {
                 "workload": f"{config + ' ' + SCENES[config] if config in SCENES else scene.name}, {W}x{H}x{S}spp, max_depth {scene.max_depth}, "
@@ -697,14 +821,16 @@ def main():
                 out["scaling_efficiency"] = round(out["value"] / (world * one_gpu["mrays_s"]), 4)
                 out["scaling_note"] = ("value / (n_gpus x the same frame on rank 0's GPU alone, measured in this run "
                                        "after the timed steps)")
-        if world == 1 and not args.no_breakdown:
+        if f64_leg is not None:
+            out["f64_books"] = f64_leg
+        if world == 1 and not args.no_breakdown and not f64:
             out["wall_clock_breakdown"] = wall_clock_breakdown(scene, accum, avg_kernel_s * 1e3)
         cpus = host_cpus()
-        if world == 1 and not args.no_extra:
+        if world == 1 and not args.no_extra and not f64:
             if config != "C3":
                 out["c3_one_gpu"] = one_gpu_frame("C3")
             out["c1"] = c1_timings(cpus)
-        if world == 1 and not args.no_f64 and config in ("C1", "C2", "C4", "C5"):
+        if world == 1 and not args.no_f64 and not f64 and config in ("C1", "C2", "C4", "C5"):
             out["f64_books"] = f64_books_frame(config)
         if world == 1 and args.ref_slot and config in ("C1", "C2", "C5"):
             out["reference_gpu_slot"] = reference_gpu_slot(config)

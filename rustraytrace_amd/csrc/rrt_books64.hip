@@ -456,18 +456,24 @@ __device__ __forceinline__ D3 texel_value64(uint32_t bytes) {
 // BOOKS returns attenuation * ray_color(scattered) [/ p] up its recursion, so a path's radiance is
 // L_k = (att_k (.) L_{k+1}) [* (1/p_k) for k >= 5] from the end of the path back to the camera ray:
 // each scatter's attenuation is kept in the lane's history (global memory, [bounce][lane slot], 12 B:
-// an attenuation is an f32 albedo, (1, 1, 1), or a texel's bytes — stored negated, the sign marks
-// them) and the product is formed back to front when a path ends with radiance (sky, background or
+// an attenuation is an f32 albedo, (1, 1, 1), or a texel's bytes — each byte b stored as the f32 bit
+// pattern kTexelTag + b, a signalling NaN no albedo can hold: the host canonicalises NaN albedos to
+// the quiet NaN, rrt_host.cpp canonical_albedo) and the product is formed back to front when a path ends with radiance (sky, background or
 // a light). The same roundings as the recursion, in the same order: the kernel's per-sample radiance
 // equals BOOKS' bit for bit. RRT_F64_B2F=0: the throughput carried front to back (a few ulps off).
 #ifndef RRT_F64_B2F
 #define RRT_F64_B2F 1
 #endif
+// the record's words are f32 bit patterns, kept as integers so that no move can quieten a tag
 struct Att32 {
-    float x, y, z;
+    uint32_t x, y, z;
 };
-__device__ __forceinline__ double att_decode(float f) {
-    return (__float_as_uint(f) >> 31) ? texel_channel64((uint32_t)(-f)) : (double)f;
+// texel byte b <-> the signalling-NaN bit pattern kTexelTag + b (payloads 1..256). Any albedo,
+// negative or -0 included, decodes as itself (round 5 tagged texels by the sign bit, which read a
+// negative albedo back as a texel byte).
+constexpr uint32_t kTexelTag = 0x7F800001u;
+__device__ __forceinline__ double att_decode(uint32_t f) {
+    return f - kTexelTag < 256u ? texel_channel64(f - kTexelTag) : (double)__uint_as_float(f);
 }
 // RRT_F64_REC4 = 1: a 4-B record instead — the primitive index (its material's albedo), kRecOne for a
 // dielectric's (1, 1, 1), or kRecTexel | the texel's bytes (kRecTexel | 0x1000000: the no-data
@@ -487,22 +493,22 @@ __device__ __forceinline__ HRec rec_albedo(int prim, const GMaterial &m) {
     return (uint32_t)prim;
 #else
     (void)prim;
-    return Att32{m.a.x, m.a.y, m.a.z};
+    return Att32{__float_as_uint(m.a.x), __float_as_uint(m.a.y), __float_as_uint(m.a.z)};
 #endif
 }
 __device__ __forceinline__ HRec rec_one() {
 #if RRT_F64_REC4
     return kRecOne;
 #else
-    return Att32{1.0f, 1.0f, 1.0f};
+    return Att32{0x3F800000u, 0x3F800000u, 0x3F800000u};
 #endif
 }
 __device__ __forceinline__ HRec rec_texel(uint32_t b) {
 #if RRT_F64_REC4
     return kRecTexel | b;
 #else
-    if (b == 0x1000000u) return Att32{0.0f, 1.0f, 1.0f};
-    return Att32{-(float)(b & 0xffu), -(float)((b >> 8) & 0xffu), -(float)(b >> 16)};
+    if (b == 0x1000000u) return Att32{0u, 0x3F800000u, 0x3F800000u};
+    return Att32{kTexelTag + (b & 0xffu), kTexelTag + ((b >> 8) & 0xffu), kTexelTag + (b >> 16)};
 #endif
 }
 // the attenuation a record stands for (kTex: the class has image textures)
@@ -515,7 +521,8 @@ __device__ __forceinline__ D3 rec_att(const HRec &r, const GMaterial *__restrict
     return f2d(a.x, a.y, a.z);
 #else
     (void)mtl;
-    return kTex ? d3(att_decode(r.x), att_decode(r.y), att_decode(r.z)) : f2d(r.x, r.y, r.z);
+    return kTex ? d3(att_decode(r.x), att_decode(r.y), att_decode(r.z))
+                : f2d(__uint_as_float(r.x), __uint_as_float(r.y), __uint_as_float(r.z));
 #endif
 }
 // camera.rs:191-195: max of the attenuation's components, clamped to [0.05, 0.95]

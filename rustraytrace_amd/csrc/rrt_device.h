@@ -32,8 +32,13 @@ struct RngState {
 };
 __device__ __forceinline__ uint32_t rotl32(uint32_t x, int k) { return (x << k) | (x >> (32 - k)); }
 // x ^ y ^ z in one gfx950 V_BITOP3_B32 (truth table 0x96)
+// (gfx950 only: on another --offload-arch the same value by two xors)
 __device__ __forceinline__ uint32_t xor3_32(uint32_t x, uint32_t y, uint32_t z) {
+#if defined(__gfx950__)
     return __builtin_amdgcn_bitop3_b32(x, y, z, 0x96);
+#else
+    return x ^ y ^ z;
+#endif
 }
 // xoshiro128+ (c ^= a; d ^= b; b ^= c; a ^= d; c ^= b << 9; d = rotl(d, 11); result a + d before
 // the step), its two chained xors per word folded into three-input xors: 7 VALU instructions per

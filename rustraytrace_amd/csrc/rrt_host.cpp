@@ -12,6 +12,7 @@
 #include "../../include/rrt_hip.h"
 
 #include <algorithm>
+#include <limits>
 #include <atomic>
 #include <chrono>
 #include <cmath>
@@ -638,6 +639,11 @@ void dielectric_consts(float eta, float &inv_eta, float &r0_front, float &r0_bac
 #ifndef RRT_PR_HOST
 #define RRT_PR_HOST 1
 #endif
+// An albedo as the f64 kernel's attenuation history may hold it: any NaN becomes the quiet NaN, so
+// no albedo carries the signalling-NaN patterns that tag texel bytes there (its value is NaN either
+// way: BOOKS propagates NaN whatever its payload).
+float canonical_albedo(float a) { return a == a ? a : std::numeric_limits<float>::quiet_NaN(); }
+
 float rr_inv_pr(float ax, float ay, float az) {
     float pr = ax;
     if (ay > pr) pr = ay;
@@ -964,6 +970,13 @@ int check_tile(const RrtScene *s, const RrtTile *t) {
     return RRT_OK;
 }
 
+// Free device memory (0 when the query fails): the f64 path sizes its buffers within it.
+size_t device_free_bytes(int device) {
+    size_t free_b = 0, total_b = 0;
+    if (hipSetDevice(device) != hipSuccess || hipMemGetInfo(&free_b, &total_b) != hipSuccess) return 0;
+    return free_b;
+}
+
 // Bytes of chunk partials one render may hold (RRT_PARTIAL_MB, default 2048 MiB): C2 (15 x
 // 33 MB) renders in one pass, a whole C3 frame on one GPU (39 x 133 MB) in three.
 size_t partial_budget() {
@@ -972,11 +985,13 @@ size_t partial_budget() {
     return mb << 20;
 }
 
-// The f64 path's tail-sample radiances (24 B per sample): 8 GiB unless RRT_PARTIAL_MB says
-// otherwise — C2's 64 tail samples of 2.07 M pixels (3.2 GB) in one pass of the 288-GB HBM.
-size_t seq_budget() {
+// The f64 path's tail-sample radiances (24 B per nonzero sample + a 4-B mask per tail unit and
+// pixel): 8 GiB, at most half the device's free memory, unless RRT_PARTIAL_MB says otherwise — C2's
+// 128 tail samples of 2.07 M pixels (6.4 GB) in one pass of the 288-GB HBM; a smaller device runs
+// more sample passes instead of failing its allocation.
+size_t seq_budget(int device) {
     if (std::getenv("RRT_PARTIAL_MB")) return partial_budget();
-    return (size_t)8192 << 20;
+    return std::min((size_t)8192 << 20, std::max(device_free_bytes(device) / 2, (size_t)64 << 20));
 }
 #ifndef RRT_F64_SEQ
 #define RRT_F64_SEQ 1
@@ -1063,7 +1078,7 @@ int fill_params(RrtScene *s, const RrtTile *t, float *d_accum, rrt::KParams &p) 
         const size_t n_px = std::max<size_t>((size_t)p.tile_rows * p.width, 1);
         const size_t per_chunk = n_px * p.chunk_small * 3u * sizeof(double) + n_px * sizeof(uint32_t);
         const uint32_t n_tail = p.n_chunks - 1u;
-        p.pass_chunks = (uint32_t)std::min<size_t>(n_tail, std::max<size_t>(1, seq_budget() / per_chunk));
+        p.pass_chunks = (uint32_t)std::min<size_t>(n_tail, std::max<size_t>(1, seq_budget(s->device) / per_chunk));
         const size_t need = (per_chunk * p.pass_chunks + sizeof(double) - 1) / sizeof(double);
         if (need > s->seq64_cap) {
             HIP_TRY(hipSetDevice(s->device), "hipSetDevice");
@@ -1103,9 +1118,21 @@ int fill_params(RrtScene *s, const RrtTile *t, float *d_accum, rrt::KParams &p) 
 #ifndef RRT_F64_HIST_LANES_PER_CU
 #define RRT_F64_HIST_LANES_PER_CU 1024  // 4 waves per SIMD x 4 SIMDs x 64 (the f64 kernel's bound)
 #endif
-        uint64_t lanes = (uint64_t)p.n_cus * RRT_F64_HIST_LANES_PER_CU;
-        lanes = std::min<uint64_t>(lanes, (4ull << 30) / per_lane / 512u * 512u);
+        // Every lane the persistent grid holds gets a slot. Within half the device's free memory
+        // (C2: 315 MB; depth 5000: 15.7 GB), so a deep max_depth costs memory, not occupancy; only
+        // beyond that is the grid cut to the lanes that fit, and the render says so on stderr.
+        const uint64_t full = (uint64_t)p.n_cus * RRT_F64_HIST_LANES_PER_CU;
+        uint64_t lanes = full;
+        if (lanes * per_lane > s->hist_cap) {
+            const uint64_t room = std::max<uint64_t>(device_free_bytes(s->device) + s->hist_cap, 1ull << 30) / 2u;
+            lanes = std::min<uint64_t>(lanes, room / per_lane / 512u * 512u);
+        } else {
+            lanes = std::min<uint64_t>(lanes, s->hist_cap / per_lane);
+        }
         if (lanes < 8u * 512u) return fail(RRT_E_INVALID, "RRT_FLAG_F64: max_depth too large for the attenuation history");
+        if (lanes < full)
+            std::fprintf(stderr, "rrt: RRT_FLAG_F64 max_depth %u: attenuation history for %llu of %llu lanes; the grid is reduced to fit\n",
+                         p.max_depth, (unsigned long long)lanes, (unsigned long long)full);
         const size_t need = (size_t)(lanes * per_lane);
         if (need > s->hist_cap) {
             HIP_TRY(hipSetDevice(s->device), "hipSetDevice");
@@ -1116,7 +1143,7 @@ int fill_params(RrtScene *s, const RrtTile *t, float *d_accum, rrt::KParams &p) 
             s->hist_cap = need;
         }
         p.hist = s->d_hist;
-        p.hist_lanes = (uint32_t)(s->hist_cap / per_lane);
+        p.hist_lanes = (uint32_t)std::min<uint64_t>(s->hist_cap / per_lane, 0xFFFFFFFFull);
     }
     return RRT_OK;
 }
@@ -1259,6 +1286,11 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
         int ref_bits;
         std::memcpy(&ref_bits, &m.ref_idx, 4);
         mats[i].a = make_float4(m.albedo_fuzz[0], m.albedo_fuzz[1], m.albedo_fuzz[2], fuzz);
+        if (f64) {  // canonical_albedo: the f64 history tags texel bytes as signalling NaNs (rrt_books64.hip kTexelTag)
+            mats[i].a.x = canonical_albedo(mats[i].a.x);
+            mats[i].a.y = canonical_albedo(mats[i].a.y);
+            mats[i].a.z = canonical_albedo(mats[i].a.z);
+        }
         mats[i].b = make_int4((int)m.kind, ref_bits, (int)m._pad[0], (int)m._pad[1]);
         if ((m.kind == RRT_MAT_LAMBERTIAN || m.kind == RRT_MAT_METAL) && RRT_PR_HOST) {
             const float inv_pr = rr_inv_pr(m.albedo_fuzz[0], m.albedo_fuzz[1], m.albedo_fuzz[2]);

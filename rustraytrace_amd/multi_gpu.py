@@ -12,6 +12,9 @@ owns (band b of period p = b // n goes to rank b % n for even p, n - 1 - b % n f
 1-GPU render: each pixel's samples are keyed by (seed, global pixel, sample) only. Rank 0 prints
 one JSON line: the slowest rank's kernel time, the gather time, Mrays/s over all ranks.
 
+`--f64` renders with the f64 books kernel (RRT_FLAG_F64) and gathers f64 tiles; the PPM then comes
+from the books path's own quantiser (color.rs), and the frame equals the 1-GPU f64 frame bit for bit.
+
 `--backend gloo` gathers host copies instead of device tensors (ranks may then share a GPU:
 device = local rank mod device count); it is the test path on a one-GPU box.
 """
@@ -36,6 +39,9 @@ def parse(argv=None):
     ap.add_argument("--out", default=None, help="PPM path on rank 0 ('-' = stdout, default: none)")
     ap.add_argument("--p6", action="store_true", help="binary P6 instead of the reference's P3")
     ap.add_argument("--save-accum", default=None, help="rank 0: save the float accum (.npy)")
+    ap.add_argument("--f64", action="store_true",
+                    help="the f64 books kernel (RRT_FLAG_F64): f64 tiles gathered, the PPM by the books path's own "
+                         "quantiser (color.rs), bit-identical to the 1-GPU f64 frame")
     return ap.parse_args(argv)
 
 
@@ -76,12 +82,14 @@ def main(argv=None) -> int:
     scene = rrt.config_scene(args.config, **over)
     W, H, S = scene.width, scene.height, scene.spp
 
-    ds = rrt.DeviceScene(scene, device=device)
+    ds = rrt.DeviceScene(scene, device=device, f64=args.f64)
     if args.band <= 0:
         args.band = balanced_band(H, world)
     tile = ds.tile(band_rows=args.band, rank=rank, n_ranks=world, sample_begin=0, sample_end=S)
     rows = ds.tile_rows(tile)
-    accum = torch.empty((max(rows, 1), W, 4), dtype=torch.float32, device=f"cuda:{device}")
+    accum = torch.empty((max(rows, 1), W, 4), dtype=torch.float64 if args.f64 else torch.float32,
+                        device=f"cuda:{device}")
+    render = ds.render_tile_f64_async if args.f64 else ds.render_tile_async
     stream = torch.cuda.current_stream()
     if use_dist:
         dist.barrier()
@@ -89,7 +97,7 @@ def main(argv=None) -> int:
     start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     start.record(stream)
     if rows:
-        ds.render_tile_async(tile, accum.data_ptr(), stream.cuda_stream)
+        render(tile, accum.data_ptr(), stream.cuda_stream)
     end.record(stream)
     torch.cuda.synchronize()
     kernel_ms = start.elapsed_time(end)
@@ -119,7 +127,10 @@ def main(argv=None) -> int:
         host = img.cpu().numpy()
         if args.save_accum:
             np.save(args.save_accum, host)
-        if args.out:
+        if args.out and args.f64:  # the books path's PPM (camera.rs:87-94 through color.rs:6-32)
+            rgb8 = rrt.quantize_accum_books_f64(W, H, host, S)
+            rrt.write_pnm_from_rgb8(W, H, rgb8, args.p6, args.out)
+        elif args.out:
             if args.p6:
                 rgb8 = rrt.quantize_accum(W, H, host, S)
                 rrt.write_pnm_from_rgb8(W, H, rgb8, True, args.out)
@@ -127,6 +138,7 @@ def main(argv=None) -> int:
                 rrt.write_ppm_from_accum(W, H, host, S, args.out)
         print(json.dumps({
             "config": args.config, "image": [W, H], "spp": S, "ranks": world, "backend": backend if use_dist else None,
+            "dtype": "f64" if args.f64 else "f32",
             "split": f"{args.band}-row bands dealt in serpentine order", "kernel_ms_max_over_ranks": round(kernel_ms, 3),
             "gather_ms": round(gather_ms, 3), "rays": rays, "mrays_per_s": round(rays / kernel_ms / 1e3, 2),
         }), file=sys.stderr if args.out == "-" else sys.stdout, flush=True)

@@ -36,6 +36,10 @@ def _worker(rank, world, port, mode, out_path):
             rows = band_rows(scene.height, 8, rank, world)
             local = torch.from_numpy(full[rows].astype(np.float32))
             img = gather_rows(local, scene.height, 8, dist)
+        elif mode == "rows64":  # the f64 books path's tiles (bench.py f64_band_leg, multi_gpu --f64)
+            rows = band_rows(scene.height, 8, rank, world)
+            local, _, _ = oracle.render(scene, oracle.BOOKS, rows=(0, scene.height))
+            img = gather_rows(torch.from_numpy(np.ascontiguousarray(local[rows])), scene.height, 8, dist)
         else:
             s0, s1 = sample_range(scene.spp, rank)
             part, _, _ = oracle.render(scene, oracle.TWIN, samples=(s0, s1))
@@ -48,7 +52,7 @@ def _worker(rank, world, port, mode, out_path):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["rows", "samples"])
+@pytest.mark.parametrize("mode", ["rows", "rows64", "samples"])
 def test_two_rank_gather(tmp_path, mode):
     from oracle import oracle
 
@@ -59,6 +63,9 @@ def test_two_rank_gather(tmp_path, mode):
     if mode == "rows":
         full, _, _ = oracle.render(scene, oracle.TWIN)
         assert np.array_equal(img, full.astype(np.float32))  # bit-identical to 1 rank
+    elif mode == "rows64":
+        full, _, _ = oracle.render(scene, oracle.BOOKS)
+        assert img.dtype == np.float64 and np.array_equal(img, full)  # f64 tiles, bit-identical to 1 rank
     else:
         parts = [oracle.render(scene, oracle.TWIN, samples=sample_range(scene.spp, r))[0].astype(np.float32)
                  for r in range(2)]

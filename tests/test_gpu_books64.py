@@ -129,6 +129,18 @@ def test_f64_full_size_rows_match_books(cfg, rows):
     assert np.isfinite(gpu).all()
 
 
+def test_f64_deep_max_depth_keeps_the_full_grid(capfd):
+    """max_depth 5000: 60 KB of attenuation history per lane slot, 15.7 GB for the full persistent grid
+    (a fixed 4-GiB history cap cut the grid silently). The history is sized within the
+    device's free memory, so the render keeps every lane and stays bit-identical to BOOKS."""
+    scene = rrt.config_scene("C1", image_width=64, samples_per_pixel=16, max_depth=5000)
+    gpu, _, gpu_rays = _gpu_f64(scene)
+    books, books_rays, _ = oracle.render(scene, oracle.BOOKS, threads=16)
+    assert gpu_rays == books_rays
+    _check(scene, gpu, books, "C1 depth 5000")
+    assert "grid is reduced" not in capfd.readouterr().err
+
+
 def test_f64_rejects_book2_scenes():
     sc = rrt.next_week_scene(1, dict(image_width=32, samples_per_pixel=4, max_depth=4))
     with pytest.raises(rrt.RrtError, match="RRT_FLAG_F64"):
@@ -170,6 +182,33 @@ def test_f64_full_class_matches_books_path():
     assert gpu_rays == books_rays, f"{gpu_rays} closest-hit queries vs BOOKS {books_rays}"
     _check(scene, gpu, books, "textured + specular")
     assert np.array_equal(gpu32, gpu.astype(np.float32))
+
+
+def _negative_albedo_scene(specular):
+    """An image-textured class (the only classes whose history records can hold texel bytes) with
+    Lambertian and metal albedos that are negative or -0 on some channels: BOOKS multiplies by them as
+    given (the round-5 history read a negative albedo back as a texel byte)."""
+    from rustraytrace_amd import scenes as S
+
+    sc = _textured_specular_scene(image_width=48, samples_per_pixel=64)
+    mats = sc.materials.copy()
+    mats[3]["albedo_fuzz"][:3] = (-0.35, 0.5, -0.0)  # the ground
+    if specular:
+        mats[1]["albedo_fuzz"][:3] = (0.7, -0.6, 0.5)  # the metal
+    else:  # no metal or dielectric: the diffuse class
+        mats[1] = S._material(0, (-0.2, 0.6, 0.4))[0]
+        mats[2] = S._material(0, (0.3, -0.0, -0.7))[0]
+    return S.SceneData(sc.camera, sc.spheres, mats, textures=sc.textures, name=f"negative_albedo_{specular}")
+
+
+@pytest.mark.parametrize("specular", [True, False])
+def test_f64_negative_albedo_matches_books_path(specular):
+    scene = _negative_albedo_scene(specular)
+    gpu, _, gpu_rays = _gpu_f64(scene)
+    books, books_rays, _ = oracle.render(scene, oracle.BOOKS, threads=16)
+    assert gpu_rays == books_rays
+    assert (books[..., :3] < 0).any(), "the scene must produce negative radiance sums"
+    _check(scene, gpu, books, f"negative albedo (specular={specular})")
 
 
 # rrt_testing_f64_layout: bit 0 widened Sphere64 records, bit 1 the 1/r table, bit 2 the f32

@@ -50,6 +50,59 @@ def test_row_bands_gathered_equal_one_gpu(tmp_path, ranks, backend, band):
         assert f.read() == rrt.format_ppm_from_accum(scene.width, scene.height, want, scene.spp)
 
 
+@pytest.mark.parametrize("ranks", [2, 3])
+def test_f64_row_bands_gathered_equal_one_gpu_f64(tmp_path, ranks):
+    """The f64 books kernel's tiles (RRT_FLAG_F64) over the row-band split, gathered as f64 over gloo
+    by ranks sharing the GPU: the frame equals the 1-GPU f64 frame bit for bit, and so its books-path
+    PPM (color.rs) byte for byte."""
+    out = str(tmp_path / "accum64.npy")
+    ppm = str(tmp_path / "img64.ppm")
+    args = ["--config", "C2", "--width", "96", "--spp", "16", "--depth", "20", "--backend", "gloo", "--f64",
+            "--save-accum", out, "--out", ppm]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ranks}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", "-m", "rustraytrace_amd.multi_gpu"] + args
+    env = dict(os.environ, PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""), OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, capture_output=True, text=True, cwd=ROOT, env=env, timeout=110)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["ranks"] == ranks and line["dtype"] == "f64"
+    scene = rrt.config_scene("C2", image_width=96, samples_per_pixel=16, max_depth=20)
+    want = rrt.render_f64(scene)
+    got = np.load(out)
+    assert got.dtype == np.float64 and got.shape == want.shape and np.array_equal(got, want)
+    rgb8 = rrt.quantize_accum_books_f64(scene.width, scene.height, want, scene.spp)
+    with open(ppm, "rb") as f:
+        assert f.read() == rrt.format_pnm_from_rgb8(scene.width, scene.height, rgb8)
+
+
+def test_bench_f64_band_leg():
+    """bench.py's N > 1 line carries the f64 books kernel over the same band split (f64_books: value,
+    per-rank kernel times, gather, 1-GPU base), 2 ranks sharing the GPU over gloo; and `--f64` makes
+    the f64 kernel the timed headline leg (dtype f64)."""
+    base = ["bench.py", "--gpus", "2", "--config", "C3", "--width", "256", "--spp", "8", "--steps", "2",
+            "--warmup", "1", "--no-cpu-baseline", "--no-breakdown"]
+    env = dict(os.environ, RRT_BENCH_BACKEND="gloo", OMP_NUM_THREADS="1")
+    scene = rrt.config_scene("C3", image_width=256, samples_per_pixel=8)
+    ds = rrt.DeviceScene(scene, f64=True)
+    want = ds.count_work(ds.tile(16, 0, 1, 0, 8))["rays"]
+    ds.close()
+    for extra in ([], ["--f64"]):
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+               "--master-addr", "127.0.0.1", f"--master-port={_free_port()}"] + base + extra
+        r = subprocess.run(cmd, capture_output=True, text=True, cwd=ROOT, env=env, timeout=110)
+        assert r.returncode == 0, r.stderr[-2000:]
+        line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+        if extra:
+            assert line["dtype"] == "f64" and line["rays_per_step"] == want and "f64_books" not in line
+            assert line["c3_one_gpu"]["rays"] == want and line["scaling_efficiency"] > 0
+        else:
+            assert line["dtype"] == "f32"
+            leg = line["f64_books"]
+            assert leg["dtype"] == "f64" and leg["rays_per_step"] == want and leg["rows_per_rank"] == [72, 72]
+            assert len(leg["kernel_ms_per_rank"]) == 2 and leg["gather_ms"] >= 0
+            assert leg["one_gpu_base"]["rays"] == want and leg["scaling_efficiency"] > 0
+
+
 @pytest.mark.parametrize("ranks", [1, 2])
 def test_bench_band_split_line(ranks):
     # bench.py's N-rank path (C3's row-band split, gather inside the timed step) at a small size:

@@ -41,7 +41,12 @@ for spec in ${CONFIGS:-C2:512 C4:1024 C5:256 NW9:64:1080 C2f64:512 C4f64:1024 C5
   [[ $c == *f64 ]] && { cfg=${c%f64}; fa="--f64"; c=${cfg}_f64; tf=f64; }
   if [[ $STEPS == *issue* ]]; then
     run pmc_issue_$c 240 rocprofv3 --pmc SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_WAVES GRBM_GUI_ACTIVE -d gpurun_out/ti_$c -o p --output-format csv -- python3 tools/prof_render.py --config $cfg $fa --spp $s $wa --iters 1 --json gpurun_out/ti_$c.json
-    run issue_$c 60 python3 tools/pmc_issue.py gpurun_out/ti_$c gpurun_out/ti_$c.json profiles/issue_$c.json
+    f64dir=""
+    if [ -n "$tf" ]; then  # the f64 kernel: its typed f64 instructions weigh 4 issue cycles (tools/pmc_issue.py)
+      run pmc_issue64_$c 240 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 GRBM_GUI_ACTIVE -d gpurun_out/ti64_$c -o p --output-format csv -- python3 tools/prof_render.py --config $cfg $fa --spp $s $wa --iters 1
+      f64dir=gpurun_out/ti64_$c
+    fi
+    run issue_$c 60 python3 tools/pmc_issue.py gpurun_out/ti_$c gpurun_out/ti_$c.json profiles/issue_$c.json $f64dir
     cp profiles/issue_$c.json gpurun_out/profiles/issue_$c.json
   fi
   if [[ $STEPS == *traffic* ]]; then

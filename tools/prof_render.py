@@ -37,7 +37,7 @@ def main():
         with open(a.json, "w") as f:
             json.dump({"config": a.config, "width": scene.width, "spp": scene.spp, "f64": a.f64, "iters": a.iters,
                        "rays_per_launch": ctr["rays"] // max(a.iters, 1),
-                       "paths_per_launch": ctr["paths"] // max(a.iters, 1)}, f)
+                       "paths_per_launch": ctr["paths"] // max(a.iters, 1), "counters": ctr}, f)
 
 
 if __name__ == "__main__":
