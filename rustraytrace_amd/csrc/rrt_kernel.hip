@@ -528,6 +528,64 @@ __device__ __forceinline__ void test_prims(const PR &prim_cr, int first, int cou
     }
 }
 
+// ---- lazy exact roots (book-1 scenes, the non-counting kernel) -------------------------------------
+// The closest hit is the lexicographic minimum of (exact root, test order) over the valid roots
+// (sphere.rs:24-51 against the running closest, strictly less: the first of equal roots wins), and
+// box tests only prune (conservative boxes, BoxSlack). So the leaf loop need not form every root
+// exactly: it brackets each root in an interval from the hardware square root and the per-ray
+// reciprocal and keeps the best candidate's interval [lo, closest]. A candidate whose interval lies
+// wholly below lo replaces the best, one wholly at or above `closest` is rejected (both decisions
+// are the exact ones), and only an overlap (nearly equal roots, or a root near tmin) is resolved on
+// the exact roots, as the exact loop forms them. The box tests prune with the upper bound `closest`,
+// so they visit a superset of the exact walk's nodes in the same order, whose extra primitives the
+// exact comparison would reject anyway. The exact root of the winner is formed once, when the query
+// ends (lazy_finish): every decision and every t equal the exact loop's, bit for bit (the GPU parity
+// suite with the whole C2 frame passed with it on). Measured and left off (round 6, same-box): C2
+// -0.1 %, C5 -0.8 %, C4 -4 % — VALU instructions per ray fell only 0.4 % (the winner's exact root at
+// the query's end and the interval bookkeeping cost about what the sparse root code did) and SALU
+// rose 4.5 % (profiles/r6_lazy_root_ab.log). RRT_LAZY_ROOT=1 turns it on.
+#ifndef RRT_LAZY_ROOT
+#define RRT_LAZY_ROOT 0
+#endif
+// The exact root the leaf loop forms (test_range's arithmetic): the near root if above tmin, else the far.
+template <bool kFastDiv, class PR>
+__device__ __forceinline__ float exact_root(const PR &prim_cr, int i, V3 o, V3 d, const RayK &rk) {
+    const float4 cr = prim_cr.at(i);
+    const V3 oc = v3(cr.x - o.x, cr.y - o.y, cr.z - o.z);
+    const float h = dot(d, oc);
+    const float c = dot(oc, oc) - (PR::kR2 ? cr.w : cr.w * cr.w);
+    const float disc = __builtin_fmaf(h, h, -(rk.a * c));
+    const float sq = sqrt_rn(disc);
+    float root = div_by_a<kFastDiv>(h - sq, rk);
+    if (!(0.001f < root)) root = div_by_a<kFastDiv>(h + sq, rk);
+    return root;
+}
+// An ambiguous candidate i (its interval overlaps the best's, or its root may lie at tmin): the exact
+// loop's decision on the exact roots. hit_prim < 0 or lo == closest: the best is exact already.
+template <bool kFastDiv, class PR>
+__device__ __forceinline__ void lazy_resolve(const PR &prim_cr, int i, V3 o, V3 d, const RayK &rk, float &lo,
+                                             float &closest, int &hit_prim) {
+    const float rc = exact_root<kFastDiv>(prim_cr, i, o, d, rk);
+    if (0.001f < rc && rc < closest) {  // else rc >= closest >= the best's root: rejected
+        const float rb = (hit_prim >= 0 && lo != closest) ? exact_root<kFastDiv>(prim_cr, hit_prim, o, d, rk) : closest;
+        if (rc < rb) {
+            hit_prim = i;
+            lo = closest = rc;
+        } else {
+            lo = closest = rb;
+        }
+    }
+}
+// The query's exact t: the winner's exact root when its interval is still open.
+template <class PR>
+__device__ __forceinline__ void lazy_finish(const PR &prim_cr, V3 o, V3 d, const RayK &rk, float &lo, float &closest,
+                                            int hit_prim) {
+    if (hit_prim >= 0 && lo != closest) {
+        closest = rk.ra != 0.0f ? exact_root<true>(prim_cr, hit_prim, o, d, rk) : exact_root<false>(prim_cr, hit_prim, o, d, rk);
+        lo = closest;
+    }
+}
+
 // Leaf primitives [first, first + count): the hit leaf children of one node visit, which are
 // adjacent in primitive order (sibling leaves split one range, rrt_host.cpp flatten2).
 // `skip` is the primitive the ray is leaving (exit_skip): it can never be accepted, so it is left
@@ -537,7 +595,10 @@ __device__ __forceinline__ void test_prims(const PR &prim_cr, int first, int cou
 // caller checked it wave-wide), so the root divisions take no branch.
 template <bool kCount, bool kFastDiv, class PR>
 __device__ __forceinline__ void test_range(const PR &prim_cr, int first, int count, V3 o, V3 d, const RayK &rk,
-                                           int skip, float &closest, int &hit_prim, Counters &cnt) {
+                                           int skip, float &closest, int &hit_prim, float &lo, Counters &cnt) {
+    // lazy roots: book-1 spheres in the non-counting kernel (the counting twin keeps the exact
+    // walk, so its test counts stay the oracle's), the per-ray reciprocal in range (kFastDiv)
+    constexpr bool kLazy = RRT_LAZY_ROOT && !kCount && kFastDiv && PR::kR2 && !PR::kHasQuads;
     const float a = rk.a;
     const bool trim = (uint32_t)(skip - first) < (uint32_t)count;
     const int n = count - (trim ? 1 : 0);
@@ -582,12 +643,45 @@ __device__ __forceinline__ void test_range(const PR &prim_cr, int first, int cou
         // when no lane takes it.
         if (disc < 0.0f) continue;
         if constexpr (RRT_PHASE_TIMING == 3) cnt.d2 += 1;
-        const float sq = sqrt_rn(disc);
-        float root = div_by_a<kFastDiv>(h - sq, rk);
-        if (!(0.001f < root)) root = div_by_a<kFastDiv>(h + sq, rk);
-        if (0.001f < root && root < closest) {
-            closest = root;
-            hit_prim = i;
+        if constexpr (kLazy) {
+            // Interval of the exact near root r0 = RN(RN(h - RN(sqrt disc)) / a): the hardware root s
+            // is within 2 ulp of sqrt(disc) (the exhaustive device check of sqrt_rn_big), so
+            // |RN(h - s) - RN(h - sq)| <= 2^-21 s + 2u |h - s| and, with ra within 2u of 1/a,
+            // |q - r0| <= 9u ra (|h - s| + s) <= 9u ra (|h| + 2s) (u = 2^-24); e = 2^-20 ra (|h| + 2s)
+            // bounds it with 1.7x to spare, which also covers the roundings of e and of q -+ e
+            // (e >= 16u |q|). Decided here: the near root surely above tmin, and surely below the
+            // best's interval (accept) or surely at or above it (reject). Anything else — a root near
+            // tmin, a ray inside the sphere (the far root), overlapping intervals, disc below 2^-96 (the
+            // square root's scaled range), an overflow or a NaN — is resolved on the exact roots.
+            const float sv = __builtin_amdgcn_sqrtf(disc);
+            const float q = (h - sv) * rk.ra;
+            const float e = __builtin_fmaf(sv, 2.0f, __builtin_fabsf(h)) * (rk.ra * 0x1.0p-20f);
+            const float l = q - e, u = q + e;
+            const bool valid = (disc >= 0x1.0p-96f) & (l > 0.001f);
+            const bool acc = valid & (u < lo);
+            const bool rej = valid & (l >= closest);
+            lo = acc ? l : lo;
+            closest = acc ? u : closest;
+            hit_prim = acc ? i : hit_prim;
+            if (!(acc | rej)) lazy_resolve<kFastDiv>(prim_cr, i, o, d, rk, lo, closest, hit_prim);
+        } else {
+            const float sq = sqrt_rn(disc);
+            float root = div_by_a<kFastDiv>(h - sq, rk);
+            if (!(0.001f < root)) root = div_by_a<kFastDiv>(h + sq, rk);
+            if (RRT_LAZY_ROOT && !kCount && PR::kR2 && !PR::kHasQuads) {
+                // exact root against a best that may be an interval (an earlier lazy batch)
+                if (0.001f < root && root < closest) {
+                    if (root < lo) {
+                        lo = closest = root;
+                        hit_prim = i;
+                    } else {
+                        lazy_resolve<kFastDiv>(prim_cr, i, o, d, rk, lo, closest, hit_prim);
+                    }
+                }
+            } else if (0.001f < root && root < closest) {
+                closest = root;
+                hit_prim = i;
+            }
         }
     }
 }
@@ -596,14 +690,16 @@ __device__ __forceinline__ void test_range(const PR &prim_cr, int first, int cou
 // Resumable BVH traversal: one call = one node. The state lives in registers (+ the LDS stack)
 // so a wave can leave the traversal loop while some lanes are still mid-tree.
 struct Trav {
-    float closest;
+    float closest;  // the best hit's root, or (lazy roots) an upper bound of it
     int hit_prim;
     int node;
     int sp;
+    float lo;       // lazy roots: a lower bound of the best hit's root (== closest when exact)
 };
 
 __device__ __forceinline__ void trav_begin(Trav &t) {
     t.closest = __builtin_inff();  // camera.rs:187 Interval(0.001, INFINITY)
+    t.lo = __builtin_inff();
     t.hit_prim = -1;
     t.node = 0;
     t.sp = 0;
@@ -700,10 +796,10 @@ __device__ __forceinline__ void trav_leaves(const PR &prims, Leaves lv, V3 o, V3
                                             Counters &cnt) {
     const int first = (int)(lv & kLinkFirstMask), count = (int)(lv >> kLinkCountShift);
     if (__ballot(rk.ra == 0.0f) == 0) {
-        test_range<kCount, true>(prims, first, count, o, d, rk, skip, t.closest, t.hit_prim, cnt);
+        test_range<kCount, true>(prims, first, count, o, d, rk, skip, t.closest, t.hit_prim, t.lo, cnt);
         return;
     }
-    test_range<kCount, false>(prims, first, count, o, d, rk, skip, t.closest, t.hit_prim, cnt);
+    test_range<kCount, false>(prims, first, count, o, d, rk, skip, t.closest, t.hit_prim, t.lo, cnt);
 }
 
 // BVH4 step: test the 4 child boxes, test leaf children's spheres in place, then descend
@@ -1565,6 +1661,8 @@ __device__ __forceinline__ void render_body(const KParams &P) {
         if (has && !need_ray && tr.node < 0) {
             need_ray = 1;
             const Prims<kBook2> spr{prims, motion, ps.time, P.quads, P.media, P.n_quads, rng_key(ps.rng) ^ ((uint64_t)ps.k << 32), perlin};
+            if constexpr (RRT_LAZY_ROOT && !kCount && Prims<kBook2>::kR2 && !kWide)
+                lazy_finish(spr, ps.o, ps.d, rk, tr.lo, tr.closest, tr.hit_prim);  // rk: the lane was in the tree this iteration
             if constexpr (Prims<kBook2>::kHasMedia) {
                 // The unbounded media (a fog around the whole scene; rrt_host.cpp unbounded_media):
                 // not in the tree, tested here against the closest hit of the walk, every lane whose
