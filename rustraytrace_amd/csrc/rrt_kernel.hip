@@ -303,6 +303,14 @@ __device__ __forceinline__ float clamped_slope(float s) {
     return __builtin_fabsf(s) < 0x1.0p-126f ? __builtin_copysignf(0x1.0p64f, s) : clamp_inv(recip_rn(s));
 }
 
+// kLdsNodes: ox, oy, oz are the byte offsets of the (entry, exit) plane pairs in an LDS GNode; for
+// the 32-B f16 nodes read from global memory (RRT_F16_ORDERED) ox packs the rotations that put each
+// axis's lo | hi << 16 word in (entry, exit) order — 16 when 1/d_a < 0, else 0 — at bits 0, 5 and 10
+// (v_alignbit reads the low 5 bits of its shift), so the traversal holds one register, not three.
+#ifndef RRT_F16_ORDERED
+#define RRT_F16_ORDERED 1
+#endif
+template <bool kLdsNodes = true>
 __device__ __forceinline__ RayK ray_consts(V3 o, V3 d) {
     RayK r;
     // aabb.rs:58 adinv, hoisted per ray, clamped to +-2^64: a zero component then gives a huge
@@ -310,9 +318,14 @@ __device__ __forceinline__ RayK ray_consts(V3 o, V3 d) {
     // is NaN or -inf, and a slab that straddles o (lo < 0 < hi about o's sign) rejects the ray.
     r.inv = v3(clamped_slope(d.x), clamped_slope(d.y), clamped_slope(d.z));
     r.oi = v3(o.x * r.inv.x, o.y * r.inv.y, o.z * r.inv.z);
-    r.ox = r.inv.x < 0.0f ? 4u : 0u;
-    r.oy = r.inv.y < 0.0f ? 16u : 12u;
-    r.oz = r.inv.z < 0.0f ? 28u : 24u;
+    if (kLdsNodes) {
+        r.ox = r.inv.x < 0.0f ? 4u : 0u;
+        r.oy = r.inv.y < 0.0f ? 16u : 12u;
+        r.oz = r.inv.z < 0.0f ? 28u : 24u;
+    } else {
+        r.ox = (r.inv.x < 0.0f ? 16u : 0u) | (r.inv.y < 0.0f ? 16u << 5 : 0u) | (r.inv.z < 0.0f ? 16u << 10 : 0u);
+        r.oy = r.oz = 0u;
+    }
     r.a = dot(d, d);                                  // sphere.rs:27, hoisted per ray
     // The reciprocal step of the IEEE f32 division expansion (v_rcp + one Newton step), done
     // once per ray instead of in every root division (div_by_a).
@@ -712,7 +725,7 @@ __device__ __forceinline__ void trav_begin(Trav &t) {
 // when nothing is left to visit. The next node depends only on these box results, so
 // testing the leaves later keeps every ray's sequence of operations unchanged. Returns
 // true when leaf tests are pending.
-template <bool kCount, typename Node, typename Stack>
+template <bool kCount, bool kOrd16, typename Node, typename Stack>
 __device__ __forceinline__ bool trav_node(const Node *__restrict__ nodes, Stack &stack, const RayK &rk, Trav &t,
                                           Leaves &lv, Counters &cnt) {
     if (kCount) { cnt.nodes++; cnt.boxes += 2; }
@@ -755,8 +768,22 @@ __device__ __forceinline__ bool trav_node(const Node *__restrict__ nodes, Stack 
             asm volatile("v_and_b32 %0, 0, %0" : "+v"(dep_zero));
         }
 #endif
-        h0 = box_hit(lo16(a.x), hi16(a.x), lo16(a.y), hi16(a.y), lo16(a.z), hi16(a.z), rk.inv, rk.oi, 0.001f, t.closest, tn0);
-        h1 = box_hit(lo16(a.w), hi16(a.w), lo16(b.x), hi16(b.x), lo16(b.y), hi16(b.y), rk.inv, rk.oi, 0.001f, t.closest, tn1);
+        if (kOrd16) {
+            // each axis's lo | hi << 16 word rotated by 16 bits when 1/d_a < 0 holds the (entry, exit)
+            // pair (the f64 kernel's rotation, rrt_books64.hip): the ordered slab, 6 v_alignbit instead
+            // of box_hit's 12 min/max; fma is monotone in the plane, so the same values and decisions
+            auto ord = [](uint32_t w, uint32_t r) { return __builtin_amdgcn_alignbit(w, w, r); };
+            const uint32_t ry = rk.ox >> 5, rz = rk.ox >> 10;
+            const uint32_t x0 = ord(a.x, rk.ox), y0 = ord(a.y, ry), z0 = ord(a.z, rz);
+            const uint32_t x1 = ord(a.w, rk.ox), y1 = ord(b.x, ry), z1 = ord(b.y, rz);
+            h0 = box_hit_ordered(lo16(x0), hi16(x0), lo16(y0), hi16(y0), lo16(z0), hi16(z0), rk.inv, rk.oi, 0.001f,
+                                 t.closest, tn0);
+            h1 = box_hit_ordered(lo16(x1), hi16(x1), lo16(y1), hi16(y1), lo16(z1), hi16(z1), rk.inv, rk.oi, 0.001f,
+                                 t.closest, tn1);
+        } else {
+            h0 = box_hit(lo16(a.x), hi16(a.x), lo16(a.y), hi16(a.y), lo16(a.z), hi16(a.z), rk.inv, rk.oi, 0.001f, t.closest, tn0);
+            h1 = box_hit(lo16(a.w), hi16(a.w), lo16(b.x), hi16(b.x), lo16(b.y), hi16(b.y), rk.inv, rk.oi, 0.001f, t.closest, tn1);
+        }
         l0 = b.z;
         l1 = b.w;
 #if RRT_DEBUG_EXTRA_NODE_LOAD == 2
@@ -1595,7 +1622,10 @@ __device__ __forceinline__ void render_body(const KParams &P) {
             tp = t;
         }
         RayK rk;
-        if (tr.node >= 0) rk = ray_consts(ps.o, ps.d);
+        // the ordered f16 slab for book-1 scenes read from global memory (C5): book-2 kernels keep the
+        // min/max slab (their 96-VGPR classes spill 20 VGPRs with the rotation register held)
+        constexpr bool kOrd16 = RRT_F16_ORDERED && !kLds && !kWide && kBook2 <= 0;
+        if (tr.node >= 0) rk = ray_consts<!kOrd16>(ps.o, ps.d);
         const Prims<kBook2> pr{prims, motion, ps.time, P.quads, P.media, P.n_quads, rng_key(ps.rng) ^ ((uint64_t)ps.k << 32), perlin};
         if constexpr (kWide) {
             for (;;) {
@@ -1633,7 +1663,7 @@ __device__ __forceinline__ void render_body(const KParams &P) {
                 }
                 if (tr.node >= 0 && lv == 0) {
                     Leaves l;
-                    if (trav_node<kCount>(nodes, stack, rk, tr, l, cnt)) lv = l;
+                    if (trav_node<kCount, kOrd16>(nodes, stack, rk, tr, l, cnt)) lv = l;
                 }
                 // wave-uniform decisions in scalar registers, without short-circuit branches:
                 // pm = lanes waiting on leaf tests, tm = lanes still in the tree (pm is a subset)
