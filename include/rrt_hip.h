@@ -579,6 +579,13 @@ int32_t rrt_testing_recip_check(uint64_t *mismatches);
  * out[3]; tests/test_gpu_trig32.py: each error at most half its bound). */
 int32_t rrt_testing_trig32_check(double *out);
 
+/* Test support, not part of the drop-in (ABI v11): the f64 kernel's IEEE square root without the
+ * library expansion's identity scalings (rrt_books64.hip sqrt64_big) against the library root, bit
+ * for bit, on 2^28 arguments from 2^-767 to the largest finite (random and nearly-square mantissas)
+ * plus +-0 and +inf: out[0] = differing results, out[1] = arguments checked
+ * (tests/test_gpu_trig32.py: 0 differ). */
+int32_t rrt_testing_sqrt64_check(uint64_t *out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -82,6 +82,7 @@ EXPORTED_SYMBOLS = (
     "rrt_testing_f64_layout",
     "rrt_testing_recip_check",
     "rrt_testing_trig32_check",
+    "rrt_testing_sqrt64_check",
 )
 
 
@@ -260,6 +261,7 @@ def load() -> ctypes.CDLL:
         "rrt_testing_f64_layout": (None, [c_int32]),
         "rrt_testing_recip_check": (c_int32, [P]),
         "rrt_testing_trig32_check": (c_int32, [P]),
+        "rrt_testing_sqrt64_check": (c_int32, [P]),
     }
     experiment = "RRT_LIB_PATH" in os.environ  # A/B of older builds: tolerate symbols they lack
     for name, (res, args) in sig.items():

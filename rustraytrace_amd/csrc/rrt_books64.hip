@@ -95,6 +95,37 @@ __device__ __forceinline__ double recip64(double x) {
     r = __builtin_fma(r, e, r);
     return __builtin_fma(__builtin_fma(-x, r, 1.0), r, r);
 }
+// sqrt(x), the IEEE root: LLVM's AMDGPU f64 expansion (v_rsq_f64, a Goldschmidt step, two remainder
+// corrections, a class check for +-0 and +inf) without its scaling of small arguments. The expansion
+// multiplies x by 2^256 when x < 2^-767 and the root by 2^-128 after; for every other x both
+// v_ldexp_f64 take exponent 0 and are identities, so this sequence is the same operations on the same
+// values (rrt_testing_sqrt64_check compares the two bit for bit on 2^28 arguments). sqrt64 takes it
+// when no active lane of the wave holds a nonzero x below 2^-767 (a wave-uniform branch, the f32
+// kernel's sqrt_rn); saves two v_ldexp_f64, a compare and two selects per root. Taken in the leaf
+// loop's root only (at the shading sites the second inlined sequence costs more registers than it
+// saves). RRT_F64_SQRT=0: the library sequence everywhere.
+#ifndef RRT_F64_SQRT
+#define RRT_F64_SQRT 1
+#endif
+__device__ __forceinline__ double sqrt64_big(double x) {
+    const double y = __builtin_amdgcn_rsq(x);
+    double g = x * y;
+    double h = y * 0.5;
+    const double r = __builtin_fma(-h, g, 0.5);
+    h = __builtin_fma(h, r, h);
+    g = __builtin_fma(g, r, g);
+    double d = __builtin_fma(-g, g, x);
+    g = __builtin_fma(d, h, g);
+    d = __builtin_fma(-g, g, x);
+    g = __builtin_fma(d, h, g);
+    return __builtin_amdgcn_class(x, 0x260) ? x : g;  // +-0, +inf: x itself
+}
+__device__ __forceinline__ bool sqrt64_small(double x) { return x < 0x1.0p-767 && x != 0.0; }
+__device__ __forceinline__ double sqrt64(double x) {
+    if (!RRT_F64_SQRT) return __builtin_sqrt(x);
+    if (__ballot(sqrt64_small(x)) == 0) return sqrt64_big(x);
+    return __builtin_sqrt(x);
+}
 // vec3.rs:168-170 unit_vector = v / |v|, Div<f64> = (1/rhs) * v (vec3.rs:142-148)
 __device__ __forceinline__ D3 unit_vector(D3 v) { return muls(v, recip64(__builtin_sqrt(dot(v, v)))); }
 __device__ __forceinline__ D3 f2d(float x, float y, float z) { return d3((double)x, (double)y, (double)z); }
@@ -619,7 +650,8 @@ __device__ __forceinline__ RayK64 ray_consts64(D3 o, D3 d) {
 }
 
 struct Trav64 {
-    double closest;
+    double closest;   // the best hit's root, or (lazy roots) an upper bound of it
+    double lo;        // lazy roots: a lower bound of the best hit's root (== closest when exact)
     float closest32;  // fl32(closest): the box test's exit bound (rrt_box32.h)
     int hit_prim;
     int node;
@@ -736,6 +768,53 @@ __device__ __forceinline__ double radius_sq_of(const Sphere64 &c) { return RRT_F
 #ifndef RRT_F64_S32_HOLD
 #define RRT_F64_S32_HOLD 0
 #endif
+// ---- lazy exact roots (rrt_kernel.hip's RRT_LAZY_ROOT, for the f64 roots) ----------------------------
+// Each root is bracketed from the f32 square root of fl32(disc) and the per-ray reciprocal: the best
+// candidate is kept as an interval [lo, closest], a candidate wholly below lo replaces it, one wholly at
+// or above closest is rejected (both the exact loop's decisions: strictly less, the first of equal
+// roots wins), and an overlap — or a root near tmin, a ray inside the sphere, disc outside
+// [2^-96, 2^126], a NaN — is decided on the exact roots. The winner's exact root is formed once, when
+// the query ends (lazy_finish64). The box tests prune with the upper bound, a superset of the exact
+// walk in the same order. So every decision and every t equal the exact loop's (tests/test_gpu_books64.py
+// green with it on). Measured and left off (round 6, same-box, profiles/r6_f64_sqrt_lazy_ab.log): C2
+// -8 %, C5 -5.5 %, C4 -10 % — the winner's exact root at each query's end, the held interval (a
+// double more: 4 VGPRs spilled at the 128-VGPR bound) and the bookkeeping cost more than the sparse
+// exact roots did. RRT_F64_LAZY=1 turns it on.
+#ifndef RRT_F64_LAZY
+#define RRT_F64_LAZY 0
+#endif
+// The exact root leaves64 forms for primitive i: the near root if above tmin, else the far.
+template <typename Rec>
+__device__ __forceinline__ double exact_root64(const Rec *__restrict__ prims, int i, D3 o, D3 d, double a, double ra) {
+    const Rec cr = prims[i];
+    const D3 oc = sub(center_of(cr), o);
+    const double h = dot(d, oc);
+    const double c = dot(oc, oc) - radius_sq_of(cr);
+    const double disc = h * h - a * c;
+    const double sq = sqrt64(disc);
+    double root = div_a64(h - sq, a, ra);
+    if (!(0.001 < root)) root = div_a64(h + sq, a, ra);
+    return root;
+}
+template <typename Rec>
+__device__ __forceinline__ void lazy_resolve64(const Rec *__restrict__ prims, int i, D3 o, D3 d, double a, double ra,
+                                               Trav64 &t) {
+    const double rc = exact_root64(prims, i, o, d, a, ra);
+    if (0.001 < rc && rc < t.closest) {  // else rc >= closest >= the best's root: rejected
+        const double rb = (t.hit_prim >= 0 && t.lo != t.closest) ? exact_root64(prims, t.hit_prim, o, d, a, ra) : t.closest;
+        if (rc < rb) t.hit_prim = i;
+        t.lo = t.closest = rc < rb ? rc : rb;
+        t.closest32 = (float)t.closest;
+    }
+}
+template <typename Rec>
+__device__ __forceinline__ void lazy_finish64(const Rec *__restrict__ prims, D3 o, D3 d, Trav64 &t) {
+    if (t.hit_prim >= 0 && t.lo != t.closest) {
+        const double a = dot(d, d);
+        t.lo = t.closest = exact_root64(prims, t.hit_prim, o, d, a, RRT_F64_DIVA ? recip_a64(a) : 0.0);
+    }
+}
+
 template <bool kCount, typename Rec>
 __device__ __forceinline__ void leaves64(const Rec *__restrict__ prims, const float4 *__restrict__ recs32, Leaves lv,
                                          D3 o, D3 d, double a, const RaySphere32 &r32, bool pre, Trav64 &t,
@@ -769,14 +848,35 @@ __device__ __forceinline__ void leaves64(const Rec *__restrict__ prims, const fl
         if (RRT_F64_STATS == 3) cnt.d0++;
         if (disc < 0.0) continue;
         if (RRT_F64_STATS == 2 || RRT_F64_STATS == 3 || RRT_F64_STATS == 5) cnt.d1++;
-        const double sq = __builtin_sqrt(disc);
-        double root = div_a64(h - sq, a, ra);
-        if (!(0.001 < root)) root = div_a64(h + sq, a, ra);
-        if (0.001 < root && root < t.closest) {
-            if (RRT_F64_STATS == 3) cnt.d2++;
-            t.closest = root;
-            t.closest32 = (float)root;
-            t.hit_prim = i;
+        if constexpr (RRT_F64_LAZY && !kCount && RRT_F64_DIVA) {
+            // |sv - sqrt(disc)| <= 2^-22.2 sqrt(disc): fl32(disc) moves the root by 2^-25 relative, and
+            // v_sqrt_f32 is within 1.5 ulp (the f32 kernel's exhaustive device check); so
+            // |q - r0| <= 2^-21.9 sv ra + 2^-50 (|h| + sv) ra, and e = 2^-20 (sv + |h|) ra bounds it
+            // with 3.7x to spare (the f64 roundings of e and of q -+ e are ~2^-52 relative)
+            const float df = (float)disc;
+            const double sv = (double)__builtin_amdgcn_sqrtf(df);
+            const double q = (h - sv) * ra;
+            const double e = (sv + __builtin_fabs(h)) * (ra * 0x1.0p-20);
+            const double l = q - e, u = q + e;
+            const bool valid = (df >= 0x1.0p-96f) & (df <= 0x1.0p126f) & (l > 0.001);
+            const bool acc = valid & (u < t.lo);
+            const bool rej = valid & (l >= t.closest);
+            t.lo = acc ? l : t.lo;
+            t.closest = acc ? u : t.closest;
+            t.closest32 = acc ? (float)u : t.closest32;
+            t.hit_prim = acc ? i : t.hit_prim;
+            if (!(acc | rej)) lazy_resolve64(prims, i, o, d, a, ra, t);
+        } else {
+            const double sq = sqrt64(disc);
+            double root = div_a64(h - sq, a, ra);
+            if (!(0.001 < root)) root = div_a64(h + sq, a, ra);
+            if (0.001 < root && root < t.closest) {
+                if (RRT_F64_STATS == 3) cnt.d2++;
+                t.closest = root;
+                t.lo = root;
+                t.closest32 = (float)root;
+                t.hit_prim = i;
+            }
         }
     }
 }
@@ -1151,6 +1251,7 @@ __device__ __forceinline__ void render64_body(const KParams &P) {
                 seg_done = 1;
             } else {
                 tr.closest = __builtin_inf();  // Interval(0.001, INFINITY)
+                tr.lo = __builtin_inf();
                 tr.closest32 = __builtin_inff();
                 tr.hit_prim = -1;
                 tr.node = 0;
@@ -1220,6 +1321,7 @@ __device__ __forceinline__ void render64_body(const KParams &P) {
         D3 Le = d3(0.0, 0.0, 0.0);
         if (has && !need_ray && tr.node < 0 && !pend) {
             need_ray = 1;
+            if constexpr (RRT_F64_LAZY && !kCount && RRT_F64_DIVA) lazy_finish64(prims, ps.o, ps.d, tr);
             seg_done = shade64<kClass>(P, prims, mtl, inv_r, ps, tr.closest, tr.hit_prim, Le, hist, pend, prec) ? 1u : 0u;
         }
         if (RRT_F64_DEFER && pend) {
@@ -1409,6 +1511,40 @@ __global__ __launch_bounds__(256) void rrt_trig32_check(unsigned long long *out)
     }
 }
 
+// Test support (rrt_testing_sqrt64_check): sqrt64_big against the library root, bit for bit, on
+// 2^28 arguments: every exponent from 2^-767 up to the largest finite, each with a random and a
+// nearly-square mantissa (k^2 and its neighbours, where the rounding is decided by the corrections),
+// plus +-0 and +inf. out[0] counts differing results, out[1] the arguments checked.
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__global__ __launch_bounds__(256) void rrt_sqrt64_check(unsigned long long *out) {
+    uint32_t bad = 0, n = 0;
+    for (uint64_t k = blockIdx.x * 256ull + threadIdx.x; k < (1ull << 28); k += (uint64_t)gridDim.x * 256ull) {
+        const uint64_t r = mix64(k);
+        const uint64_t e = 256u + (r >> 52) % (2046u - 256u);  // biased exponents of [2^-767, 2^1023)
+        uint64_t bits;
+        if (k & 1u) {
+            bits = (e << 52) | (r & 0xFFFFFFFFFFFFFull);
+        } else {  // a square of a 26-bit integer (exact), scaled, then moved by a few ulps
+            const double q = (double)(((r >> 8) & 0x3FFFFFFu) | 1u);
+            const double sq = q * q;
+            const uint64_t b = (uint64_t)__double_as_longlong(sq);
+            bits = ((b & 0xFFFFFFFFFFFFFull) | (((e & ~1ull) | 0x1ull) << 52)) + ((r >> 3) & 7u) - 3u;
+        }
+        if (k < 4) bits = k == 0 ? 0ull : k == 1 ? 0x8000000000000000ull : k == 2 ? 0x7FF0000000000000ull : 0x0010000000000000ull;
+        const double x = __longlong_as_double((long long)bits);
+        if (sqrt64_small(x)) continue;
+        ++n;
+        if (__double_as_longlong(sqrt64_big(x)) != __double_as_longlong(__builtin_sqrt(x))) ++bad;
+    }
+    atomicAdd(&out[0], (unsigned long long)bad);
+    atomicAdd(&out[1], (unsigned long long)n);
+}
+
 size_t lds64_bytes(const KParams &p, int mode, int blk = kBlock64) {
     size_t lds = ((size_t)p.stack_depth * blk * sizeof(uint16_t) + 15u) / 16u * 16u;
     lds += (size_t)RRT_F64_LDS_HIST * blk * sizeof(HRec);  // the history ring
@@ -1537,6 +1673,11 @@ void set_f64_layout(int layout) { g_f64_layout.store(layout < 0 ? -1 : layout & 
 // Passes of the sequential-sum schedule: the first holds the prefix chunk (chunk 0) and up to
 // pass_chunks tail chunks, each later one up to pass_chunks tail chunks; after a pass its tail samples
 // are folded into accum64 in order.
+hipError_t launch_sqrt64_check(unsigned long long *d_out, hipStream_t stream) {
+    hipLaunchKernelGGL(rrt_sqrt64_check, dim3(8192), dim3(256), 0, stream, d_out);
+    return hipGetLastError();
+}
+
 hipError_t launch_trig32_check(unsigned long long *d_out, double *bounds, hipStream_t stream) {
     bounds[0] = kAcos32Err;
     bounds[1] = kAtan32Err;

@@ -1811,6 +1811,20 @@ extern "C" int32_t rrt_testing_recip_check(uint64_t *mismatches) {
     for (int i = 0; i < 3; ++i) mismatches[i] = h[i];
     return RRT_OK;
 }
+extern "C" int32_t rrt_testing_sqrt64_check(uint64_t *out) {
+    if (!out) return fail(RRT_E_INVALID, "null out");
+    unsigned long long *d = nullptr;
+    HIP_TRY(hipMalloc((void **)&d, 2 * sizeof(unsigned long long)), "hipMalloc");
+    hipError_t e = hipMemset(d, 0, 2 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = rrt::launch_sqrt64_check(d, nullptr);
+    unsigned long long h[2] = {0, 0};
+    if (e == hipSuccess) e = hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess) return fail(RRT_E_HIP, std::string("rrt_testing_sqrt64_check: ") + hipGetErrorString(e));
+    out[0] = h[0];
+    out[1] = h[1];
+    return RRT_OK;
+}
 extern "C" int32_t rrt_testing_trig32_check(double *out) {
     if (!out) return fail(RRT_E_INVALID, "null out");
     unsigned long long *d = nullptr;

@@ -310,6 +310,7 @@ hipError_t launch_recip_check(unsigned long long *d_out, hipStream_t stream);
 // over [-1, 1] and atanf over [0, 1] against its f64 acos / atan (d_out: 2 zeroed u64 holding f64
 // bits), and the error bounds the f64 kernel's texel enclosures assume (bounds[2])
 hipError_t launch_trig32_check(unsigned long long *d_out, double *bounds, hipStream_t stream);
+hipError_t launch_sqrt64_check(unsigned long long *d_out, hipStream_t stream);
 // Implemented in rrt_books64.hip: one sample pass of the f64 books kernel (+ its chunk combine)
 // into p.accum64, and the f64 sums rounded to the f32 RGBA accum of the ABI.
 hipError_t launch_render_pass_f64(const KParams &p, bool count, hipStream_t stream);
