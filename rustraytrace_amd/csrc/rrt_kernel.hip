@@ -310,6 +310,17 @@ __device__ __forceinline__ float clamped_slope(float s) {
 #ifndef RRT_F16_ORDERED
 #define RRT_F16_ORDERED 1
 #endif
+// the ordered f16 slab for kernel classes up to this one (book 1 <= 0, book 2 1-3): book 1 and book-2
+// classes 1-2 (C5 +7.9 %, bouncing spheres +4.7 % same-box). The media class (3: final_scene) spills
+// 20 VGPRs at its 5-wave bound with the rotation register held (final_scene -0.4 %), and at 4 waves
+// loses 8.5 % (profiles/r6_f16_ordered_ab.log).
+#ifndef RRT_F16_ORDERED_MAX_CLASS
+#define RRT_F16_ORDERED_MAX_CLASS 2
+#endif
+// waves per SIMD of the book-2 media class (3) for scenes read from L2 (0: kBook2Waves)
+#ifndef RRT_B2_MEDIA_GLOBAL_WAVES
+#define RRT_B2_MEDIA_GLOBAL_WAVES 0
+#endif
 template <bool kLdsNodes = true>
 __device__ __forceinline__ RayK ray_consts(V3 o, V3 d) {
     RayK r;
@@ -773,7 +784,11 @@ __device__ __forceinline__ bool trav_node(const Node *__restrict__ nodes, Stack 
             // pair (the f64 kernel's rotation, rrt_books64.hip): the ordered slab, 6 v_alignbit instead
             // of box_hit's 12 min/max; fma is monotone in the plane, so the same values and decisions
             auto ord = [](uint32_t w, uint32_t r) { return __builtin_amdgcn_alignbit(w, w, r); };
-            const uint32_t ry = rk.ox >> 5, rz = rk.ox >> 10;
+            // the y and z rotations unpacked per node step (asm volatile: not hoisted out of the
+            // traversal loop, where they would hold two more registers)
+            uint32_t ry, rz;
+            asm volatile("v_lshrrev_b32 %0, 5, %1" : "=v"(ry) : "v"(rk.ox));
+            asm volatile("v_lshrrev_b32 %0, 10, %1" : "=v"(rz) : "v"(rk.ox));
             const uint32_t x0 = ord(a.x, rk.ox), y0 = ord(a.y, ry), z0 = ord(a.z, rz);
             const uint32_t x1 = ord(a.w, rk.ox), y1 = ord(b.x, ry), z1 = ord(b.y, rz);
             h0 = box_hit_ordered(lo16(x0), hi16(x0), lo16(y0), hi16(y0), lo16(z0), hi16(z0), rk.inv, rk.oi, 0.001f,
@@ -1622,9 +1637,9 @@ __device__ __forceinline__ void render_body(const KParams &P) {
             tp = t;
         }
         RayK rk;
-        // the ordered f16 slab for book-1 scenes read from global memory (C5): book-2 kernels keep the
-        // min/max slab (their 96-VGPR classes spill 20 VGPRs with the rotation register held)
-        constexpr bool kOrd16 = RRT_F16_ORDERED && !kLds && !kWide && kBook2 <= 0;
+        // the ordered f16 slab for scenes read from global memory (C5, bouncing spheres); the media
+        // class keeps the min/max slab (RRT_F16_ORDERED_MAX_CLASS)
+        constexpr bool kOrd16 = RRT_F16_ORDERED && !kLds && !kWide && kBook2 <= RRT_F16_ORDERED_MAX_CLASS;
         if (tr.node >= 0) rk = ray_consts<!kOrd16>(ps.o, ps.d);
         const Prims<kBook2> pr{prims, motion, ps.time, P.quads, P.media, P.n_quads, rng_key(ps.rng) ^ ((uint64_t)ps.k << 32), perlin};
         if constexpr (kWide) {
@@ -1890,9 +1905,11 @@ hipError_t launch_width(const KParams &p, bool count, hipStream_t stream) {
         // 1/4-spp scene table against 512 threads unbounded (~105 VGPRs, 4 waves): +2 ... +16 %
         // on every book-2 scene once the parameter spills were gone (256 x 4: +-1 %, 256 x 6:
         // -21 ... +9 %). Book 3 (class 4, the light-list pdfs) keeps the unbounded 512: -8 % at 5.
+        // Class 3 (media: final_scene, cornell_smoke) read from L2: RRT_B2_MEDIA_GLOBAL_WAVES.
+        constexpr int kGW = (kBook2 == 3 && RRT_B2_MEDIA_GLOBAL_WAVES > 0) ? RRT_B2_MEDIA_GLOBAL_WAVES : kBook2Waves;
         if constexpr (kBook2 != 4 && kBook2Waves > 1)
             return p.scene_in_lds ? launch_variant<true, uint16_t, kWide, kBook2, kBook2Waves, kBook2Block>(p, count, stream)
-                                  : launch_variant<false, uint16_t, kWide, kBook2, kBook2Waves, kBook2Block>(p, count, stream);
+                                  : launch_variant<false, uint16_t, kWide, kBook2, kGW, kBook2Block>(p, count, stream);
         return p.scene_in_lds ? launch_variant<true, uint16_t, kWide, kBook2>(p, count, stream)
                               : launch_variant<false, uint16_t, kWide, kBook2>(p, count, stream);
     } else {
