@@ -310,18 +310,28 @@ __device__ __forceinline__ float clamped_slope(float s) {
 #ifndef RRT_F16_ORDERED
 #define RRT_F16_ORDERED 1
 #endif
-// the ordered f16 slab for kernel classes up to this one (book 1 <= 0, book 2 1-3): book 1 and book-2
-// classes 1-2 (C5 +7.9 %, bouncing spheres +4.7 % same-box). The media class (3: final_scene) spills
-// 20 VGPRs at its 5-wave bound with the rotation register held (final_scene -0.4 %), and at 4 waves
-// loses 8.5 % (profiles/r6_f16_ordered_ab.log).
+// the ordered f16 slab for kernel classes up to this one (book 1 <= 0, book 2 1-3; all by default):
+// C5 +7.9 %, bouncing spheres +4.7 %, final_scene +3.0 % same-box (profiles/r6_f16_ordered_ab.log).
+// The media class (3: final_scene) forms ra per leaf batch to hold the rotation register within its
+// 96-VGPR bound (kHoldRa; with ra held it spilled 20 VGPRs and lost 0.4 %, at 4 waves 8.5 %).
 #ifndef RRT_F16_ORDERED_MAX_CLASS
-#define RRT_F16_ORDERED_MAX_CLASS 2
+#define RRT_F16_ORDERED_MAX_CLASS 3
 #endif
 // waves per SIMD of the book-2 media class (3) for scenes read from L2 (0: kBook2Waves)
 #ifndef RRT_B2_MEDIA_GLOBAL_WAVES
 #define RRT_B2_MEDIA_GLOBAL_WAVES 0
 #endif
-template <bool kLdsNodes = true>
+// The reciprocal step of the IEEE f32 division expansion (v_rcp + one Newton step) of a = |d|^2, done
+// once per ray (or per leaf batch) instead of in every root division (div_by_a); 0 outside
+// [2^-64, 2^64].
+__device__ __forceinline__ float refine_ra(float a) {
+    const float r0 = __builtin_amdgcn_rcpf(a);
+    const float e = __builtin_fmaf(-a, r0, 1.0f);
+    return (a >= 0x1.0p-64f && a <= 0x1.0p64f) ? __builtin_fmaf(e, r0, r0) : 0.0f;
+}
+// kHoldRa = false: ra is formed per leaf batch (trav_leaves) from a, so the node steps hold one
+// register less (the media class with the ordered f16 slab, which spills at its 96-VGPR bound).
+template <bool kLdsNodes = true, bool kHoldRa = true>
 __device__ __forceinline__ RayK ray_consts(V3 o, V3 d) {
     RayK r;
     // aabb.rs:58 adinv, hoisted per ray, clamped to +-2^64: a zero component then gives a huge
@@ -338,11 +348,7 @@ __device__ __forceinline__ RayK ray_consts(V3 o, V3 d) {
         r.oy = r.oz = 0u;
     }
     r.a = dot(d, d);                                  // sphere.rs:27, hoisted per ray
-    // The reciprocal step of the IEEE f32 division expansion (v_rcp + one Newton step), done
-    // once per ray instead of in every root division (div_by_a).
-    const float r0 = __builtin_amdgcn_rcpf(r.a);
-    const float e = __builtin_fmaf(-r.a, r0, 1.0f);
-    r.ra = (r.a >= 0x1.0p-64f && r.a <= 0x1.0p64f) ? __builtin_fmaf(e, r0, r0) : 0.0f;
+    r.ra = kHoldRa ? refine_ra(r.a) : 0.0f;
     return r;
 }
 
@@ -833,9 +839,11 @@ __device__ __forceinline__ bool trav_node(const Node *__restrict__ nodes, Stack 
 }
 
 // The postponed leaf tests of one node visit (leaf 0's primitives, then leaf 1's).
-template <bool kCount, class PR>
-__device__ __forceinline__ void trav_leaves(const PR &prims, Leaves lv, V3 o, V3 d, const RayK &rk, int skip, Trav &t,
+template <bool kCount, bool kHoldRa, class PR>
+__device__ __forceinline__ void trav_leaves(const PR &prims, Leaves lv, V3 o, V3 d, const RayK &rk_, int skip, Trav &t,
                                             Counters &cnt) {
+    RayK rk = rk_;
+    if (!kHoldRa) rk.ra = refine_ra(rk.a);
     const int first = (int)(lv & kLinkFirstMask), count = (int)(lv >> kLinkCountShift);
     if (__ballot(rk.ra == 0.0f) == 0) {
         test_range<kCount, true>(prims, first, count, o, d, rk, skip, t.closest, t.hit_prim, t.lo, cnt);
@@ -1640,7 +1648,8 @@ __device__ __forceinline__ void render_body(const KParams &P) {
         // the ordered f16 slab for scenes read from global memory (C5, bouncing spheres); the media
         // class keeps the min/max slab (RRT_F16_ORDERED_MAX_CLASS)
         constexpr bool kOrd16 = RRT_F16_ORDERED && !kLds && !kWide && kBook2 <= RRT_F16_ORDERED_MAX_CLASS;
-        if (tr.node >= 0) rk = ray_consts<!kOrd16>(ps.o, ps.d);
+        constexpr bool kHoldRa = !(kOrd16 && kBook2 == 3);
+        if (tr.node >= 0) rk = ray_consts<!kOrd16, kHoldRa>(ps.o, ps.d);
         const Prims<kBook2> pr{prims, motion, ps.time, P.quads, P.media, P.n_quads, rng_key(ps.rng) ^ ((uint64_t)ps.k << 32), perlin};
         if constexpr (kWide) {
             for (;;) {
@@ -1689,7 +1698,7 @@ __device__ __forceinline__ void render_body(const KParams &P) {
                 if ((pm != 0) & batch) {
                     __builtin_amdgcn_s_setprio(RRT_PRIO_LEAF);
                     if (lv != 0) {
-                        trav_leaves<kCount>(pr, lv, ps.o, ps.d, rk, ps.skip, tr, cnt);
+                        trav_leaves<kCount, kHoldRa>(pr, lv, ps.o, ps.d, rk, ps.skip, tr, cnt);
                         lv = 0;
                     }
                     __builtin_amdgcn_s_setprio(RRT_PRIO_NODE);
@@ -1714,6 +1723,7 @@ __device__ __forceinline__ void render_body(const KParams &P) {
                 // query ended this iteration together. The same hit as testing them in the tree: the
                 // free flight is clipped to the closest hit so far and the draw is fixed per
                 // (path, segment, medium). rk is this iteration's: the lane was in the tree.
+                if (!kHoldRa) rk.ra = refine_ra(rk.a);
                 for (uint32_t u = P.n_prims - P.n_unbounded; u < P.n_prims; ++u) {
                     if (kCount) cnt.spheres++;
                     const int m = (int)(-prims[u].w) - 1 - (int)P.n_quads;
