@@ -325,11 +325,15 @@ def f64_books_frame(config, frames=2, issue_json=None):
 
         with open(rrt._lib.LIB_PATH, "rb") as f:
             same = hashlib.sha256(f.read()).hexdigest() == rec.get("lib_sha256")
-        roofline.update({k: rec[k] for k in ("valu_busy", "lanes_per_valu", "valu_insts_per_ray") if k in rec})
+        roofline.update({k: rec[k] for k in ("valu_busy", "lanes_per_valu", "valu_insts_per_ray", "f64_share_of_valu")
+                         if rec.get(k) is not None})
+        weighted = rec.get("f64_share_of_valu") is not None
         roofline["issue_source"] = (f"{os.path.relpath(path, ROOT)}: rocprofv3 --pmc over one f64 {config} launch, "
                                     f"{'this' if same else 'an earlier'} librrt_hip.so build "
-                                    f"({rec.get('lib_sha256', '')[:12]}); valu_busy counts 2 cycles per VALU "
-                                    f"wave-instruction (an f64 FMA takes 4)")
+                                    f"({rec.get('lib_sha256', '')[:12]}); valu_busy = issue cycles / SIMD cycles, "
+                                    + ("an f64 VALU instruction weighted 4 cycles and any other 2 (typed counters "
+                                       "from a second pass)" if weighted else
+                                       "2 cycles per VALU wave-instruction (an f64 one takes 4: an underestimate)"))
     return {"workload": f"{config} {scene.width}x{scene.height}x{scene.spp}spp, f64 books arithmetic (RRT_FLAG_F64)",
             "dtype": "f64", "value": round(rays / wall / 1e6, 2), "unit": "Mrays/s", "ms_per_frame": round(wall * 1e3, 3),
             "kernel_ms": round(ms, 3), "rays_per_frame": rays, "frames": frames,

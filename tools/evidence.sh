@@ -3,11 +3,11 @@
 # default with its f64 leg; C4, C5, NW9), rocprofv3 kernel stats of each bench command (the
 # rocprof average must agree with the line's kernel_ms_avg) and of the f64 C2 frame, the issue-side
 # PMC pass and the HBM traffic passes per config (f32 and the f64 C2 launch). Stops at the first
-# failing step. TAG names the outputs (gpurun_out/profiles/<TAG>_*); STEPS=suite,bench,stats,issue,traffic
+# failing step. TAG names the outputs (gpurun_out/profiles/<TAG>_*); STEPS=suite,bench,multi,stats,issue,traffic
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 TAG=${TAG:-r5}
-STEPS=${STEPS:-suite,bench,stats,issue,traffic}
+STEPS=${STEPS:-suite,bench,multi,stats,issue,traffic}
 mkdir -p gpurun_out/profiles
 run() { local name=$1 limit=$2; shift 2
   timeout -k 10 "$limit" "$@" > "gpurun_out/$name.log" 2>&1; local rc=$?
@@ -25,6 +25,12 @@ if [[ $STEPS == *bench* ]]; then
     run bench_$c 300 python3 bench.py --config $c --no-extra --no-cpu-baseline --no-breakdown
     tail -n 1 gpurun_out/bench_$c.log > gpurun_out/profiles/${TAG}_bench_$c.json
   done
+fi
+if [[ $STEPS == *multi* ]]; then  # full-size rehearsals of the N > 1 legs on one GPU
+  run bench_C3_f64 600 python3 bench.py --config C3 --f64 --steps 2 --warmup 1 --no-cpu-baseline --no-breakdown
+  tail -n 1 gpurun_out/bench_C3_f64.log > gpurun_out/profiles/${TAG}_bench_C3_f64.json
+  run bench_gpus2_gloo 900 env RRT_BENCH_BACKEND=gloo python3 bench.py --gpus 2 --steps 2 --warmup 1 --no-cpu-baseline
+  tail -n 1 gpurun_out/bench_gpus2_gloo.log > gpurun_out/profiles/${TAG}_bench_gpus2_gloo_rehearsal.json
 fi
 if [[ $STEPS == *stats* ]]; then
   for c in C2 C4 C5; do
