@@ -28,7 +28,9 @@ COUNTERS = ("SQ_INSTS_VALU", "SQ_THREAD_CYCLES_VALU", "SQ_INSTS_SALU", "SQ_INSTS
 
 
 def per_dispatch(d, kernel="rrt_render"):
-    """Per-dispatch averages of every counter over the dispatches of kernels named `kernel`."""
+    """Every counter summed over the dispatches of kernels named `kernel` in one render call
+    (tools/prof_render.py --iters 1: a frame the f64 kernel renders in several sample passes counts
+    all of them; round 5 averaged per dispatch, which divided C4's f64 instructions per ray by 4)."""
     vals = {}
     for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(path)):
@@ -39,7 +41,7 @@ def per_dispatch(d, kernel="rrt_render"):
             vals[r["Counter_Name"]][key] += float(r["Counter_Value"])
     if not vals:
         raise SystemExit(f"no {kernel} rows in {d}")
-    return {k: sum(v.values()) / len(v) for k, v in vals.items()}, max(len(v) for v in vals.values())
+    return {k: sum(v.values()) for k, v in vals.items()}, max(len(v) for v in vals.values())
 
 
 F64 = ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64")

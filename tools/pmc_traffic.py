@@ -21,8 +21,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def counter(d, name, kernel="rrt_render"):
-    """Average per dispatch of `name` over the dispatches whose kernel name contains `kernel`
-    (rocprofv3 writes one row per dispatch and counter; values summed over the row's dimensions)."""
+    """Sum of `name` over the dispatches whose kernel name contains `kernel` in one render call
+    (tools/prof_render.py --iters 1; rocprofv3 writes one row per dispatch and counter, values summed
+    over the row's dimensions): a frame the f64 kernel renders in several sample passes (C4's 1024
+    samples: 4 dispatches) counts all of them. Round 5 averaged per dispatch, which reported a quarter
+    of C4's f64 frame."""
     per = {}
     for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(path)):
@@ -34,7 +37,7 @@ def counter(d, name, kernel="rrt_render"):
         if kernel != "rrt_render":
             return 0.0, 0
         raise SystemExit(f"no {name} rows in {d}")
-    return sum(vals) / len(vals), len(vals)
+    return sum(vals), len(vals)
 
 
 def main(fetch_dir, write_dir, config, width, spp, out, f64=""):
@@ -59,7 +62,8 @@ def main(fetch_dir, write_dir, config, width, spp, out, f64=""):
         "combine_fetch_size_kib": cf_kib,
         "combine_write_size_kib": cw_kib,
         "lib_sha256": hashlib.sha256(open(so, "rb").read()).hexdigest(),
-        "note": "separate --pmc passes FETCH_SIZE / WRITE_SIZE on tools/prof_render.py (1 launch)",
+        "note": "separate --pmc passes FETCH_SIZE / WRITE_SIZE on tools/prof_render.py --iters 1 (one render call: "
+                "the sum over its render dispatches)",
     }
     with open(out, "w") as f:
         json.dump(rec, f, indent=1)
