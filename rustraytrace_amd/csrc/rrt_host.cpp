@@ -1536,7 +1536,7 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
     {  // Perlin tables in LDS when the block's LDS (stack + staged scene + tables) stays within 64 KB
         // the block that launches (book-2 classes 1-3: 256 threads; book 3: 512), as launch_variant sizes it
         const bool wide = fb.n_nodes > 65535u;
-        const size_t threads = (size_t)rrt::render_block_threads(book2 && !book3, wide);
+        const size_t threads = (size_t)rrt::render_block_threads(book2 && !book3, wide, book3);
         const size_t stack = ((size_t)p.stack_depth * threads * (wide ? 4u : 2u) + 15u) / 16u * 16u;
         const size_t scene = p.scene_in_lds ? fb.bytes.size() + (size_t)n_prims * (rrt::kPrimBytes + (book2 ? rrt::kMotionBytes : 0)) : 0;
         p.perlin_in_lds = book2 && n_perlin > 0 &&

@@ -281,13 +281,21 @@ constexpr int kGlobalWaves = 7;           // and waves per SIMD (72 VGPRs)
 #ifndef RRT_B2_BLOCK
 #define RRT_B2_BLOCK 256
 #endif
+// Book 3 at 256 x 5 (its noise-free kernel needs ~112 VGPRs): B3 +4.8 % same-box over the
+// unbounded 512-thread blocks (4 waves), +3.9 % over 256 x 4.
+#ifndef RRT_B3_WAVES
+#define RRT_B3_WAVES 5
+#endif
 constexpr int kBook2Waves = RRT_B2_WAVES;  // book-2 kernels (classes 1-3): launch bound (1 = none)
 constexpr int kBook2Block = RRT_B2_BLOCK;  // and block size; book 3 and unbounded launches use kBlock
+constexpr int kBook3Waves = RRT_B3_WAVES;  // book 3 (class 4): launch bound (1 = none, 512-thread blocks;
+                                           // else kBook2Block-thread blocks)
 // Threads per block of the render launch for a scene (rrt_kernel.hip launch_width): the host sizes
 // the block's LDS (traversal stack, Perlin tables) with it. book2_class: a book-2 scene rendered by
 // kernel classes 1-3 (not book 3); wide_stack: more than 65535 nodes (32-bit stack, kBlock).
-inline int render_block_threads(bool book2_class, bool wide_stack) {
+inline int render_block_threads(bool book2_class, bool wide_stack, bool book3 = false) {
     if (wide_stack) return kBlock;
+    if (book3) return kBook3Waves > 1 ? kBook2Block : kBlock;
     return book2_class && kBook2Waves > 1 ? kBook2Block : kBlock;
 }
 // Per-block LDS budget for staging the scene (BVH nodes + spheres + per-sphere materials)

@@ -30,7 +30,7 @@
 namespace rrt {
 namespace {
 
-// Debug builds only (-DRRT_PHASE_TIMING=1..8, never the shipped library): per-wave phase
+// Debug builds only (-DRRT_PHASE_TIMING=1..9, never the shipped library): per-wave phase
 // statistics written into counter slots 2..4 by the non-counting kernel.
 //   1: s_memtime cycles spent in refill+ray start / traversal loop / shading
 //   2: traversal wave-iterations x 64 / sum of tracing lanes per iteration / outer iterations
@@ -40,6 +40,7 @@ namespace {
 //   6: metal lanes / miss (sky) wave entries x 64 / miss lanes
 //   7: camera-ray wave entries x 64 (after a path ends) / their lanes / disk-loop wave-iterations x 64
 //   8: node-step wave-iterations x 64 / those whose stepping lanes all visit one node x 64 / their lanes
+//   9: noise-texture wave entries x 64 / noise lanes / shade entries x 64
 #ifndef RRT_PHASE_TIMING
 #define RRT_PHASE_TIMING 0
 #endif
@@ -316,6 +317,10 @@ __device__ __forceinline__ float clamped_slope(float s) {
 // 96-VGPR bound (kHoldRa; with ra held it spilled 20 VGPRs and lost 0.4 %, at 4 waves 8.5 %).
 #ifndef RRT_F16_ORDERED_MAX_CLASS
 #define RRT_F16_ORDERED_MAX_CLASS 3
+#endif
+// waves per SIMD of the book-2 classes 1-2 for scenes without noise textures
+#ifndef RRT_B2_NF_WAVES
+#define RRT_B2_NF_WAVES 6
 #endif
 // waves per SIMD of the book-2 media class (3) for scenes read from L2 (0: kBook2Waves)
 #ifndef RRT_B2_MEDIA_GLOBAL_WAVES
@@ -1044,6 +1049,16 @@ __device__ __forceinline__ float rrt_cosf(float xx) {
     return sign < 0.0f ? -y : y;
 }
 
+#ifndef RRT_NOISE_UNROLL
+#define RRT_NOISE_UNROLL 1
+#endif
+#ifndef RRT_PERLIN_LDS_PTR
+#define RRT_PERLIN_LDS_PTR 1
+#endif
+#ifndef RRT_DEBUG_NOISE_FIXED  // debug builds only: a constant-time stand-in (prices the texture; wrong images)
+#define RRT_DEBUG_NOISE_FIXED 0
+#endif
+
 // Rust `f32 as i32` of a floored value: saturating, NaN -> 0.
 __device__ __forceinline__ int floor_i32(float x) {
     const float f = __builtin_floorf(x);
@@ -1053,9 +1068,17 @@ __device__ __forceinline__ int floor_i32(float x) {
     return (int)f;
 }
 
+// The Perlin tables are read through a pointer of type PP: an LDS (address space 3) pointer when
+// the block staged them (ds_read, 32-bit addresses), else the generic one.
+using LdsPerlin = const __attribute__((address_space(3))) GPerlin *;
+
+template <class Q>
+__device__ __forceinline__ V3 gradient(Q randvec, uint32_t idx) { return v3(randvec[idx].x, randvec[idx].y, randvec[idx].z); }
+
 // Perlin::noise (perlin.rs:25-48) + perlin_interp (perlin.rs:79-98), operation order kept:
 // the (i*uu + (1-i)*(1-uu)) factors are exactly uu or 1-uu for i in {0,1}.
-__device__ __forceinline__ float perlin_noise(const GPerlin *__restrict__ pt, V3 p) {
+template <class PP, bool kUnroll = RRT_NOISE_UNROLL>
+__device__ __forceinline__ float perlin_noise(PP pt, V3 p) {
     const float fx = __builtin_floorf(p.x), fy = __builtin_floorf(p.y), fz = __builtin_floorf(p.z);
     const float u = p.x - fx, v = p.y - fy, w = p.z - fz;
     const int i = floor_i32(p.x), j = floor_i32(p.y), k = floor_i32(p.z);
@@ -1067,24 +1090,57 @@ __device__ __forceinline__ float perlin_noise(const GPerlin *__restrict__ pt, V3
     const uint32_t py0 = (pt->perm[(uint32_t)j & 255u] >> 8) & 0xffu, py1 = (pt->perm[(uint32_t)(j + 1) & 255u] >> 8) & 0xffu;
     const uint32_t pz0 = (pt->perm[(uint32_t)k & 255u] >> 16) & 0xffu, pz1 = (pt->perm[(uint32_t)(k + 1) & 255u] >> 16) & 0xffu;
     float accum = 0.0f;
+    if constexpr (!kUnroll) {
 #pragma unroll 1
-    for (int corner = 0; corner < 8; ++corner) {  // (di, dj, dk) in perlin_interp's nested order
-        const int di = corner >> 2, dj = (corner >> 1) & 1, dk = corner & 1;
-        const float4 c = pt->randvec[(di ? px1 : px0) ^ (dj ? py1 : py0) ^ (dk ? pz1 : pz0)];
-        const float wx = u - (float)di, wy = v - (float)dj, wz = w - (float)dk;
+        for (int corner = 0; corner < 8; ++corner) {  // (di, dj, dk) in perlin_interp's nested order
+            const int di = corner >> 2, dj = (corner >> 1) & 1, dk = corner & 1;
+            const V3 c = gradient(pt->randvec, (di ? px1 : px0) ^ (dj ? py1 : py0) ^ (dk ? pz1 : pz0));
+            const float wx = u - (float)di, wy = v - (float)dj, wz = w - (float)dk;
+            const float fi = di ? uu : 1.0f - uu;
+            const float fj = dj ? vv : 1.0f - vv;
+            const float fk = dk ? ww : 1.0f - ww;
+            accum = accum + fi * fj * fk * dot(c, v3(wx, wy, wz));
+        }
+        return accum;
+    }
+    // RRT_NOISE_UNROLL: the corner loop unrolled. The corner offsets are constants (u - 0 = u and
+    // 0 * uu + 1 * (1 - uu) = 1 - uu exactly, as above), each (fi * fj) is formed once per pair
+    // (perlin_interp multiplies left to right: (fi * fj) * fk * dot is the loop's product), and a
+    // face's four gradient reads are independent loads in flight together instead of one round
+    // trip per corner. Same operations on the same values in the same order: bit-identical.
+    const float v1 = v - 1.0f, w1 = w - 1.0f;
+    const float fv0 = 1.0f - vv, fw0 = 1.0f - ww;
+    const uint32_t q00 = py0 ^ pz0, q01 = py0 ^ pz1, q10 = py1 ^ pz0, q11 = py1 ^ pz1;
+#pragma unroll 1
+    for (int di = 0; di < 2; ++di) {  // one x face per pass: four reads in flight, not eight
+        const uint32_t px = di ? px1 : px0;
+        const float wx = di ? u - 1.0f : u;
         const float fi = di ? uu : 1.0f - uu;
-        const float fj = dj ? vv : 1.0f - vv;
-        const float fk = dk ? ww : 1.0f - ww;
-        accum = accum + fi * fj * fk * dot(v3(c.x, c.y, c.z), v3(wx, wy, wz));
+        const V3 c0 = gradient(pt->randvec, px ^ q00), c1 = gradient(pt->randvec, px ^ q01);
+        const V3 c2 = gradient(pt->randvec, px ^ q10), c3 = gradient(pt->randvec, px ^ q11);
+        const float f0 = fi * fv0, f1 = fi * vv;
+        accum = accum + f0 * fw0 * dot(c0, v3(wx, v, w));
+        accum = accum + f0 * ww * dot(c1, v3(wx, v, w1));
+        accum = accum + f1 * fw0 * dot(c2, v3(wx, v1, w));
+        accum = accum + f1 * ww * dot(c3, v3(wx, v1, w1));
     }
     return accum;
 }
 
 // NoiseTexture::value (texture.rs:122-126): 0.5 * (1 + sin(scale * p.z + 10 * turb(p, 7))),
-// turb (perlin.rs:50-62): |sum of weight * noise(p * 2^i)|, weight halving. The octave and
-// corner loops stay rolled: unrolled (56 corner evaluations) they swamp the megakernel's
-// register allocation.
-__device__ __forceinline__ float noise_value(const GPerlin *__restrict__ pt, float scale, V3 p) {
+// turb (perlin.rs:50-62): |sum of weight * noise(p * 2^i)|, weight halving. The octave loop stays
+// rolled: unrolled (56 corner evaluations) it swamps the megakernel's register allocation.
+#ifndef RRT_NOISE_CALL
+#define RRT_NOISE_CALL 1
+#endif
+#if RRT_NOISE_CALL
+#define RRT_NOISE_FN __attribute__((noinline))
+#else
+#define RRT_NOISE_FN __forceinline__
+#endif
+template <class PP>
+__device__ RRT_NOISE_FN float noise_value(PP pt, float scale, V3 p) {
+    if (RRT_DEBUG_NOISE_FIXED) return 0.5f + p.z * 0x1.0p-30f;
     float accum = 0.0f, weight = 1.0f;
     V3 tp = p;
 #pragma unroll 1
@@ -1095,6 +1151,91 @@ __device__ __forceinline__ float noise_value(const GPerlin *__restrict__ pt, flo
     }
     const float turb = __builtin_fabsf(accum);
     return 0.5f * (1.0f + rrt_sinf(scale * p.z + 10.0f * turb));
+}
+// Noise texture `table` at p: a wave-uniform branch on where the block keeps the tables.
+template <class KP>
+__device__ __forceinline__ float noise_at(const KP &P, const GPerlin *perlin, int table, float scale, V3 p) {
+    if (RRT_PERLIN_LDS_PTR && P.perlin_in_lds) return noise_value((LdsPerlin)(perlin + table), scale, p);
+    return noise_value(perlin + table, scale, p);
+}
+
+#ifndef RRT_NOISE_WAVE
+#define RRT_NOISE_WAVE 0
+#endif
+// x from lane (this lane + n) of the same 16-lane row (DPP row_shl:n; 0 past the row's end)
+template <int n>
+__device__ __forceinline__ float row_shl(float x) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x100 | n, 0xf, 0xf, true));
+}
+
+// NoiseTexture::value for the lanes in `want` (a ballot), evaluated by the whole wave together (every lane
+// of the wave must be active). In final_scene a shading pass that meets the noise texture has 3.3
+// such lanes on average, and the per-lane evaluation costs the wave all 7 x 8 corners for them.
+// Here a pass takes up to 8 noise lanes: lane 8k + o (o < 7) evaluates octave o of the k-th one,
+// perlin_noise at p * 2^o (turb's doublings are exact, so that is the value its loop reaches) times
+// weight 2^-o (its halvings, exact too); lane 8k folds the seven terms in octave order by DPP row
+// shifts, ((0 + t0) + t1) + ... + t6, turb's own left fold; the noise lane pulls the sum back and
+// finishes value(). The same operations on the same values: bit-identical to noise_value.
+#ifndef RRT_NOISE_WAVE_MAX  // noise lanes per shading pass the wave evaluates together (above: per lane)
+#define RRT_NOISE_WAVE_MAX 64
+#endif
+#ifndef RRT_NOISE_WAVE_CALL
+#define RRT_NOISE_WAVE_CALL 0
+#endif
+#ifndef RRT_WAVE_NOISE_UNROLL  // the corner loop inside the wave pass (rolled: fewer live registers)
+#define RRT_WAVE_NOISE_UNROLL 0
+#endif
+#if RRT_NOISE_WAVE_CALL
+#define RRT_WAVE_NOISE_FN __attribute__((noinline))
+#else
+#define RRT_WAVE_NOISE_FN __forceinline__
+#endif
+template <class KP>
+__device__ RRT_WAVE_NOISE_FN float wave_noise(const KP &P, const GPerlin *perlin, uint64_t want, V3 p, int table,
+                                              float scale) {
+    const uint32_t lane = __lane_id();
+    const uint32_t slot = lane >> 3, oct = lane & 7u;
+    const uint64_t below = (1ull << lane) - 1ull;
+    float g = 0.0f;
+    for (uint64_t need = want; need != 0;) {
+        // this pass's source lanes: the first (up to) 8 noise lanes, slot k = the k-th
+        uint64_t rest = need;
+        int src = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int b = rest ? __builtin_ctzll(rest) : 0;
+            src = slot == (uint32_t)k ? b : src;
+            rest &= rest - 1ull;
+        }
+        const uint64_t pass = need ^ rest;
+        const uint32_t n_slots = (uint32_t)__popcll(pass);
+        const float qx = __int_as_float(__builtin_amdgcn_ds_bpermute(src << 2, __float_as_int(p.x)));
+        const float qy = __int_as_float(__builtin_amdgcn_ds_bpermute(src << 2, __float_as_int(p.y)));
+        const float qz = __int_as_float(__builtin_amdgcn_ds_bpermute(src << 2, __float_as_int(p.z)));
+        const int tbl = __builtin_amdgcn_ds_bpermute(src << 2, table);
+        float term = 0.0f;
+        if (oct < 7u && slot < n_slots) {
+            const float up = __int_as_float((int)(127u + oct) << 23);    // 2^oct
+            const float down = __int_as_float((int)(127u - oct) << 23);  // 2^-oct
+            const V3 tp = v3(qx * up, qy * up, qz * up);
+            const float nz = (RRT_PERLIN_LDS_PTR && P.perlin_in_lds)
+                                 ? perlin_noise<LdsPerlin, RRT_WAVE_NOISE_UNROLL>((LdsPerlin)(perlin + tbl), tp)
+                                 : perlin_noise<const GPerlin *, RRT_WAVE_NOISE_UNROLL>(perlin + tbl, tp);
+            term = down * nz;
+        }
+        float acc = 0.0f + term;
+        acc = acc + row_shl<1>(term);
+        acc = acc + row_shl<2>(term);
+        acc = acc + row_shl<3>(term);
+        acc = acc + row_shl<4>(term);
+        acc = acc + row_shl<5>(term);
+        acc = acc + row_shl<6>(term);
+        const uint32_t rank = (uint32_t)__popcll(pass & below);
+        const float turb_acc = __int_as_float(__builtin_amdgcn_ds_bpermute((int)(rank << 5), __float_as_int(acc)));
+        if ((pass >> lane) & 1ull) g = 0.5f * (1.0f + rrt_sinf(scale * p.z + 10.0f * __builtin_fabsf(turb_acc)));
+        need = rest;
+    }
+    return g;
 }
 
 // CheckerTexture::value (texture.rs:66-77) with solid even/odd colours.
@@ -1121,13 +1262,14 @@ __device__ __forceinline__ V3 texel(const KParams &P, int tex, float u, float v)
 // After the closest-hit query of the current segment (prim < 0: miss): background, or
 // emission / scatter / RR (camera.rs:182-209). Returns true when the path has ended; a
 // path ending at the sky or an emitter adds T*Le to `sum`.
-template <int kBook2, typename C, class PR>
+template <int kBook2, bool kNoise, typename C, class PR>
 __device__ __forceinline__ bool shade(const KParams &P, const PR &prims, const GMaterial *mtl, PathState &ps,
-                                      float t, int prim, V3 &sum, C &cnt) {
+                                      float t, int prim, V3 &sum, C &cnt, float gnoise, bool gnoise_ok) {
     if constexpr (RRT_PHASE_TIMING == 4) {
         cnt.d0 += wave_slot();
         cnt.d1 += 1;
     }
+    if constexpr (RRT_PHASE_TIMING == 9) cnt.d2 += wave_slot();
     if (prim < 0) {
         if constexpr (RRT_PHASE_TIMING == 6) {
             cnt.d1 += wave_slot();
@@ -1200,8 +1342,13 @@ __device__ __forceinline__ bool shade(const KParams &P, const PR &prims, const G
         } else if (kBook2 > 0 && kind == 5) {  // CheckerTexture at p
             att = checker_even(m.a.w, p) ? v3(m.a.x, m.a.y, m.a.z)
                                          : v3(__int_as_float(m.b.y), __int_as_float(m.b.z), __int_as_float(m.b.w));
-        } else if (kBook2 > 0 && kind == 6) {  // NoiseTexture at p
-            const float g = noise_value(prims.perlin + m.b.z, m.a.w, p);
+        } else if (kBook2 > 0 && kNoise && kind == 6) {  // NoiseTexture at p
+            if constexpr (RRT_PHASE_TIMING == 9) {
+                cnt.d0 += wave_slot();
+                cnt.d1 += 1;
+            }
+            // evaluated by the wave before shading (RRT_NOISE_WAVE: gnoise_ok, wave-uniform), or here
+            const float g = gnoise_ok ? gnoise : noise_at(P, prims.perlin, m.b.z, m.a.w, p);
             att = v3(g, g, g);
         } else {
             att = v3(m.a.x, m.a.y, m.a.z);
@@ -1337,9 +1484,9 @@ __device__ __forceinline__ V3 lights_random(const KParams &P, V3 o, RngState &rn
 // the_rest_of_your_life/camera.rs:184-254 in throughput form. Metal / dielectric keep the
 // book-2 scatter (skip_pdf); Lambertian (cosine pdf) and Isotropic (sphere pdf) sample the
 // mixture 0.5 * lights + 0.5 * material and weight by scattering_pdf / (pdf * rr).
-template <typename C, class PR>
+template <bool kNoise, typename C, class PR>
 __device__ __forceinline__ bool shade_b3(const KParams &P, const PR &prims, const GMaterial *mtl, PathState &ps,
-                                         float t, int prim, V3 &sum, C &cnt) {
+                                         float t, int prim, V3 &sum, C &cnt, float gnoise, bool gnoise_ok) {
     if (prim < 0) {
         sum = add(sum, mul(ps.T, v3(P.background[0], P.background[1], P.background[2])));
         return true;
@@ -1415,8 +1562,8 @@ __device__ __forceinline__ bool shade_b3(const KParams &P, const PR &prims, cons
     } else if (kind == 5) {
         att = checker_even(m.a.w, p) ? v3(m.a.x, m.a.y, m.a.z)
                                      : v3(__int_as_float(m.b.y), __int_as_float(m.b.z), __int_as_float(m.b.w));
-    } else if (kind == 6) {
-        const float g = noise_value(prims.perlin + m.b.z, m.a.w, p);
+    } else if (kNoise && kind == 6) {
+        const float g = gnoise_ok ? gnoise : noise_at(P, prims.perlin, m.b.z, m.a.w, p);
         att = v3(g, g, g);
     } else {
         att = v3(m.a.x, m.a.y, m.a.z);
@@ -1467,7 +1614,26 @@ __device__ __forceinline__ bool shade_b3(const KParams &P, const PR &prims, cons
 }
 
 
-template <bool kLds, bool kCount, typename StackT, bool kWide, int kBook2, int kBlk>
+// The shading step of the scene class: book 3's MIS integrator or the book-1/2 one.
+template <int kBook2, bool kNoise, typename C, class PR>
+__device__ __forceinline__ bool shade_any(const KParams &P, const PR &prims, const GMaterial *mtl, PathState &ps,
+                                          float t, int prim, V3 &sum, C &cnt, float gnoise, bool gnoise_ok) {
+    if constexpr (kBook2 == 4) return shade_b3<kNoise>(P, prims, mtl, ps, t, prim, sum, cnt, gnoise, gnoise_ok);
+    else return shade<kBook2, kNoise>(P, prims, mtl, ps, t, prim, sum, cnt, gnoise, gnoise_ok);
+}
+
+// Debug builds only (-DRRT_TRACE_X/Y/S): one path's segments, printed at shading.
+__device__ __forceinline__ void trace_segment(uint32_t xy, uint32_t s, const PathState &ps, float t, int prim) {
+#ifdef RRT_TRACE_X
+    if ((xy & 0xffffu) == RRT_TRACE_X && (xy >> 16) == RRT_TRACE_Y && s == RRT_TRACE_S)
+        printf("K k=%u o=(%a %a %a) d=(%a %a %a) t=%a prim=%d T=(%a %a %a) rng=%llx\n", ps.k, ps.o.x, ps.o.y, ps.o.z,
+               ps.d.x, ps.d.y, ps.d.z, t, prim, ps.T.x, ps.T.y, ps.T.z, (unsigned long long)rng_key(ps.rng));
+#endif
+}
+
+// kNoise: the scene has Perlin tables (noise textures); false compiles the noise path out (a noise
+// material needs a table: the host checks the index).
+template <bool kLds, bool kCount, typename StackT, bool kWide, int kBook2, int kBlk, bool kNoise>
 __device__ __forceinline__ void render_body(const KParams &P) {
     extern __shared__ uint4 lds_dyn[];
     // LDS layout: [traversal stack: stack_depth x kBlk x StackT, 16-B aligned][nodes][primitives]
@@ -1712,7 +1878,12 @@ __device__ __forceinline__ void render_body(const KParams &P) {
             ph1 += t - tp;
             tp = t;
         }
-        if (has && !need_ray && tr.node < 0) {
+        // Noise kernels evaluate the shading lanes' noise textures with the whole wave between the
+        // closest-hit query and shade (RRT_NOISE_WAVE): the shading block splits around it. Every
+        // lane is active there (the loop leaves on a wave-uniform ballot).
+        constexpr bool kWaveNoise = kNoise && RRT_NOISE_WAVE;
+        const bool shading = has && !need_ray && tr.node < 0;
+        if (shading) {
             need_ray = 1;
             const Prims<kBook2> spr{prims, motion, ps.time, P.quads, P.media, P.n_quads, rng_key(ps.rng) ^ ((uint64_t)ps.k << 32), perlin};
             if constexpr (RRT_LAZY_ROOT && !kCount && Prims<kBook2>::kR2 && !kWide)
@@ -1734,14 +1905,34 @@ __device__ __forceinline__ void render_body(const KParams &P) {
                     }
                 }
             }
-#ifdef RRT_TRACE_X
-            if ((xy & 0xffffu) == RRT_TRACE_X && (xy >> 16) == RRT_TRACE_Y && s == RRT_TRACE_S)
-                printf("K k=%u o=(%a %a %a) d=(%a %a %a) t=%a prim=%d T=(%a %a %a) rng=%llx\n", ps.k, ps.o.x, ps.o.y,
-                       ps.o.z, ps.d.x, ps.d.y, ps.d.z, tr.closest, tr.hit_prim, ps.T.x, ps.T.y, ps.T.z,
-                       (unsigned long long)rng_key(ps.rng));
-#endif
-            if constexpr (kBook2 == 4) seg_done = shade_b3(P, spr, mtl, ps, tr.closest, tr.hit_prim, sum, cnt) ? 1u : 0u;
-            else seg_done = shade<kBook2>(P, spr, mtl, ps, tr.closest, tr.hit_prim, sum, cnt) ? 1u : 0u;
+            if constexpr (!kWaveNoise) {
+                trace_segment(xy, s, ps, tr.closest, tr.hit_prim);
+                seg_done = shade_any<kBook2, kNoise>(P, spr, mtl, ps, tr.closest, tr.hit_prim, sum, cnt, 0.0f, false) ? 1u : 0u;
+            }
+        }
+        if constexpr (kWaveNoise) {
+            bool want = false;
+            int tbl = 0;
+            float scale = 0.0f;
+            if (shading && tr.hit_prim >= 0) {
+                const GMaterial &hm = mtl[tr.hit_prim];
+                want = hm.b.x == 6;
+                tbl = hm.b.z;
+                scale = hm.a.w;
+            }
+            const V3 ph = v3(__builtin_fmaf(ps.d.x, tr.closest, ps.o.x), __builtin_fmaf(ps.d.y, tr.closest, ps.o.y),
+                             __builtin_fmaf(ps.d.z, tr.closest, ps.o.z));  // shade's Ray::at
+            // one wave pass for up to RRT_NOISE_WAVE_MAX noise lanes; more are evaluated per lane
+            // in shade (perlin_spheres: ~35 per shading pass; final_scene: 3.3)
+            const uint64_t nm = __ballot(want);
+            const bool gnoise_ok = nm != 0 && (uint32_t)__popcll(nm) <= RRT_NOISE_WAVE_MAX;
+            float gnoise = 0.0f;
+            if (gnoise_ok) gnoise = wave_noise(P, perlin, nm, ph, tbl, scale);
+            if (shading) {
+                const Prims<kBook2> spr{prims, motion, ps.time, P.quads, P.media, P.n_quads, rng_key(ps.rng) ^ ((uint64_t)ps.k << 32), perlin};
+                trace_segment(xy, s, ps, tr.closest, tr.hit_prim);
+                seg_done = shade_any<kBook2, kNoise>(P, spr, mtl, ps, tr.closest, tr.hit_prim, sum, cnt, gnoise, gnoise_ok) ? 1u : 0u;
+            }
         }
         w_paths += (uint32_t)__popcll(__ballot(seg_done));
         if (seg_done) {  // pixel_color += ray_color(..) (camera.rs:73-76): already in `sum`
@@ -1772,7 +1963,7 @@ __device__ __forceinline__ void render_body(const KParams &P) {
         }
         if constexpr (RRT_PHASE_TIMING == 1) ph2 += __builtin_amdgcn_s_memtime() - tp;
     }
-    if constexpr (RRT_PHASE_TIMING >= 3 && RRT_PHASE_TIMING <= 7 && !kCount) {
+    if constexpr (((RRT_PHASE_TIMING >= 3 && RRT_PHASE_TIMING <= 7) || RRT_PHASE_TIMING == 9) && !kCount) {
         ph0 = wave_sum_u32(cnt.d0);
         ph1 = wave_sum_u32(cnt.d1);
         ph2 = wave_sum_u32(cnt.d2);
@@ -1804,9 +1995,9 @@ __device__ __forceinline__ void render_body(const KParams &P) {
     }
 }
 
-template <bool kLds, bool kCount, typename StackT, bool kWide, int kWaves, int kBook2, int kBlk>
+template <bool kLds, bool kCount, typename StackT, bool kWide, int kWaves, int kBook2, int kBlk, bool kNoise>
 __global__ __launch_bounds__(kBlk, kWaves) void rrt_render(KParams P) {
-    render_body<kLds, kCount, StackT, kWide, kBook2, kBlk>(P);
+    render_body<kLds, kCount, StackT, kWide, kBook2, kBlk, kNoise>(P);
 }
 
 // The pass's chunk sums into accum, continuing the left fold over chunks in order: the first
@@ -1874,16 +2065,20 @@ __global__ __launch_bounds__(256) void rrt_quantize(const float4 *__restrict__ a
     }
 }
 
-template <bool kLds, typename StackT, bool kWide, int kBook2, int kWaves = 1, int kBlk = kBlock>
+template <bool kLds, typename StackT, bool kWide, int kBook2, int kWaves = 1, int kBlk = kBlock, int kWavesNF = kWaves>
 hipError_t launch_variant(const KParams &p, bool count, hipStream_t stream) {
+    // Book 2/3: a noise-free scene runs a kernel without the noise path (the counting twin and the
+    // 32-bit-stack kernels keep it: one instantiation each serves both), at kWavesNF waves per SIMD.
+    constexpr bool kNoiseFree = kBook2 > 0 && sizeof(StackT) == 2;
     if (p.n_units == 0) return hipSuccess;
     size_t lds = ((size_t)p.stack_depth * kBlk * sizeof(StackT) + 15u) / 16u * 16u;
     if (kLds)
         lds += (size_t)p.n_nodes * (kWide ? sizeof(GNode4) : sizeof(GNode)) +  // LDS BVH2 = GNode
                (size_t)p.n_prims * (kPrimBytes + (kBook2 > 0 ? kMotionBytes : 0));
     if (kBook2 > 0 && p.perlin_in_lds) lds += (size_t)p.n_perlin * sizeof(GPerlin);
-    auto kernel = count ? rrt_render<kLds, true, StackT, kWide, kWaves, kBook2, kBlk>
-                        : rrt_render<kLds, false, StackT, kWide, kWaves, kBook2, kBlk>;
+    auto kernel = count                       ? rrt_render<kLds, true, StackT, kWide, kWaves, kBook2, kBlk, (kBook2 > 0)>
+                  : !kNoiseFree || p.n_perlin ? rrt_render<kLds, false, StackT, kWide, kWaves, kBook2, kBlk, (kBook2 > 0)>
+                                              : rrt_render<kLds, false, StackT, kWide, kWavesNF, kBook2, kBlk, false>;
     // Persistent grid: as many blocks as can be resident (occupancy at this LDS size), capped
     // by the work; the queue counter is zeroed on the stream before the launch.
     int per_cu = 0;
@@ -1917,9 +2112,17 @@ hipError_t launch_width(const KParams &p, bool count, hipStream_t stream) {
         // -21 ... +9 %). Book 3 (class 4, the light-list pdfs) keeps the unbounded 512: -8 % at 5.
         // Class 3 (media: final_scene, cornell_smoke) read from L2: RRT_B2_MEDIA_GLOBAL_WAVES.
         constexpr int kGW = (kBook2 == 3 && RRT_B2_MEDIA_GLOBAL_WAVES > 0) ? RRT_B2_MEDIA_GLOBAL_WAVES : kBook2Waves;
+        // Classes 1-2 without noise textures need ~88 VGPRs and run at RRT_B2_NF_WAVES (6: bouncing
+        // spheres +6.4 %, checkered spheres +4 %, quads +3.3 %, cornell_box +6.8 % same-box over 5;
+        // the media class and the noise kernels lose 8-15 % at 6 and stay at 5).
+        constexpr int kNF = kBook2 <= 2 ? RRT_B2_NF_WAVES : kBook2Waves;
+        constexpr int kGNF = kBook2 <= 2 ? RRT_B2_NF_WAVES : kGW;
         if constexpr (kBook2 != 4 && kBook2Waves > 1)
-            return p.scene_in_lds ? launch_variant<true, uint16_t, kWide, kBook2, kBook2Waves, kBook2Block>(p, count, stream)
-                                  : launch_variant<false, uint16_t, kWide, kBook2, kGW, kBook2Block>(p, count, stream);
+            return p.scene_in_lds ? launch_variant<true, uint16_t, kWide, kBook2, kBook2Waves, kBook2Block, kNF>(p, count, stream)
+                                  : launch_variant<false, uint16_t, kWide, kBook2, kGW, kBook2Block, kGNF>(p, count, stream);
+        if constexpr (kBook2 == 4 && kBook3Waves > 1)
+            return p.scene_in_lds ? launch_variant<true, uint16_t, kWide, kBook2, kBook3Waves, kBook2Block>(p, count, stream)
+                                  : launch_variant<false, uint16_t, kWide, kBook2, kBook3Waves, kBook2Block>(p, count, stream);
         return p.scene_in_lds ? launch_variant<true, uint16_t, kWide, kBook2>(p, count, stream)
                               : launch_variant<false, uint16_t, kWide, kBook2>(p, count, stream);
     } else {

@@ -85,6 +85,20 @@ def test_cornell_smoke_and_final_scene_larger_frames_kbvh():
         assert_bit_exact(gpu, ref, sc.spp)
 
 
+def test_noise_texture_scenes_larger_frames_kbvh():
+    # Perlin noise (perlin_spheres: ~35 noise lanes per shading pass, evaluated per lane; simple_light
+    # with its quad light) and final_scene's marble sphere (3.3 noise lanes per pass, evaluated by
+    # the whole wave: rrt_kernel.hip wave_noise): both paths occur in each frame, bit-exact
+    for scene, kw in ((4, dict(image_width=192, samples_per_pixel=8, max_depth=20)),
+                      (6, dict(image_width=192, samples_per_pixel=8, max_depth=20)),
+                      (9, dict(image_width=96, samples_per_pixel=8, max_depth=20))):
+        sc = rrt.next_week_scene(scene, kw)
+        gpu = rrt.render(sc)
+        nodes, order, info = build_bvh(sc)
+        ref, _, _ = oracle.render_kbvh(sc, nodes, order, info, threads=16)
+        assert_bit_exact(gpu, ref, sc.spp)
+
+
 def test_medium_box_transmittance_gpu():
     # Beer-Lambert through a black-phase box medium, bit-exact with the oracle and within
     # statistics of exp(-density * 2) on the axis (tests/test_book2.py builds the scene)

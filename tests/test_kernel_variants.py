@@ -1,6 +1,6 @@
 """Every compile-time arm left in the kernel sources is the shipped default or compiled here.
 
-rrt_kernel.hip keeps only debug builds (-DRRT_PHASE_TIMING=1..4: per-wave phase statistics,
+rrt_kernel.hip keeps only debug builds (-DRRT_PHASE_TIMING=1..9: per-wave phase statistics,
 -DRRT_TRACE_X/Y/S: a printf trace of one path) and numeric tuning knobs (launch shapes, issue
 priorities, the work-unit tile). Rejected variants are deleted (DESIGN.md §5 keeps their
 measurements). Each non-default arm is type-checked for gfx950 here (hipcc -fsyntax-only
@@ -25,6 +25,13 @@ VARIANTS = {
     "phase6": ["-DRRT_PHASE_TIMING=6"],
     "phase7": ["-DRRT_PHASE_TIMING=7"],
     "phase8": ["-DRRT_PHASE_TIMING=8"],
+    "phase9": ["-DRRT_PHASE_TIMING=9"],
+    # the noise texture's generic-pointer reads, rolled corner loop, inlined evaluation; and the
+    # debug stand-in that prices the texture
+    "noise": ["-DRRT_PERLIN_LDS_PTR=0", "-DRRT_NOISE_UNROLL=0", "-DRRT_NOISE_CALL=0", "-DRRT_DEBUG_NOISE_FIXED=1"],
+    # noise textures evaluated per lane only; the wave pass as a call, unrolled, for every count
+    "noise_per_lane": ["-DRRT_NOISE_WAVE=0"],
+    "noise_wave": ["-DRRT_NOISE_WAVE_CALL=1", "-DRRT_WAVE_NOISE_UNROLL=1", "-DRRT_NOISE_WAVE_MAX=64"],
     "trace": ["-DRRT_TRACE_X=3", "-DRRT_TRACE_Y=4", "-DRRT_TRACE_S=5"],
     # lazy exact roots in the leaf loop (bit-exact, measured and left off: DESIGN.md §4)
     "lazy_root": ["-DRRT_LAZY_ROOT=1", "-DRRT_F64_LAZY=0", "-DRRT_F64_SQRT=0", "-DRRT_F16_ORDERED=0"],
