@@ -1545,10 +1545,16 @@ static int32_t scene_create(const RrtCamera *cam, const RrtSphere *spheres, uint
     }
     // traversal exit / leaf batch thresholds (x/256 of the live lanes), same-box sweeps against 32/32:
     // book-1 LDS scenes 56/56 (C2 +0.6 %, C4 +0.25 %); L2 scenes 64/48 (C5 +2.0 %, final_scene and
-    // bouncing spheres +4 %); book-2/3 LDS scenes keep 32/32 (56/56: cornell_box +5 %, but
-    // cornell_smoke -10 %, perlin_spheres -4 %)
-    p.trav_frac = p.scene_in_lds ? (book2 ? 32 : 56) : 64;
-    p.leaf_frac = p.scene_in_lds ? (book2 ? 32 : 56) : 48;
+    // bouncing spheres +4 %). Book-2/3 LDS scenes by kernel class (round 6, after the class launch
+    // shapes): spheres only 32/32; quads 48/48 (cornell_box +3.6 %); media 24/24 (cornell_smoke
+    // +3.2 %); book 3 48/32 (+1.4 %) (profiles/r6_thresholds_sweep.log)
+    {
+        const int cls = book3 ? 4 : n_media ? 3 : n_quads ? 2 : 1;
+        const uint32_t b2_trav = cls == 2 || cls == 4 ? 48u : cls == 3 ? 24u : 32u;
+        const uint32_t b2_leaf = cls == 2 ? 48u : cls == 3 ? 24u : 32u;
+        p.trav_frac = p.scene_in_lds ? (book2 ? b2_trav : 56u) : 64u;
+        p.leaf_frac = p.scene_in_lds ? (book2 ? b2_leaf : 56u) : 48u;
+    }
     p.min_waves = 6;
     p.chunk = accum_chunk();
     {

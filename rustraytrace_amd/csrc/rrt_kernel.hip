@@ -318,6 +318,11 @@ __device__ __forceinline__ float clamped_slope(float s) {
 #ifndef RRT_F16_ORDERED_MAX_CLASS
 #define RRT_F16_ORDERED_MAX_CLASS 3
 #endif
+// waves per SIMD of the book-1 diffuse-only class (C4) staged in LDS (6: 512-thread blocks); its
+// small scenes leave LDS for 8 blocks of 256: C4 +3.1 % at 256 x 8, +2.4 % at 256 x 7 (round 6)
+#ifndef RRT_B1D_WAVES
+#define RRT_B1D_WAVES 8
+#endif
 // waves per SIMD of the book-2 classes 1-2 for scenes without noise textures
 #ifndef RRT_B2_NF_WAVES
 #define RRT_B2_NF_WAVES 6
@@ -2126,6 +2131,10 @@ hipError_t launch_width(const KParams &p, bool count, hipStream_t stream) {
         return p.scene_in_lds ? launch_variant<true, uint16_t, kWide, kBook2>(p, count, stream)
                               : launch_variant<false, uint16_t, kWide, kBook2>(p, count, stream);
     } else {
+        // the diffuse-only class (C4) staged in LDS: RRT_B1D_WAVES > 6 runs 256-thread blocks
+        if constexpr (kBook2 == kBook1Diffuse && RRT_B1D_WAVES > 6)
+            if (!kWide && p.scene_in_lds && p.min_waves >= 6)
+                return launch_variant<true, uint16_t, kWide, kBook2, RRT_B1D_WAVES, kGlobalBlock>(p, count, stream);
         if (!kWide && p.scene_in_lds && p.min_waves >= 6)
             return launch_variant<true, uint16_t, kWide, kBook2, kWavesPerSimd>(p, count, stream);
         // Scenes read from L2 (C5) hold only the stack in LDS: 256-thread blocks at 7 waves/SIMD
