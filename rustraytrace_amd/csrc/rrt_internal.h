@@ -274,7 +274,10 @@ constexpr uint32_t kTileW = RRT_TILE_W, kTileH = 64u / RRT_TILE_W;
 constexpr int kBlock = RRT_BLOCK;          // threads per block (4 or 8 waves)
 constexpr int kWavesPerSimd = RRT_WAVES;   // launch-bounds occupancy target of the main variant
 constexpr int kGlobalBlock = 256;         // book-1 kernels whose scene is read from L2: block size
-constexpr int kGlobalWaves = 7;           // and waves per SIMD (72 VGPRs)
+#ifndef RRT_B1_GLOBAL_WAVES
+#define RRT_B1_GLOBAL_WAVES 7
+#endif
+constexpr int kGlobalWaves = RRT_B1_GLOBAL_WAVES;  // and waves per SIMD (7: 72 VGPRs)
 #ifndef RRT_B2_WAVES
 #define RRT_B2_WAVES 5
 #endif

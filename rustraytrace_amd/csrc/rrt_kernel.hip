@@ -318,6 +318,16 @@ __device__ __forceinline__ float clamped_slope(float s) {
 #ifndef RRT_F16_ORDERED_MAX_CLASS
 #define RRT_F16_ORDERED_MAX_CLASS 3
 #endif
+// waves per SIMD and block size of the book-1 untextured class (C2) staged in LDS (6: 512 threads).
+// Each block stages its own scene copy (C2: 37 KB), which held C2 at three 512-thread blocks per CU;
+// two 1024-thread blocks hold two copies and reach 8 waves/SIMD (64 VGPRs, 28 spilled): C2 +4.6 %
+// same-box (round 6). 896 x 7 loses 24 %: 14-wave blocks do not pack onto 4 SIMDs twice.
+#ifndef RRT_B1U_WAVES
+#define RRT_B1U_WAVES 8
+#endif
+#ifndef RRT_B1U_BLOCK
+#define RRT_B1U_BLOCK 1024
+#endif
 // waves per SIMD of the book-1 diffuse-only class (C4) staged in LDS (6: 512-thread blocks); its
 // small scenes leave LDS for 8 blocks of 256: C4 +3.1 % at 256 x 8, +2.4 % at 256 x 7 (round 6)
 #ifndef RRT_B1D_WAVES
@@ -2131,6 +2141,10 @@ hipError_t launch_width(const KParams &p, bool count, hipStream_t stream) {
         return p.scene_in_lds ? launch_variant<true, uint16_t, kWide, kBook2>(p, count, stream)
                               : launch_variant<false, uint16_t, kWide, kBook2>(p, count, stream);
     } else {
+        // C2's class staged in LDS: RRT_B1U_WAVES > 6 runs RRT_B1U_BLOCK-thread blocks (fewer scene copies)
+        if constexpr (kBook2 == kBook1Untextured && RRT_B1U_WAVES > 6)
+            if (!kWide && p.scene_in_lds && p.min_waves >= 6)
+                return launch_variant<true, uint16_t, kWide, kBook2, RRT_B1U_WAVES, RRT_B1U_BLOCK>(p, count, stream);
         // the diffuse-only class (C4) staged in LDS: RRT_B1D_WAVES > 6 runs 256-thread blocks
         if constexpr (kBook2 == kBook1Diffuse && RRT_B1D_WAVES > 6)
             if (!kWide && p.scene_in_lds && p.min_waves >= 6)
