@@ -35,6 +35,9 @@ VARIANTS = {
     "trace": ["-DRRT_TRACE_X=3", "-DRRT_TRACE_Y=4", "-DRRT_TRACE_S=5"],
     # lazy exact roots in the leaf loop (bit-exact, measured and left off: DESIGN.md §4)
     "lazy_root": ["-DRRT_LAZY_ROOT=1", "-DRRT_F64_LAZY=0", "-DRRT_F64_SQRT=0", "-DRRT_F16_ORDERED=0"],
+    # round-6 launch shapes back at their earlier values
+    "launch_knobs": ["-DRRT_B1U_WAVES=6", "-DRRT_B1D_WAVES=6", "-DRRT_B3_WAVES=1", "-DRRT_B2_NF_WAVES=5",
+                     "-DRRT_B1_GLOBAL_WAVES=6"],
     "knobs": ["-DRRT_BLOCK=256", "-DRRT_WAVES=4", "-DRRT_TILE_W=16", "-DRRT_B2_WAVES=1", "-DRRT_B2_BLOCK=512",
               "-DRRT_PRIO_REFILL=0", "-DRRT_PRIO_NODE=0", "-DRRT_PRIO_LEAF=0", "-DRRT_PRIO_SHADE=0"],
     # rrt_books64.hip: the per-ray reciprocal root division, one class for every scene, f32 nodes in
