@@ -1629,6 +1629,22 @@ __device__ __forceinline__ bool shade_b3(const KParams &P, const PR &prims, cons
 }
 
 
+#ifndef RRT_LEAN_8W
+#define RRT_LEAN_8W 0
+#endif
+#ifndef RRT_PKEY_HOLD  // with RRT_LEAN_8W: 0 = the 8-wave class forms the pixel key per path
+#define RRT_PKEY_HOLD 0
+#endif
+#ifndef RRT_SUM_LDS  // with RRT_LEAN_8W: 1 = the 8-wave class keeps its radiance sum in LDS
+#define RRT_SUM_LDS 1
+#endif
+// This lane's radiance-sum slot in LDS (12-B stride: lanes fall on distinct banks).
+template <int kBlk>
+__device__ __forceinline__ V3 *sum_slot() {
+    __shared__ V3 slots[kBlk];
+    return &slots[threadIdx.x];
+}
+
 // The shading step of the scene class: book 3's MIS integrator or the book-1/2 one.
 template <int kBook2, bool kNoise, typename C, class PR>
 __device__ __forceinline__ bool shade_any(const KParams &P, const PR &prims, const GMaterial *mtl, PathState &ps,
@@ -1712,8 +1728,16 @@ __device__ __forceinline__ void render_body(const KParams &P) {
     bool q_open = true;   // wave-uniform: the queue may still hold units
     // lane's unit: global pixel (x | y << 16), next sample s, end of its sample chunk s_hi
     uint32_t xy = 0, s = 0, s_hi = 0;
+    // The 8-wave class (C2's, 1024-thread blocks, 64 VGPRs) frees registers: its pixel key is formed
+    // again at each path start instead of held, and its radiance sum lives in LDS (RRT_LEAN_8W).
+    constexpr bool kLean = RRT_LEAN_8W && kLds && kBook2 == kBook1Untextured && kBlk >= 1024;
     uint64_t pkey = 0;  // the unit's pixel key (one splitmix64 per unit instead of per path)
-    V3 sum = v3(0.0f, 0.0f, 0.0f);
+    V3 sum_reg = v3(0.0f, 0.0f, 0.0f);
+    V3 *sum_ptr;
+    if constexpr (kLean && RRT_SUM_LDS) sum_ptr = sum_slot<kBlk>();
+    else sum_ptr = &sum_reg;
+    V3 &sum = *sum_ptr;
+    sum = v3(0.0f, 0.0f, 0.0f);
     PathState ps;
     Trav tr;
     // A lane is in the tree while tr.node >= 0 (or, inside the BVH2 loop, while it holds postponed
@@ -1791,8 +1815,9 @@ __device__ __forceinline__ void render_body(const KParams &P) {
                         s = Q.sample_begin + chunk_first(Q, chunk);
                         s_hi = min(s + (chunk < Q.n_big ? Q.chunk : Q.chunk_small), Q.sample_end);
                         sum = v3(0.0f, 0.0f, 0.0f);
-                        pkey = pixel_key(Q, x, y);
-                        ps.rng = path_rng_k(pkey, s);
+                        const uint64_t key = pixel_key(Q, x, y);
+                        if constexpr (!(kLean && !RRT_PKEY_HOLD)) pkey = key;
+                        ps.rng = path_rng_k(key, s);
                         camera_ray<kBook2 == 4>(P, x, y, s, ps, cnt);
                         need_ray = 1;
                         has = 1;
@@ -1954,7 +1979,8 @@ __device__ __forceinline__ void render_body(const KParams &P) {
             ++s;
             const uint32_t x = xy & 0xffffu, y = xy >> 16;
             if (s < s_hi) {
-                ps.rng = path_rng_k(pkey, s);
+                if constexpr (kLean && !RRT_PKEY_HOLD) ps.rng = path_rng_k(pixel_key(*kernarg_params(), x, y), s);
+                else ps.rng = path_rng_k(pkey, s);
                 if constexpr (RRT_PHASE_TIMING == 7) {
                     cnt.d0 += wave_slot();
                     cnt.d1 += 1;

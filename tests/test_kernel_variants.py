@@ -35,6 +35,8 @@ VARIANTS = {
     "trace": ["-DRRT_TRACE_X=3", "-DRRT_TRACE_Y=4", "-DRRT_TRACE_S=5"],
     # lazy exact roots in the leaf loop (bit-exact, measured and left off: DESIGN.md §4)
     "lazy_root": ["-DRRT_LAZY_ROOT=1", "-DRRT_F64_LAZY=0", "-DRRT_F64_SQRT=0", "-DRRT_F16_ORDERED=0"],
+    # the 8-wave class freeing registers (pixel key per path, radiance sum in LDS)
+    "lean_8w": ["-DRRT_LEAN_8W=1"],
     # round-6 launch shapes back at their earlier values
     "launch_knobs": ["-DRRT_B1U_WAVES=6", "-DRRT_B1D_WAVES=6", "-DRRT_B3_WAVES=1", "-DRRT_B2_NF_WAVES=5",
                      "-DRRT_B1_GLOBAL_WAVES=6"],
