@@ -1776,7 +1776,7 @@ __device__ __forceinline__ void render_body(const KParams &P) {
             const uint32_t xq = (pool_base >> 6) & (kQueues - 1u);
             uint32_t k = 0;
             if (lane == 0) k = atomicAdd(P.unit_counter + 32u * xq, 1u);
-            const uint32_t base = (__shfl(k, 0, 64) * kQueues + xq) * 64u;
+            const uint32_t base = ((uint32_t)__builtin_amdgcn_readlane((int)k, 0) * kQueues + xq) * 64u;
             if (base >= P.n_units) {
                 q_open = false;
             } else {
@@ -1786,7 +1786,8 @@ __device__ __forceinline__ void render_body(const KParams &P) {
         }
         if (idle != 0 && pool_left != 0) {
             const uint32_t n = min((uint32_t)__popcll(idle), pool_left);
-            const uint32_t r = (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
+            // idle lanes below this one (v_mbcnt: no 64-bit lane mask held across the loop)
+            const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
             if (!has && r < n) {
                 const uint32_t u = pool_base + r;
                 {
